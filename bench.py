@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""bench.py — BFT instance-rounds/s of the batched PBFT core on MI355X (BASELINE.json metric).
+
+One step = one full run of the metric workload on every rank: cfg3 =
+16,384 independent consensus-rs clusters of N=64 validators with f=21 equivocating Byzantine
+validators, 100 heights, seeded synthetic schedule — the consensus kernel plus the block-hash
+kernel, inputs resident on the GPU, results left in HBM. Ranks shard instances (rank r runs ids
+[r*I, (r+1)*I)), no data-path collective; the per-run statistics are all-reduced over RCCL.
+
+Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the roofline model.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "consensus-rs_amd"))
+
+METRIC = "BFT instance-rounds/sec (whole node), N=64 f=21, 1/2/4/8 GPUs; bit-exact"
+VALU_PEAK = 256 * 4 * 32 * 2.4e9        # lane-ops/s (MI355X_MICROARCH.md chip table)
+HBM_PEAK = 8.0e12                       # B/s spec
+
+
+def consensus_ops_per_view(n: int) -> int:
+    """Algorithmic 32-bit lane-ops of one instance-round in the consensus kernel:
+    4 delivery phases x N receivers x (AND + 2 popcount per 64-bit word + compare/update)."""
+    return 4 * n * (3 * ((n + 63) // 64) + 8)
+
+
+HEADER_HASH_OPS = 14_976                # 2 Keccak-f[1600] x 24 rounds x 156 64-bit ops x 2
+
+
+def cpu_baseline(cfg, sample: int, threads: int):
+    """The C oracle (oracle/, a scalar restatement of the reference handlers) timed on this
+    host's cores over a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    r = O.run(cfg, 0, sample, threads=threads)
+    views = int(r["views"].sum())
+    secs = r["seconds"]
+    return dict(value=views / secs, unit="instance-rounds/s", cores=threads, kind="port",
+                sample=f"{sample} cfg3 instances ({views} instance-rounds) on {threads} threads, "
+                       f"{secs:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--instances", type=int, default=16_384, help="instances per GPU")
+    ap.add_argument("--heights", type=int, default=100)
+    ap.add_argument("--cpu-sample", type=int, default=768)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from bftsim.configs import cfg3
+    from bftsim.runtime import Simulator
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    cfg = cfg3(heights=args.heights)
+    sim = Simulator(cfg, device=local)
+    I = args.instances
+    sim.prepare(I)
+    first = rank * I
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    for _ in range(args.warmup):
+        sim.launch(first, stream)
+    torch.cuda.synchronize(dev)
+
+    # work per step: instance-rounds of this shard (identical every step), summed over ranks
+    st = sim.stats()
+    totals = torch.tensor([st["views"], st["committed_heights"], st["instances"],
+                           st["flagged"][0], st["flagged"][4]], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(totals)           # RCCL over xGMI
+    views_all, heights_all, inst_all, safety_all, timeout_all = [int(x) for x in totals.tolist()]
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    cms_sum = hms_sum = 0.0
+    for _ in range(args.steps):
+        sim.launch(first, stream)
+        c, h = sim.kernel_ms()
+        cms_sum += c
+        hms_sum += h
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    tmax = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    dt = float(tmax.item())
+
+    ms_step = 1000.0 * dt / args.steps
+    value = views_all * args.steps / dt
+    cms = cms_sum / args.steps
+    hms = hms_sum / args.steps
+
+    if rank == 0:
+        views_rank = st["views"]
+        # dominant kernel by device time
+        c_ops = consensus_ops_per_view(cfg.n) * views_rank
+        h_ops = HEADER_HASH_OPS * st["committed_heights"]
+        if cms >= hms:
+            dom, ops, ms = "bft_consensus_kernel", c_ops, cms
+        else:
+            dom, ops, ms = "bft_hash_kernel", h_ops, hms
+        achieved = ops / (ms / 1e3) / 1e12
+        peak = VALU_PEAK / 1e12
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "instance-rounds/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (seeded Philox schedule, SPEC.md)",
+            "config": {
+                "workload": f"cfg3: {I} instances per GPU, N=64, f=21 equivocating, "
+                            f"{args.heights} heights",
+                "instances_per_gpu": I, "n_validators": cfg.n, "byzantine": cfg.byz_count,
+                "heights": args.heights, "parallelism": f"instance-sharded x{world}",
+                "instance_rounds_per_step": views_all,
+                "committed_heights_per_step": heights_all,
+                "safety_violations": safety_all, "timeouts": timeout_all,
+            },
+            "roofline": {
+                "bound": "valu", "kernel": dom, "achieved": achieved, "peak": peak,
+                "unit": "Tops/s", "frac": achieved / peak, "traffic": None,
+                "kernel_ms": {"bft_consensus_kernel": cms, "bft_hash_kernel": hms},
+                "ops_model": "consensus 4*N*(3*ceil(N/64)+8) lane-ops per instance-round; "
+                             "hash 14976 lane-ops per header (SURVEY.md 8d)",
+            },
+        }
+        if not args.no_cpu:
+            try:
+                threads = min(16, os.cpu_count() or 1)
+                out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample, threads)
+            except Exception as e:  # the baseline is reported, never the target
+                out["cpu_baseline"] = {"error": str(e)}
+        print(json.dumps(out), flush=True)
+    sim.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

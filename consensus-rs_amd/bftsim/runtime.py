@@ -1,0 +1,119 @@
+"""Host binding of libbftsim (the HIP path). Mirrors the reference's engine surface:
+`Simulator` stands for one `create_bft_engine` per instance (src/consensus/consensus.rs:42-60),
+batched. There is no CPU fallback: if the HIP library is missing this raises."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import _abi
+from .configs import BftConfig
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "build", "libbftsim.so")
+
+_lib = None
+
+
+class BftsimError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise BftsimError(f"libbftsim.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        L.bftsim_create.argtypes = [ctypes.POINTER(_abi.CConfig), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.bftsim_destroy.argtypes = [ctypes.c_void_p]
+        L.bftsim_last_error.argtypes = [ctypes.c_void_p]
+        L.bftsim_last_error.restype = ctypes.c_char_p
+        L.bftsim_run.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(_abi.CResult)]
+        L.bftsim_prepare.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.bftsim_launch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        L.bftsim_sync.argtypes = [ctypes.c_void_p]
+        L.bftsim_fetch.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.CResult)]
+        L.bftsim_stats_get.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.CStats)]
+        L.bftsim_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
+                                            ctypes.POINTER(ctypes.c_float)]
+        L.bftsim_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
+        L.bftsim_two_thirds_majority.restype = ctypes.c_uint32
+        L.bftsim_seed_from_hash.restype = ctypes.c_uint32
+        L.bftsim_calc_proposer.restype = ctypes.c_uint32
+        L.bftsim_calc_proposer.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint64]
+        L.bftsim_keccak256.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.bftsim_genesis_hash.argtypes = [ctypes.POINTER(_abi.CConfig), ctypes.c_void_p]
+        L.bftsim_view_cmp.argtypes = [ctypes.c_uint64] * 4
+        _lib = L
+    return _lib
+
+
+def _check(h, rc, what):
+    if rc != 0:
+        msg = lib().bftsim_last_error(h).decode() if h else ""
+        raise BftsimError(f"{what} failed ({rc}): {msg}")
+
+
+class Simulator:
+    """Runs many independent seeded consensus-rs clusters of one configuration on one GPU."""
+
+    def __init__(self, cfg: BftConfig, device: int = 0):
+        self.cfg = cfg
+        self._c, self._keep = _abi.to_cconfig(cfg)
+        h = ctypes.c_void_p()
+        rc = lib().bftsim_create(ctypes.byref(self._c), device, ctypes.byref(h))
+        self.h = h.value
+        _check(self.h, rc, "bftsim_create")
+        self.n_prepared = 0
+
+    def close(self):
+        if self.h:
+            lib().bftsim_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, first: int, n: int, trace_ticks: int = 0):
+        r, arrs = _abi.alloc_result(n, self.cfg.heights)
+        tr = None
+        if trace_ticks:
+            tr = np.zeros(n * trace_ticks * self.cfg.n, np.uint64)
+            _check(self.h, lib().bftsim_set_trace(self.h, tr.ctypes.data, trace_ticks), "set_trace")
+        try:
+            _check(self.h, lib().bftsim_run(self.h, first, n, ctypes.byref(r)), "bftsim_run")
+        finally:
+            if trace_ticks:
+                lib().bftsim_set_trace(self.h, None, 0)
+        arrs = _abi.shape_result(arrs, n, self.cfg.heights)
+        if tr is not None:
+            arrs["trace"] = tr.reshape(n, trace_ticks, self.cfg.n)
+        return arrs
+
+    # device-resident path (bench)
+    def prepare(self, n: int):
+        _check(self.h, lib().bftsim_prepare(self.h, n), "bftsim_prepare")
+        self.n_prepared = n
+
+    def launch(self, first: int, stream: int = 0):
+        _check(self.h, lib().bftsim_launch(self.h, first, ctypes.c_void_p(stream)), "bftsim_launch")
+
+    def sync(self):
+        _check(self.h, lib().bftsim_sync(self.h), "bftsim_sync")
+
+    def kernel_ms(self):
+        a, b = ctypes.c_float(), ctypes.c_float()
+        _check(self.h, lib().bftsim_last_kernel_ms(self.h, ctypes.byref(a), ctypes.byref(b)), "kernel_ms")
+        return a.value, b.value
+
+    def stats(self):
+        s = _abi.CStats()
+        _check(self.h, lib().bftsim_stats_get(self.h, ctypes.byref(s)), "bftsim_stats_get")
+        return dict(instances=s.instances, committed_heights=s.committed_heights, views=s.views,
+                    ticks=s.ticks, flagged=list(s.flagged), round_hist=list(s.round_hist))

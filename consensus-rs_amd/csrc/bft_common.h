@@ -1,0 +1,343 @@
+// bft_common.h — definitions shared by the HIP kernels and the host code of libbftsim.
+//
+// Everything here is a restatement of SPEC.md (the seeded schedule, block identity, quorum,
+// proposer selection, header encoding) written for gfx950 lanes: 32/64-bit integer ops only.
+// Compiled by hipcc for the device and by the host compiler for libbftsim's host helpers and for
+// the CPU wave emulator used by the tests.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define BFT_FN __host__ __device__ inline
+#else
+#define BFT_FN inline
+#endif
+
+namespace bft {
+
+// ---------------------------------------------------------------------------------------------
+// Parameters of one launch (plain data, copied by value into the kernel argument buffer).
+// ---------------------------------------------------------------------------------------------
+struct Params {
+    uint32_t n;               // validators per instance (1..64 on the GPU path)
+    uint32_t seg;             // lanes per instance segment: power of two >= n
+    uint32_t heights;         // H
+    uint32_t hcap;            // rows per instance in the record tables (H + margin)
+    uint32_t max_ticks;
+    uint32_t block_period;
+    uint64_t genesis_time;
+    uint64_t seed;
+    uint32_t thr16;           // drop threshold (0 = no drops)
+    uint32_t byz_count;
+    uint32_t crash_thr32;     // proposer-crash threshold (0 = none)
+    uint32_t crash_on;
+    uint32_t phase_cap;
+    uint32_t need_seed;       // N not a power of two: proposer seeds need block hashes in-kernel
+    uint64_t silent_mask;
+    uint32_t first_instance;
+    uint32_t n_instances;
+    uint32_t genesis_seed;
+    uint32_t pad0;
+    const uint8_t* addresses;         // n*20
+    const uint8_t* genesis_hash;      // 32
+    // outputs
+    uint32_t* committed_height;       // [n_inst]
+    uint32_t* flags;                  // [n_inst]
+    uint32_t* ticks;                  // [n_inst]
+    uint64_t* views;                  // [n_inst]
+    uint32_t* rec;                    // [n_inst * hcap * 4] {round, prop|var<<16|set<<24, T, seed}
+    uint8_t* hash;                    // [n_inst * hcap * 32]
+    uint64_t* trace;                  // optional [n_inst][trace_ticks][n] state digests
+    uint32_t trace_ticks;
+    uint32_t pad1;
+};
+
+// flags (same bits as the oracle)
+constexpr uint32_t FLAG_SAFETY = 1u, FLAG_PHASE_CAP = 2u, FLAG_CORE_PANIC = 4u, FLAG_OUTBOX = 8u,
+                   FLAG_TIMEOUT = 16u, FLAG_RCS_OVERFLOW = 32u;
+
+// State (src/protocol/mod.rs:25-30)
+constexpr uint32_t ST_ACCEPT_REQUEST = 1, ST_PREPREPARED = 2, ST_PREPARED = 3, ST_COMMITTED = 4;
+
+// ---------------------------------------------------------------------------------------------
+// Block identity (SPEC.md §4) packed in 64 bits:
+//   [0,24) height  [24,33) proposer  [33] variant  [34] valid  [35,64) time tick
+// Equality ignores the time tick (a function of height and proposer).
+// ---------------------------------------------------------------------------------------------
+constexpr uint64_t BLK_NONE = 0;
+constexpr uint64_t BLK_VALID = 1ull << 34;
+constexpr uint64_t BLK_ID_MASK = (1ull << 35) - 1;      // height|proposer|variant|valid
+constexpr uint64_t BLK_HP_MASK = (1ull << 33) - 1;      // height|proposer
+BFT_FN uint64_t blk_make(uint32_t h, uint32_t prop, uint32_t var, uint32_t T) {
+    return (uint64_t)(h & 0xffffffu) | ((uint64_t)(prop & 0x1ffu) << 24) | ((uint64_t)(var & 1u) << 33) |
+           BLK_VALID | ((uint64_t)T << 35);
+}
+BFT_FN bool blk_valid(uint64_t b) { return (b & BLK_VALID) != 0; }
+BFT_FN uint32_t blk_h(uint64_t b) { return (uint32_t)(b & 0xffffffu); }
+BFT_FN uint32_t blk_prop(uint64_t b) { return (uint32_t)((b >> 24) & 0x1ffu); }
+BFT_FN uint32_t blk_var(uint64_t b) { return (uint32_t)((b >> 33) & 1u); }
+BFT_FN uint32_t blk_T(uint64_t b) { return (uint32_t)(b >> 35); }
+BFT_FN bool blk_eq(uint64_t a, uint64_t b) {
+    return blk_valid(a) && blk_valid(b) && ((a ^ b) & BLK_ID_MASK) == 0;
+}
+// digest comparison; a Byzantine vote's wildcard digest matches both variants (SPEC.md §6)
+BFT_FN bool digest_match(uint64_t d, bool wild, uint64_t t) {
+    if (!blk_valid(d) || !blk_valid(t)) return false;
+    if (((d ^ t) & BLK_HP_MASK) != 0) return false;
+    return wild || blk_var(d) == blk_var(t);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Seeded randomness (SPEC.md §3, §5)
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t DOM_DROP = 1, DOM_SPLIT = 2, DOM_CRASH = 3, DOM_BYZ = 4, DOM_TX = 5, DOM_TX2 = 6;
+
+BFT_FN uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+
+// Philox4x32-10 (Salmon et al. SC'11); 10 rounds of two 32x32→64 multiplies.
+BFT_FN void philox(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t out[4]) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint32_t hi0 = mulhi32(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        uint32_t hi1 = mulhi32(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+BFT_FN uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+
+// first sender of the receiver's rotated delivery order (SPEC.md §3)
+BFT_FN uint32_t delivery_offset(uint64_t seed, uint32_t n, uint32_t inst, uint32_t tick, uint32_t phase,
+                                uint32_t recv) {
+    uint32_t h = lowbias32(inst ^ (uint32_t)seed);
+    h = lowbias32(h ^ tick);
+    h = lowbias32(h ^ ((phase << 16) | recv) ^ (uint32_t)(seed >> 32));
+    return mulhi32(h, n);
+}
+
+// N-bit delivery mask of receiver `recv` for (tick, phase); self always delivered.
+BFT_FN uint64_t deliver_mask(uint64_t seed, uint32_t n, uint32_t thr16, uint32_t inst, uint32_t tick,
+                             uint32_t phase, uint32_t recv) {
+    uint64_t all = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    if (thr16 == 0) return all;
+    uint64_t m = 0;
+    for (uint32_t j = 0; 8 * j < n; ++j) {
+        uint32_t w[4];
+        philox(seed, inst, tick, (phase << 24) | (recv << 8) | j, DOM_DROP, w);
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i) {
+            uint32_t u = (w[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+            if (u >= thr16) m |= 1ull << (8 * j + i);
+        }
+    }
+    return (m & all) | (1ull << recv);
+}
+
+BFT_FN uint32_t split_bit(uint64_t seed, uint32_t inst, uint32_t h, uint32_t r, uint32_t v) {
+    uint32_t w[4];
+    philox(seed, inst, h, r, DOM_SPLIT | ((v >> 7) << 8), w);
+    uint32_t vv = v & 127u;
+    uint32_t word = (vv >> 5) == 0 ? w[0] : (vv >> 5) == 1 ? w[1] : (vv >> 5) == 2 ? w[2] : w[3];
+    return (word >> (vv & 31u)) & 1u;
+}
+
+BFT_FN bool proposer_crashed(uint64_t seed, uint32_t thr32, uint32_t on, uint32_t inst, uint32_t h, uint32_t r) {
+    if (!on) return false;
+    uint32_t w[4];
+    philox(seed, inst, h, r, DOM_CRASH, w);
+    return w[0] < thr32;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Keccak-256 over the MessagePack header (SPEC.md §7). The absorber keeps the 25-word state in
+// registers and stages one 136-byte rate block in a caller-provided byte buffer (LDS on the
+// device) so that variable-length encodings never index registers dynamically.
+// ---------------------------------------------------------------------------------------------
+BFT_FN uint64_t rotl64(uint64_t x, int n) { return (x << n) | (x >> (64 - n)); }
+
+BFT_FN void keccak_f1600(uint64_t a[25]) {
+    const uint64_t RC[24] = {
+        0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
+        0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+        0x000000000000008Aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000Aull,
+        0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
+        0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
+        0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+    for (int rnd = 0; rnd < 24; ++rnd) {
+        uint64_t c0 = a[0] ^ a[5] ^ a[10] ^ a[15] ^ a[20];
+        uint64_t c1 = a[1] ^ a[6] ^ a[11] ^ a[16] ^ a[21];
+        uint64_t c2 = a[2] ^ a[7] ^ a[12] ^ a[17] ^ a[22];
+        uint64_t c3 = a[3] ^ a[8] ^ a[13] ^ a[18] ^ a[23];
+        uint64_t c4 = a[4] ^ a[9] ^ a[14] ^ a[19] ^ a[24];
+        uint64_t d0 = c4 ^ rotl64(c1, 1), d1 = c0 ^ rotl64(c2, 1), d2 = c1 ^ rotl64(c3, 1);
+        uint64_t d3 = c2 ^ rotl64(c4, 1), d4 = c3 ^ rotl64(c0, 1);
+        // theta + rho + pi (b[y + 5*((2x+3y)%5)] = rotl(a[x+5y], r[x+5y]))
+        uint64_t b0 = a[0] ^ d0;
+        uint64_t b10 = rotl64(a[1] ^ d1, 1);
+        uint64_t b20 = rotl64(a[2] ^ d2, 62);
+        uint64_t b5 = rotl64(a[3] ^ d3, 28);
+        uint64_t b15 = rotl64(a[4] ^ d4, 27);
+        uint64_t b16 = rotl64(a[5] ^ d0, 36);
+        uint64_t b1 = rotl64(a[6] ^ d1, 44);
+        uint64_t b11 = rotl64(a[7] ^ d2, 6);
+        uint64_t b21 = rotl64(a[8] ^ d3, 55);
+        uint64_t b6 = rotl64(a[9] ^ d4, 20);
+        uint64_t b7 = rotl64(a[10] ^ d0, 3);
+        uint64_t b17 = rotl64(a[11] ^ d1, 10);
+        uint64_t b2 = rotl64(a[12] ^ d2, 43);
+        uint64_t b12 = rotl64(a[13] ^ d3, 25);
+        uint64_t b22 = rotl64(a[14] ^ d4, 39);
+        uint64_t b23 = rotl64(a[15] ^ d0, 41);
+        uint64_t b8 = rotl64(a[16] ^ d1, 45);
+        uint64_t b18 = rotl64(a[17] ^ d2, 15);
+        uint64_t b3 = rotl64(a[18] ^ d3, 21);
+        uint64_t b13 = rotl64(a[19] ^ d4, 8);
+        uint64_t b14 = rotl64(a[20] ^ d0, 18);
+        uint64_t b24 = rotl64(a[21] ^ d1, 2);
+        uint64_t b9 = rotl64(a[22] ^ d2, 61);
+        uint64_t b19 = rotl64(a[23] ^ d3, 56);
+        uint64_t b4 = rotl64(a[24] ^ d4, 14);
+        // chi
+        a[0] = b0 ^ (~b1 & b2);   a[1] = b1 ^ (~b2 & b3);   a[2] = b2 ^ (~b3 & b4);
+        a[3] = b3 ^ (~b4 & b0);   a[4] = b4 ^ (~b0 & b1);
+        a[5] = b5 ^ (~b6 & b7);   a[6] = b6 ^ (~b7 & b8);   a[7] = b7 ^ (~b8 & b9);
+        a[8] = b8 ^ (~b9 & b5);   a[9] = b9 ^ (~b5 & b6);
+        a[10] = b10 ^ (~b11 & b12); a[11] = b11 ^ (~b12 & b13); a[12] = b12 ^ (~b13 & b14);
+        a[13] = b13 ^ (~b14 & b10); a[14] = b14 ^ (~b10 & b11);
+        a[15] = b15 ^ (~b16 & b17); a[16] = b16 ^ (~b17 & b18); a[17] = b17 ^ (~b18 & b19);
+        a[18] = b18 ^ (~b19 & b15); a[19] = b19 ^ (~b15 & b16);
+        a[20] = b20 ^ (~b21 & b22); a[21] = b21 ^ (~b22 & b23); a[22] = b22 ^ (~b23 & b24);
+        a[23] = b23 ^ (~b24 & b20); a[24] = b24 ^ (~b20 & b21);
+        a[0] ^= RC[rnd];
+    }
+}
+
+// Streaming absorber: bytes go to buf[0..136); a full block is xored into the state.
+struct Absorb {
+    uint64_t a[25];
+    uint8_t* buf;   // 136 bytes (+8 slack)
+    uint32_t pos;
+};
+
+BFT_FN void absorb_init(Absorb& s, uint8_t* buf) {
+#pragma unroll
+    for (int i = 0; i < 25; ++i) s.a[i] = 0;
+    s.buf = buf;
+    s.pos = 0;
+}
+BFT_FN void absorb_block(Absorb& s) {
+#pragma unroll
+    for (int i = 0; i < 17; ++i) {
+        uint64_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) w |= (uint64_t)s.buf[8 * i + b] << (8 * b);
+        s.a[i] ^= w;
+    }
+    keccak_f1600(s.a);
+    s.pos = 0;
+}
+BFT_FN void absorb_byte(Absorb& s, uint32_t byte) {
+    s.buf[s.pos] = (uint8_t)byte;
+    s.pos += 1;
+    if (s.pos == 136) absorb_block(s);
+}
+BFT_FN void absorb_finish(Absorb& s, uint8_t out[32]) {
+    // pad10*1 with the Keccak domain byte 0x01
+    uint32_t p = s.pos;
+    for (uint32_t i = p; i < 136; ++i) s.buf[i] = 0;
+    s.buf[p] ^= 0x01;
+    s.buf[135] ^= 0x80;
+    absorb_block(s);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) out[8 * i + b] = (uint8_t)(s.a[i] >> (8 * b));
+}
+
+// MessagePack pieces (compact uint, byte arrays as arrays of uints, fixed str8 address)
+BFT_FN void mp_uint(Absorb& s, uint64_t v) {
+    if (v < 128) { absorb_byte(s, (uint32_t)v); return; }
+    if (v < 256) { absorb_byte(s, 0xcc); absorb_byte(s, (uint32_t)v); return; }
+    if (v < 65536) { absorb_byte(s, 0xcd); absorb_byte(s, (uint32_t)(v >> 8) & 0xff); absorb_byte(s, (uint32_t)v & 0xff); return; }
+    if (v < 4294967296ull) {
+        absorb_byte(s, 0xce);
+        for (int i = 0; i < 4; ++i) absorb_byte(s, (uint32_t)(v >> (24 - 8 * i)) & 0xff);
+        return;
+    }
+    absorb_byte(s, 0xcf);
+    for (int i = 0; i < 8; ++i) absorb_byte(s, (uint32_t)(v >> (56 - 8 * i)) & 0xff);
+}
+BFT_FN void mp_u8(Absorb& s, uint32_t b) {
+    if (b < 128) absorb_byte(s, b);
+    else { absorb_byte(s, 0xcc); absorb_byte(s, b); }
+}
+BFT_FN void mp_hash_words(Absorb& s, const uint32_t w[8]) {   // 32 bytes, little-endian words
+    absorb_byte(s, 0xdc); absorb_byte(s, 0x00); absorb_byte(s, 0x20);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) mp_u8(s, (w[i] >> (8 * b)) & 0xffu);
+}
+BFT_FN void mp_zero_hash(Absorb& s) {
+    absorb_byte(s, 0xdc); absorb_byte(s, 0x00); absorb_byte(s, 0x20);
+    for (int i = 0; i < 32; ++i) absorb_byte(s, 0);
+}
+BFT_FN uint32_t hexdigit(uint32_t x) { return x < 10 ? 48u + x : 87u + x; }
+
+// tx_hash words of a candidate (SPEC.md §5, domain TX)
+BFT_FN void tx_hash_words(uint64_t seed, uint32_t inst, uint32_t h, uint32_t prop, uint32_t var, uint32_t w[8]) {
+    philox(seed, inst, h, (prop << 8) | var, DOM_TX, w);
+    philox(seed, inst, h, (prop << 8) | var, DOM_TX2, w + 4);
+}
+
+// Candidate block hash (SPEC.md §7): prev_hash (8 LE words), proposer address (20 bytes).
+BFT_FN void block_hash(Absorb& s, const uint32_t prev[8], const uint8_t* addr20, uint64_t seed,
+                       uint32_t inst, uint32_t h, uint32_t prop, uint32_t var, uint64_t time,
+                       uint8_t out[32]) {
+    s.pos = 0;
+#pragma unroll
+    for (int i = 0; i < 25; ++i) s.a[i] = 0;
+    absorb_byte(s, 0x9d);
+    mp_hash_words(s, prev);
+    absorb_byte(s, 0xd9); absorb_byte(s, 42); absorb_byte(s, '0'); absorb_byte(s, 'x');
+    for (int i = 0; i < 20; ++i) {
+        uint32_t b = addr20[i];
+        absorb_byte(s, hexdigit(b >> 4));
+        absorb_byte(s, hexdigit(b & 15));
+    }
+    mp_zero_hash(s);                       // root
+    uint32_t tx[8];
+    tx_hash_words(seed, inst, h, prop, var, tx);
+    mp_hash_words(s, tx);                  // tx_hash
+    mp_zero_hash(s);                       // receipt_hash
+    absorb_byte(s, 0); absorb_byte(s, 0);  // bloom, difficulty
+    mp_uint(s, h);
+    absorb_byte(s, 0); absorb_byte(s, 0);  // gas_limit, gas_used
+    mp_uint(s, time);
+    // extra = "Coinse base" (minner/mod.rs:113) as an array of 11 uints
+    const char* ex = "Coinse base";
+    absorb_byte(s, 0x9b);
+    for (int i = 0; i < 11; ++i) absorb_byte(s, (uint32_t)(uint8_t)ex[i]);
+    absorb_byte(s, 0xc0);                  // votes: None
+    absorb_finish(s, out);
+}
+
+// randon_seed (validator.rs:39-48): (BE64(hash[0..8]) * 2^64) mod n
+BFT_FN uint32_t seed_from_hash(const uint8_t* h, uint32_t n) {
+    uint64_t be = 0;
+    for (int i = 0; i < 8; ++i) be = (be << 8) | h[i];
+    uint64_t a = be % n;
+    uint64_t t = (0xffffffffffffffffull % n + 1ull) % n;   // 2^64 mod n
+    return (uint32_t)((a * t) % n);
+}
+
+}  // namespace bft

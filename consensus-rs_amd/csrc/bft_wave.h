@@ -1,0 +1,664 @@
+// bft_wave.h — the batched PBFT core: one wavefront simulates 64/S instances, one lane per
+// validator (lane = reference `Core` actor, src/consensus/pbft/core/core.rs:119-140).
+//
+// The body is written once against a tiny wave-ops interface W (HIP intrinsics on gfx950, a
+// fiber emulator on the CPU for the tests). Rules that keep it correct on both:
+//   * collectives (W::ballot, W::shfl_xor, W::sync) are only called from wave-uniform control
+//     flow; the message handlers below are per-lane code and never call them;
+//   * a phase's outbox is published to LDS, then W::sync(), then receivers gather senders'
+//     records in their own rotated order (SPEC.md §3) and run the reference handlers one message
+//     at a time (SPEC.md §2). Everything they send goes to the per-lane `nx` outbox for the next
+//     phase;
+//   * the instance's canonical chain lives in global memory (rec/hash tables); the first Core
+//     commit of a height is recorded by the segment leader after the phase, in lane order, which
+//     is the oracle's receiver order.
+#pragma once
+#include "bft_common.h"
+
+namespace bft {
+
+constexpr int RCS_K = 8;                 // RoundChangeSet rounds kept per validator (LDS)
+constexpr int REC_WORDS = 22;            // LDS words per published outbox record
+constexpr int SCRATCH_BYTES = 144;       // per-lane Keccak rate buffer (136 + slack)
+
+// outbox record flags
+constexpr uint32_t F_PP = 1u, F_PP_EQ = 2u, F_PR = 4u, F_PR_W = 8u, F_CM = 16u, F_CM_W = 32u,
+                   F_OCM = 64u, F_OCM_W = 128u, F_RC = 256u, F_SYNC = 512u, F_BLK = 1024u;
+
+struct Outbox {
+    uint32_t f;
+    uint32_t pp_h, pp_r; uint64_t pp_b;
+    uint32_t pr_h, pr_r; uint64_t pr_d;
+    uint32_t cm_h, cm_r; uint64_t cm_d;
+    uint32_t ocm_h, ocm_r; uint64_t ocm_d;
+    uint32_t rc_h, rc_r;
+    uint32_t sync_h;
+    uint32_t blk_lo, blk_hi;
+};
+
+BFT_FN void outbox_clear(Outbox& o) {
+    o.f = 0;
+    o.pp_h = o.pp_r = 0; o.pp_b = 0;
+    o.pr_h = o.pr_r = 0; o.pr_d = 0;
+    o.cm_h = o.cm_r = 0; o.cm_d = 0;
+    o.ocm_h = o.ocm_r = 0; o.ocm_d = 0;
+    o.rc_h = o.rc_r = 0;
+    o.sync_h = 0;
+    o.blk_lo = o.blk_hi = 0;
+}
+
+// LDS layout of one wave:
+//   [0, 64*REC_WORDS*4)               published outbox records (one per lane)
+//   [.., + 3*RCS_K*64*4)              RoundChangeSet, SoA [k][lane]: round, bitmap lo, bitmap hi
+//   [.., + 64*8*4)                    per-lane commit hand-off {x, blk lo, blk hi, round, seed}
+//                                     (also the Fisher-Yates scratch at init)
+//   [.., + 16*8*4)                    per-segment shared words
+//   need_seed only:
+//   [.., + 64*32)                     per-lane commit hash
+//   [.., + 64*SCRATCH_BYTES)          per-lane Keccak rate buffer
+constexpr uint32_t LDS_REC_OFF = 0;
+constexpr uint32_t LDS_RC_OFF = LDS_REC_OFF + 64 * REC_WORDS * 4;
+constexpr uint32_t LDS_CMT_OFF = LDS_RC_OFF + 3 * RCS_K * 64 * 4;
+constexpr uint32_t LDS_SEG_OFF = LDS_CMT_OFF + 64 * 8 * 4;
+constexpr uint32_t LDS_CHASH_OFF = LDS_SEG_OFF + 16 * 8 * 4;
+constexpr uint32_t LDS_SCR_OFF = LDS_CHASH_OFF + 64 * 32;
+constexpr uint32_t LDS_BYTES_POW2 = LDS_CHASH_OFF;
+constexpr uint32_t LDS_BYTES_SEED = LDS_SCR_OFF + 64 * SCRATCH_BYTES;
+BFT_FN uint32_t lds_bytes_per_wave(bool need_seed) { return need_seed ? LDS_BYTES_SEED : LDS_BYTES_POW2; }
+
+template <class W, bool NEED_SEED>
+struct Sim {
+    const Params& P;
+    uint8_t* lds;
+    // identity
+    uint32_t lane, S, seg_base, me, inst_local, inst;
+    uint64_t seg_mask;       // this segment's bits in a wave ballot
+    bool is_val, running, byz, core_dead;
+    // segment-uniform
+    bool seg_done, frozen;
+    uint32_t canon_h, done_tick, seg_flags;
+    // Core + RoundState (round_state.rs:12-22)
+    uint32_t h, r, st;
+    bool wait;
+    uint64_t lock, pp, pend;
+    uint64_t prep, comm;
+    uint32_t n_rcs;          // RoundChangeSet entries (the table itself lives in LDS)
+    uint32_t proposer;       // 0xffffffff = None
+    // chain tip
+    uint32_t last, last_seed;
+    int32_t last_T;
+    // timers / limiter / miner / sync
+    int32_t tick, timer_tick, rc_last_tick, wake_tick;
+    uint32_t mint_height, miner_queue, sync_pending;
+    uint64_t cand;
+    // gossip outbound cache (last subject per kind)
+    uint32_t s_pp_h, s_pp_r, s_pr_h, s_pr_r, s_cm_h, s_cm_r, s_ocm_h, s_ocm_r;
+    uint64_t s_pp_b, s_pr_d, s_cm_d, s_ocm_d;   // 0 = nothing sent yet
+    // outbox of the next phase
+    Outbox nx;
+    // Core commit of this phase (for canonical resolution)
+    uint32_t commit_x, commit_round, commit_seed;
+    uint64_t commit_blk;
+    uint32_t lane_flags;
+
+    BFT_FN Sim(const Params& p, uint8_t* l, uint32_t wave_global) : P(p), lds(l) {
+        lane = W::lane();
+        S = p.seg;
+        seg_base = lane & ~(S - 1);
+        me = lane - seg_base;
+        inst_local = wave_global * (64u / S) + (lane / S);
+        inst = p.first_instance + inst_local;
+        seg_mask = (S >= 64) ? ~0ull : (((1ull << S) - 1ull) << seg_base);
+        bool inst_ok = inst_local < p.n_instances;
+        is_val = inst_ok && me < p.n;
+        running = is_val && !((p.silent_mask >> me) & 1ull);
+        byz = false;
+        core_dead = false;
+        seg_done = !inst_ok;
+        frozen = false;
+        canon_h = 0;
+        done_tick = p.max_ticks;
+        seg_flags = 0;
+        h = 0; r = 0; st = ST_ACCEPT_REQUEST; wait = false;
+        lock = pp = pend = BLK_NONE;
+        prep = comm = 0;
+        n_rcs = 0;
+        proposer = 0xffffffffu;
+        last = 0; last_seed = p.genesis_seed; last_T = -1;
+        tick = 0; timer_tick = -1; rc_last_tick = 0; wake_tick = -1;
+        mint_height = 0; miner_queue = 0; sync_pending = 0;
+        cand = BLK_NONE;
+        s_pp_h = s_pp_r = s_pr_h = s_pr_r = s_cm_h = s_cm_r = s_ocm_h = s_ocm_r = 0;
+        s_pp_b = s_pr_d = s_cm_d = s_ocm_d = 0;
+        outbox_clear(nx);
+        commit_x = 0; commit_round = 0; commit_seed = 0; commit_blk = 0;
+        lane_flags = 0;
+    }
+
+    // ---------------------------------------------------------------- global canonical table
+    BFT_FN uint32_t* rec_row(uint32_t x) const { return P.rec + ((uint64_t)inst_local * P.hcap + x) * 4; }
+    BFT_FN uint8_t* hash_row(uint32_t x) const { return P.hash + ((uint64_t)inst_local * P.hcap + x) * 32; }
+    BFT_FN uint32_t canon_seed(uint32_t x) const { return x == 0 ? P.genesis_seed : W::gload(rec_row(x) + 3); }
+    // canonical block id at x (x >= 1, must be recorded)
+    BFT_FN uint64_t canon_blk(uint32_t x) const {
+        uint32_t w1 = W::gload(rec_row(x) + 1);
+        uint32_t T = W::gload(rec_row(x) + 2);
+        return blk_make(x, w1 & 0xffffu, (w1 >> 16) & 1u, T);
+    }
+    BFT_FN void prev_hash_words(uint32_t x, uint32_t w[8]) const {   // hash of canonical block x
+        if (x == 0) {
+            for (int i = 0; i < 8; ++i)
+                w[i] = (uint32_t)P.genesis_hash[4 * i] | ((uint32_t)P.genesis_hash[4 * i + 1] << 8) |
+                       ((uint32_t)P.genesis_hash[4 * i + 2] << 16) | ((uint32_t)P.genesis_hash[4 * i + 3] << 24);
+            return;
+        }
+        const uint32_t* p = (const uint32_t*)hash_row(x);
+        for (int i = 0; i < 8; ++i) w[i] = W::gload(p + i);
+    }
+
+    // ---------------------------------------------------------------- outbox (backend.rs:140-160)
+    BFT_FN void out_preprepare(uint32_t vh, uint32_t vr, uint64_t b, bool equiv) {
+        if (s_pp_b != 0 && s_pp_h == vh && s_pp_r == vr && blk_eq(s_pp_b, b)) return;
+        s_pp_h = vh; s_pp_r = vr; s_pp_b = b;
+        if (nx.f & F_PP) { lane_flags |= FLAG_OUTBOX; return; }
+        nx.f |= F_PP | (equiv ? F_PP_EQ : 0u); nx.pp_h = vh; nx.pp_r = vr; nx.pp_b = b;
+    }
+    BFT_FN void out_prepare(uint32_t vh, uint32_t vr, uint64_t d, bool wild) {
+        if (s_pr_d != 0 && s_pr_h == vh && s_pr_r == vr && blk_eq(s_pr_d, d)) return;
+        s_pr_h = vh; s_pr_r = vr; s_pr_d = d;
+        if (nx.f & F_PR) { lane_flags |= FLAG_OUTBOX; return; }
+        nx.f |= F_PR | (wild ? F_PR_W : 0u); nx.pr_h = vh; nx.pr_r = vr; nx.pr_d = d;
+    }
+    BFT_FN void out_commit(uint32_t vh, uint32_t vr, uint64_t d, bool wild) {
+        if (s_cm_d != 0 && s_cm_h == vh && s_cm_r == vr && blk_eq(s_cm_d, d)) return;
+        s_cm_h = vh; s_cm_r = vr; s_cm_d = d;
+        if (nx.f & F_CM) { lane_flags |= FLAG_OUTBOX; return; }
+        nx.f |= F_CM | (wild ? F_CM_W : 0u); nx.cm_h = vh; nx.cm_r = vr; nx.cm_d = d;
+    }
+    BFT_FN void out_old_commit(uint32_t vh, uint32_t vr, uint64_t d, bool wild) {
+        if (s_ocm_d != 0 && s_ocm_h == vh && s_ocm_r == vr && blk_eq(s_ocm_d, d)) return;
+        s_ocm_h = vh; s_ocm_r = vr; s_ocm_d = d;
+        if (nx.f & F_OCM) { lane_flags |= FLAG_OUTBOX; return; }
+        nx.f |= F_OCM | (wild ? F_OCM_W : 0u); nx.ocm_h = vh; nx.ocm_r = vr; nx.ocm_d = d;
+    }
+    BFT_FN void out_round_change(uint32_t vh, uint32_t vr) {
+        if (nx.f & F_RC) { lane_flags |= FLAG_OUTBOX; return; }
+        nx.f |= F_RC; nx.rc_h = vh; nx.rc_r = vr;
+    }
+    BFT_FN void out_sync(uint32_t height) {
+        if (nx.f & F_SYNC) { if (height < nx.sync_h) nx.sync_h = height; return; }
+        nx.f |= F_SYNC; nx.sync_h = height;
+    }
+    BFT_FN void out_blocks(uint32_t lo, uint32_t hi) {
+        if (lo > hi) return;
+        if (!(nx.f & F_BLK)) { nx.f |= F_BLK; nx.blk_lo = lo; nx.blk_hi = hi; return; }
+        if (lo < nx.blk_lo) nx.blk_lo = lo;
+        if (hi > nx.blk_hi) nx.blk_hi = hi;
+    }
+
+    // ---------------------------------------------------------------- timers, chain, miner
+    BFT_FN void new_round_change_timer() { timer_tick = tick + 1; }     // core.rs:643-657
+    BFT_FN void stop_timer() { timer_tick = -1; }                         // core.rs:638-641
+
+    // the tip moved to a block recorded by an earlier phase: refresh its time tick and seed
+    BFT_FN void refresh_tip_from_table() {
+        uint32_t w1 = W::gload(rec_row(last) + 1);
+        (void)w1;
+        last_T = (int32_t)W::gload(rec_row(last) + 2);
+        last_seed = W::gload(rec_row(last) + 3);
+    }
+
+    // Chain::insert_block for a Core commit (core/chain.rs:45-71 via backend.rs:163-200)
+    BFT_FN void chain_insert_core(uint64_t b) {
+        uint32_t x = blk_h(b);
+        if (x <= last) return;                              // ChainError::Exists
+        if (last + 1 < x) { out_sync(last + 1); return; }    // Not found ancestor → SyncBlock
+        if (commit_x != 0) lane_flags |= FLAG_OUTBOX;        // (cannot happen: one insert per phase)
+        commit_x = x;
+        commit_blk = b;
+        commit_round = r;
+        uint32_t sd = 0;
+        if (NEED_SEED) {
+            uint32_t prev[8];
+            prev_hash_words(last, prev);
+            Absorb ab;
+            ab.buf = lds + LDS_SCR_OFF + lane * SCRATCH_BYTES;
+            uint8_t out[32];
+            uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
+            block_hash(ab, prev, P.addresses + 20u * blk_prop(b), P.seed, inst, x, blk_prop(b), blk_var(b), time, out);
+            uint8_t* hs = lds + LDS_CHASH_OFF + lane * 32;
+            for (int i = 0; i < 32; ++i) hs[i] = out[i];
+            sd = seed_from_hash(out, P.n);
+        }
+        commit_seed = sd;
+        last = x;
+        last_T = (int32_t)blk_T(b);
+        last_seed = sd;
+        out_blocks(x, x);                                   // ChainEvent::NewBlock (chain.rs:61)
+        if (x > miner_queue) miner_queue = x;               // ChainEvent::NewHeader (chain.rs:62)
+    }
+
+    // handle_msg_middle Block branch (core.rs:75-82): insert lo..hi in order, unverified
+    BFT_FN void handle_blocks(uint32_t lo, uint32_t hi) {
+        if (hi <= last) return;                             // all Exists
+        if (lo > last + 1) { out_sync(last + 1); return; }  // every block is a gap
+        uint32_t from = last + 1;
+        last = hi;
+        refresh_tip_from_table();
+        out_blocks(from, hi);
+        if (hi > miner_queue) miner_queue = hi;
+    }
+
+    // handle_msg_middle Sync branch (core.rs:83-110)
+    BFT_FN void handle_sync(uint32_t height) {
+        if (height > last) return;
+        uint32_t hi = last < height + 101u ? last : height + 101u;
+        out_blocks(height, hi);
+    }
+
+    // Minner::mine + packet_next_block + next_block + Engine::seal (minner/mod.rs:95-143)
+    BFT_FN void miner_mine() {
+        uint32_t x = last + 1;
+        int32_t T = tick > last_T + 1 ? tick : last_T + 1;
+        cand = blk_make(x, me, 0, (uint32_t)T);
+        mint_height = x;
+        wake_tick = T;
+        if (T > tick) return;            // seal sleeps until header.time (backend.rs:437-449)
+        wake_tick = -1;
+        handle_new_header_event();
+    }
+    // Minner: Handler<ChainEvent::NewHeader> (minner/mod.rs:56-69)
+    BFT_FN void miner_step() {
+        if (wake_tick >= 0) return;
+        uint32_t q = miner_queue;
+        miner_queue = 0;
+        if (q != 0 && q >= mint_height) miner_mine();
+    }
+
+    // ---------------------------------------------------------------- Core
+    BFT_FN bool is_proposer(uint32_t who) const { return proposer == who; }
+
+    // Core::check_message (core.rs:366-399): 0 ok, 1 unknown, 2 future block, 3 old, 4 future msg
+    BFT_FN int check_message(int code, uint32_t vh) const {
+        if (vh == 0) return 1;
+        if (code == 4) { if (vh > h) return 2; if (vh < h) return 3; return 0; }
+        if (vh > h) return 2;
+        if (vh < h) return 3;
+        if (st == ST_ACCEPT_REQUEST) return code > 1 ? 4 : 0;
+        return 0;
+    }
+    BFT_FN void note_future_block(uint32_t vh) { if (vh > sync_pending) sync_pending = vh; }
+    BFT_FN void lock_hash() { if (blk_valid(pp)) lock = pp; }               // round_state.rs:100-110
+
+    BFT_FN void send_preprepare(uint64_t req) {                               // preprepare.rs:30-43
+        if (h == blk_h(req) && is_proposer(me)) {
+            if (proposer_crashed(P.seed, P.crash_thr32, P.crash_on, inst, h, r)) return;
+            bool equiv = byz && blk_prop(req) == me && blk_var(req) == 0;
+            out_preprepare(h, r, req, equiv);
+        }
+    }
+    BFT_FN void send_prepare() {                                              // prepare.rs:28-38
+        out_prepare(h, r, pp, byz);
+        if (byz) out_commit(h, r, pp, true);
+    }
+    BFT_FN void send_commit() { out_commit(h, r, pp, byz); }                 // commit.rs:37-60
+    BFT_FN void catchup_round() { wait = true; new_round_change_timer(); }   // core.rs:555-565
+
+    BFT_FN void send_round_change(uint32_t round) {                          // round_change.rs:38-63
+        if (rc_last_tick == tick) { new_round_change_timer(); return; }
+        rc_last_tick = tick;
+        if (r < round) catchup_round();
+        out_round_change(h, round);
+    }
+    // RoundChangeSet table in LDS, SoA [k][lane] (conflict-free per-lane access)
+    BFT_FN uint32_t* rc_round_p(uint32_t k) const { return (uint32_t*)(lds + LDS_RC_OFF) + k * 64 + lane; }
+    BFT_FN uint32_t* rc_lo_p(uint32_t k) const { return (uint32_t*)(lds + LDS_RC_OFF) + (RCS_K + k) * 64 + lane; }
+    BFT_FN uint32_t* rc_hi_p(uint32_t k) const { return (uint32_t*)(lds + LDS_RC_OFF) + (2 * RCS_K + k) * 64 + lane; }
+    BFT_FN uint64_t rc_set_at(uint32_t k) const { return (uint64_t)*rc_lo_p(k) | ((uint64_t)*rc_hi_p(k) << 32); }
+
+    BFT_FN uint32_t rcs_max_round() const {                                  // round_change_set.rs:64-74
+        uint32_t mx = 0;
+        int total = 0;
+        for (uint32_t i = 0; i < n_rcs; ++i) {               // ascending rounds (canonical order)
+            int len = __builtin_popcountll(rc_set_at(i));
+            uint32_t rd = *rc_round_p(i);
+            if (len >= total && rd > mx) { mx = rd; total = len; }
+        }
+        return mx;
+    }
+    BFT_FN int rcs_add(uint32_t round, uint32_t sender) {                    // round_change_set.rs:28-35
+        uint32_t pos = 0;
+        while (pos < n_rcs && *rc_round_p(pos) < round) ++pos;
+        if (pos == n_rcs || *rc_round_p(pos) != round) {
+            if (n_rcs == (uint32_t)RCS_K) { lane_flags |= FLAG_RCS_OVERFLOW; return 0; }
+            for (uint32_t i = n_rcs; i > pos; --i) {
+                *rc_round_p(i) = *rc_round_p(i - 1);
+                *rc_lo_p(i) = *rc_lo_p(i - 1);
+                *rc_hi_p(i) = *rc_hi_p(i - 1);
+            }
+            *rc_round_p(pos) = round;
+            *rc_lo_p(pos) = 0;
+            *rc_hi_p(pos) = 0;
+            n_rcs += 1;
+        }
+        uint64_t set = rc_set_at(pos) | (1ull << sender);
+        *rc_lo_p(pos) = (uint32_t)set;
+        *rc_hi_p(pos) = (uint32_t)(set >> 32);
+        return __builtin_popcountll(set);
+    }
+    BFT_FN void send_next_round_change() {                                   // round_change.rs:26-36
+        uint32_t round = rcs_max_round();
+        if (round <= r) send_round_change(r + 1);
+        else send_round_change(round);
+    }
+
+    BFT_FN void start_new_zero_round() {                                     // core.rs:441-470
+        uint32_t last_height = last;
+        h = last_height + 1;
+        r = 0;
+        n_rcs = 0;
+        lock = pp = pend = BLK_NONE;
+        prep = comm = 0;
+        proposer = (last_seed + 0u) % P.n;
+        wait = false;
+        st = ST_ACCEPT_REQUEST;
+        new_round_change_timer();
+    }
+
+    BFT_FN void start_new_round(uint32_t round) {                            // core.rs:474-551
+        uint32_t last_height = last;
+        if (last_height > h) return;
+        n_rcs = 0;
+        if (!blk_valid(lock)) pp = BLK_NONE;
+        prep = comm = 0;
+        r = round;
+        proposer = (last_seed + round) % P.n;
+        wait = false;
+        st = ST_ACCEPT_REQUEST;
+        if (is_proposer(me)) {
+            if (blk_valid(lock)) {
+                send_preprepare(pp);
+            } else {
+                if (!blk_valid(pend)) { core_dead = true; lane_flags |= FLAG_CORE_PANIC; return; }
+                send_preprepare(pend);
+            }
+        }
+        new_round_change_timer();
+    }
+
+    BFT_FN void handle_new_header_event() {                // core.rs:154-163 + request.rs:19-42
+        if (core_dead) return;
+        start_new_zero_round();
+        uint64_t req = cand;
+        if (h != blk_h(req)) return;                       // OldMessage / FutureMessage
+        pend = req;
+        send_preprepare(req);
+    }
+
+    BFT_FN void handle_timer_event() {                     // core.rs:207-225
+        if (last >= h) { stop_timer(); wait = false; }
+        else send_next_round_change();
+    }
+
+    BFT_FN void core_commit() {                            // core.rs:402-422
+        st = ST_COMMITTED;
+        chain_insert_core(pp);
+    }
+
+    BFT_FN void handle_preprepare(uint32_t src, uint32_t vh, uint32_t vr, uint64_t b, bool equiv) {   // preprepare.rs:45-126
+        if (equiv && me != src && split_bit(P.seed, inst, vh, vr, me)) b |= 1ull << 33;
+        int res = check_message(1, vh);
+        if (res != 0) {
+            if (res == 3) {
+                uint32_t bh = blk_h(b);
+                if (bh > last) return;                                        // InvalidProposal
+                if (!blk_eq(canon_blk(bh), b)) return;                        // InvalidProposal
+                uint32_t old_prop = (canon_seed(bh - 1) + vr) % P.n;
+                if (old_prop == src) out_old_commit(vh, vr, b, byz);
+            } else if (res != 2) {
+                return;
+            }
+        }
+        if (!is_proposer(src)) return;                                        // NotFromProposer
+        if (blk_h(b) == 0 || blk_h(b) - 1 > last) { send_next_round_change(); return; }  // verify
+        if (st == ST_ACCEPT_REQUEST) {
+            if (blk_valid(lock)) {
+                if (blk_eq(b, lock)) { pp = b; st = ST_PREPARED; send_commit(); }
+                else send_next_round_change();
+            } else {
+                pp = b; st = ST_PREPREPARED; send_prepare();
+            }
+        }
+    }
+
+    BFT_FN void handle_prepare(uint32_t src, uint32_t vh, uint32_t vr, uint64_t d, bool wild) {   // prepare.rs:48-66
+        int res = check_message(2, vh);
+        if (res != 0) { if (res == 2) note_future_block(vh); return; }
+        if (vh != h || vr != r) return;
+        prep |= 1ull << src;
+        if (blk_valid(lock) && digest_match(d, wild, lock)) { lock_hash(); st = ST_PREPARED; send_commit(); }
+        if ((uint32_t)__builtin_popcountll(prep | comm) > (2u * P.n) / 3u) { lock_hash(); st = ST_PREPARED; send_commit(); }
+    }
+
+    BFT_FN void handle_commit(uint32_t src, uint32_t vh, uint32_t vr, uint64_t d, bool wild) {    // commit.rs:63-111
+        int res = check_message(3, vh);
+        if (res != 0) { if (res == 2) note_future_block(vh); return; }
+        if (!digest_match(d, wild, pp) || vh != h || vr != r) return;
+        comm |= 1ull << src;
+        if ((uint32_t)__builtin_popcountll(comm) > (2u * P.n) / 3u && st < ST_COMMITTED) { lock_hash(); core_commit(); }
+    }
+
+    BFT_FN void handle_round_change(uint32_t src, uint32_t vh, uint32_t mr) {   // round_change.rs:65-98
+        int res = check_message(4, vh);
+        if (res != 0) { if (res == 2) note_future_block(vh); return; }
+        if (r > mr && mr > 0) { send_round_change(mr); return; }
+        int n = rcs_add(mr, src);
+        if ((uint32_t)n >= (2u * P.n) / 3u + 1u && wait && r < mr) {
+            send_round_change(mr);
+            start_new_round(mr);
+        }
+    }
+
+    // ---------------------------------------------------------------- phase machinery
+    BFT_FN uint32_t* rec_lds(uint32_t l) const { return (uint32_t*)(lds + LDS_REC_OFF) + l * REC_WORDS; }
+
+    BFT_FN void publish() {      // nx → LDS (this lane's slot), clear nx
+        uint32_t* o = rec_lds(lane);
+        o[0] = nx.f;
+        o[1] = nx.pp_h; o[2] = nx.pp_r; o[3] = (uint32_t)nx.pp_b; o[4] = (uint32_t)(nx.pp_b >> 32);
+        o[5] = nx.pr_h; o[6] = nx.pr_r; o[7] = (uint32_t)nx.pr_d; o[8] = (uint32_t)(nx.pr_d >> 32);
+        o[9] = nx.cm_h; o[10] = nx.cm_r; o[11] = (uint32_t)nx.cm_d; o[12] = (uint32_t)(nx.cm_d >> 32);
+        o[13] = nx.ocm_h; o[14] = nx.ocm_r; o[15] = (uint32_t)nx.ocm_d; o[16] = (uint32_t)(nx.ocm_d >> 32);
+        o[17] = nx.rc_h; o[18] = nx.rc_r; o[19] = nx.sync_h; o[20] = nx.blk_lo; o[21] = nx.blk_hi;
+        outbox_clear(nx);
+    }
+
+    BFT_FN void deliver_from(uint32_t s) {     // all messages of sender s (SPEC.md §2 order)
+        const uint32_t* m = rec_lds(seg_base + s);
+        uint32_t f = m[0];
+        if (f == 0) return;
+        if (s != me && (f & F_BLK)) handle_blocks(m[20], m[21]);
+        if (s != me && (f & F_SYNC)) handle_sync(m[19]);
+        if (core_dead) return;
+        if (f & F_PP) {
+            handle_preprepare(s, m[1], m[2], (uint64_t)m[3] | ((uint64_t)m[4] << 32), (f & F_PP_EQ) != 0);
+            if (core_dead) return;
+        }
+        if (f & F_PR) handle_prepare(s, m[5], m[6], (uint64_t)m[7] | ((uint64_t)m[8] << 32), (f & F_PR_W) != 0);
+        if (f & F_OCM) handle_commit(s, m[13], m[14], (uint64_t)m[15] | ((uint64_t)m[16] << 32), (f & F_OCM_W) != 0);
+        if (f & F_CM) handle_commit(s, m[9], m[10], (uint64_t)m[11] | ((uint64_t)m[12] << 32), (f & F_CM_W) != 0);
+        if (f & F_RC) handle_round_change(s, m[17], m[18]);
+    }
+
+    BFT_FN bool pending_local() const {
+        return running && (nx.f != 0 || (wake_tick < 0 && miner_queue != 0 && miner_queue >= mint_height));
+    }
+
+    BFT_FN void t_step() {
+        if (tick == 0) {
+            start_new_zero_round();          // Core::started (core.rs:144-147)
+            miner_mine();                    // Minner::started (minner/mod.rs:43-48)
+            return;
+        }
+        if (wake_tick == tick) { wake_tick = -1; handle_new_header_event(); }
+        miner_step();
+        if (sync_pending) {
+            if (last < sync_pending) out_sync(last + 1);
+            sync_pending = 0;
+        }
+        if (!core_dead && timer_tick == tick) { timer_tick = -1; handle_timer_event(); }
+    }
+
+    // segment reductions (butterfly inside the segment)
+    BFT_FN uint32_t seg_max(uint32_t v) {
+        for (uint32_t m = 1; m < S; m <<= 1) { uint32_t o = W::shfl_xor(v, m); v = v > o ? v : o; }
+        return v;
+    }
+    BFT_FN uint32_t seg_or(uint32_t v) {
+        for (uint32_t m = 1; m < S; m <<= 1) v |= W::shfl_xor(v, m);
+        return v;
+    }
+
+    // first Core commits of the phase → canonical table, in lane order (oracle receiver order)
+    BFT_FN void resolve_commits() {
+        bool c = commit_x != 0;
+        uint64_t bal = W::ballot(c);
+        if (bal == 0) return;
+        uint32_t* cm = (uint32_t*)(lds + LDS_CMT_OFF) + lane * 8;
+        if (c) {
+            cm[0] = commit_x; cm[1] = (uint32_t)commit_blk; cm[2] = (uint32_t)(commit_blk >> 32);
+            cm[3] = commit_round; cm[4] = commit_seed;
+        }
+        W::sync();
+        uint64_t segbits = bal & seg_mask;
+        uint32_t* segw = (uint32_t*)(lds + LDS_SEG_OFF) + (lane / S) * 8;
+        if (segbits != 0 && !seg_done && lane == (uint32_t)__builtin_ctzll(segbits)) {
+            // the segment leader replays the commits of this phase in lane order
+            uint32_t ch = canon_h;
+            bool fr = false;
+            uint64_t bits = segbits;
+            while (bits != 0) {
+                uint32_t j = (uint32_t)__builtin_ctzll(bits);
+                bits &= bits - 1;
+                const uint32_t* cj = (const uint32_t*)(lds + LDS_CMT_OFF) + j * 8;
+                uint32_t x = cj[0];
+                uint64_t b = (uint64_t)cj[1] | ((uint64_t)cj[2] << 32);
+                if (x >= P.hcap) { fr = true; break; }
+                uint32_t* row = rec_row(x);
+                uint32_t w1 = W::gload(row + 1);
+                if (w1 & (1u << 24)) {
+                    if ((w1 & 0xffffu) != blk_prop(b) || ((w1 >> 16) & 1u) != blk_var(b)) { fr = true; break; }
+                } else {
+                    W::gstore(row + 0, cj[3]);
+                    W::gstore(row + 2, blk_T(b));
+                    W::gstore(row + 3, cj[4]);
+                    W::gstore(row + 1, blk_prop(b) | (blk_var(b) << 16) | (1u << 24));
+                    if (NEED_SEED) {
+                        const uint32_t* hs = (const uint32_t*)(lds + LDS_CHASH_OFF + j * 32);
+                        uint32_t* dst = (uint32_t*)hash_row(x);
+                        for (int i = 0; i < 8; ++i) W::gstore(dst + i, hs[i]);
+                    }
+                    if (x > ch) ch = x;
+                }
+            }
+            segw[0] = ch;
+            segw[1] = fr ? 1u : 0u;
+        }
+        W::sync();
+        if (segbits != 0 && !seg_done) {
+            canon_h = segw[0];
+            if (segw[1]) { frozen = true; seg_flags |= FLAG_SAFETY; }
+        }
+        commit_x = 0;
+        W::sync();
+    }
+
+    BFT_FN uint64_t state_digest() const {
+        return (uint64_t)(h & 0xffffu) | ((uint64_t)(r & 0xffu) << 16) | ((uint64_t)(st & 7u) << 24) |
+               ((uint64_t)(wait ? 1 : 0) << 27) | ((uint64_t)(last & 0xffffu) << 28) |
+               ((uint64_t)(blk_valid(lock) ? 1 : 0) << 44) | ((uint64_t)(blk_valid(pp) ? 1 : 0) << 45) |
+               ((uint64_t)(blk_valid(pend) ? 1 : 0) << 46) | ((uint64_t)(core_dead ? 1 : 0) << 47) |
+               ((uint64_t)(__builtin_popcountll(prep) & 0xff) << 48) |
+               ((uint64_t)(__builtin_popcountll(comm) & 0xff) << 56);
+    }
+
+    BFT_FN void init_byzantine() {       // partial Fisher-Yates by the segment's lane 0 (SPEC.md §5)
+        uint8_t* perm = lds + LDS_CMT_OFF + seg_base;                   // segment scratch (S bytes)
+        uint32_t* segw = (uint32_t*)(lds + LDS_SEG_OFF) + (lane / S) * 8;
+        if (me == 0 && !seg_done) {
+            uint32_t n = P.n;
+            for (uint32_t i = 0; i < n; ++i) perm[i] = (uint8_t)i;
+            uint64_t mask = 0;
+            uint32_t f = P.byz_count < n ? P.byz_count : n;
+            for (uint32_t i = 0; i < f; ++i) {
+                uint32_t w[4];
+                philox(P.seed, inst, i, 0, DOM_BYZ, w);
+                uint32_t j = i + w[0] % (n - i);
+                uint8_t t = perm[i]; perm[i] = perm[j]; perm[j] = t;
+                mask |= 1ull << perm[i];
+            }
+            segw[2] = (uint32_t)mask;
+            segw[3] = (uint32_t)(mask >> 32);
+        }
+        W::sync();
+        uint64_t mask = (uint64_t)segw[2] | ((uint64_t)segw[3] << 32);
+        byz = is_val && !seg_done && ((mask >> me) & 1ull);
+        W::sync();
+    }
+
+    // ---------------------------------------------------------------- the run
+    BFT_FN void run() {
+        if (P.byz_count > 0) init_byzantine();
+        for (tick = 0; tick < (int32_t)P.max_ticks; ++tick) {
+            if (W::ballot(!seg_done) == 0) break;
+            bool act = running && !seg_done;
+            if (act) t_step();
+            for (uint32_t p = 0;; ++p) {
+                bool pend_l = act && !frozen && pending_local();
+                uint64_t bal = W::ballot(pend_l);
+                if (bal == 0) break;
+                bool seg_pending = (bal & seg_mask) != 0;
+                if (p >= P.phase_cap) {
+                    // messages still in flight are dropped (SPEC.md §2)
+                    uint64_t inflight = W::ballot(act && nx.f != 0);
+                    if ((inflight & seg_mask) != 0 && !seg_done) seg_flags |= FLAG_PHASE_CAP;
+                    outbox_clear(nx);
+                    break;
+                }
+                publish();
+                W::sync();
+                if (act && seg_pending) {
+                    miner_step();                             // event step
+                    uint64_t mk = deliver_mask(P.seed, P.n, P.thr16, inst, (uint32_t)tick, p, me);
+                    uint32_t off = delivery_offset(P.seed, P.n, inst, (uint32_t)tick, p, me);
+                    for (uint32_t k = 0; k < P.n; ++k) {
+                        uint32_t s = off + k;
+                        if (s >= P.n) s -= P.n;
+                        if ((mk >> s) & 1ull) deliver_from(s);
+                    }
+                }
+                W::sync();
+                resolve_commits();
+                if (frozen) act = false;
+            }
+            if (P.trace && is_val && !seg_done && (uint32_t)tick < P.trace_ticks)
+                P.trace[((uint64_t)inst_local * P.trace_ticks + (uint32_t)tick) * P.n + me] = state_digest();
+            if (!seg_done && (frozen || canon_h >= P.heights)) { seg_done = true; done_tick = (uint32_t)tick + 1; }
+        }
+        // outputs (segment lane 0)
+        uint32_t lf = seg_or(lane_flags);
+        if (me == 0 && inst_local < P.n_instances) {
+            uint32_t flags = lf | seg_flags;
+            if (!frozen && canon_h < P.heights) flags |= FLAG_TIMEOUT;
+            uint32_t chh = canon_h < P.heights ? canon_h : P.heights;
+            uint64_t views = 0;
+            for (uint32_t x = 1; x <= chh; ++x) views += (uint64_t)W::gload(rec_row(x)) + 1ull;
+            P.committed_height[inst_local] = chh;
+            P.flags[inst_local] = flags;
+            P.ticks[inst_local] = done_tick;
+            P.views[inst_local] = views;
+        }
+    }
+};
+
+}  // namespace bft

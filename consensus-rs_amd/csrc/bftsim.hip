@@ -1,0 +1,364 @@
+// bftsim.hip — gfx950 kernels and the C ABI of libbftsim (include/bftsim.h).
+//
+// Kernels:
+//   bft_consensus_kernel  one 64-lane wave per 64/S instances, lane = validator (bft_wave.h);
+//   bft_hash_kernel       one lane per instance: Keccak-256 of every committed header, chained
+//                         through prev_hash (power-of-two N, where proposer seeds are always 0
+//                         and the consensus kernel does not need hashes);
+//   bft_stats_kernel      per-launch totals for the RCCL all-reduce of the benchmark.
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/bftsim.h"
+#include "bft_common.h"
+#include "bft_wave.h"
+
+namespace bft {
+
+// ------------------------------------------------------------------------------ wave ops (gfx950)
+struct WaveHip {
+    __device__ static uint32_t lane() { return __lane_id(); }
+    __device__ static uint64_t ballot(bool p) { return __ballot(p); }
+    __device__ static uint32_t shfl_xor(uint32_t v, int m) { return (uint32_t)__shfl_xor((int)v, m, 64); }
+    __device__ static void sync() {
+        // LDS traffic of one wave is processed in order; this orders the compiler's view and
+        // drains outstanding LDS operations before other lanes read what this lane wrote.
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __device__ static uint32_t gload(const uint32_t* p) {
+        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ static void gstore(uint32_t* p, uint32_t v) {
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+};
+
+template <bool NEED_SEED>
+__global__ __launch_bounds__(64) void bft_consensus_kernel(Params p) {
+    extern __shared__ uint8_t lds[];
+    Sim<WaveHip, NEED_SEED> sim(p, lds, blockIdx.x);
+    sim.run();
+}
+
+__global__ __launch_bounds__(64) void bft_hash_kernel(Params p) {
+    extern __shared__ uint8_t lds[];
+    uint32_t il = blockIdx.x * 64u + threadIdx.x;
+    if (il >= p.n_instances) return;
+    uint32_t inst = p.first_instance + il;
+    uint32_t ch = p.committed_height[il];
+    uint32_t prev[8];
+    for (int i = 0; i < 8; ++i)
+        prev[i] = (uint32_t)p.genesis_hash[4 * i] | ((uint32_t)p.genesis_hash[4 * i + 1] << 8) |
+                  ((uint32_t)p.genesis_hash[4 * i + 2] << 16) | ((uint32_t)p.genesis_hash[4 * i + 3] << 24);
+    Absorb ab;
+    ab.buf = lds + threadIdx.x * SCRATCH_BYTES;
+    for (uint32_t x = 1; x <= ch; ++x) {
+        const uint32_t* row = p.rec + ((uint64_t)il * p.hcap + x) * 4;
+        uint32_t w1 = row[1];
+        uint32_t prop = w1 & 0xffffu, var = (w1 >> 16) & 1u, T = row[2];
+        uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)T + 1ull);
+        uint8_t out[32];
+        block_hash(ab, prev, p.addresses + 20u * prop, p.seed, inst, x, prop, var, time, out);
+        uint32_t* dst = (uint32_t*)(p.hash + ((uint64_t)il * p.hcap + x) * 32);
+        for (int i = 0; i < 8; ++i) {
+            uint32_t w = (uint32_t)out[4 * i] | ((uint32_t)out[4 * i + 1] << 8) | ((uint32_t)out[4 * i + 2] << 16) |
+                         ((uint32_t)out[4 * i + 3] << 24);
+            dst[i] = w;
+            prev[i] = w;
+        }
+    }
+}
+
+// totals: [0] instances [1] committed [2] views [3] ticks [4..9] flag counts [10..74] round hist
+__global__ __launch_bounds__(256) void bft_stats_kernel(Params p, unsigned long long* st) {
+    uint32_t il = blockIdx.x * 256u + threadIdx.x;
+    if (il >= p.n_instances) return;
+    uint32_t ch = p.committed_height[il];
+    atomicAdd(&st[0], 1ull);
+    atomicAdd(&st[1], (unsigned long long)ch);
+    atomicAdd(&st[2], (unsigned long long)p.views[il]);
+    atomicAdd(&st[3], (unsigned long long)p.ticks[il]);
+    uint32_t f = p.flags[il];
+    for (int b = 0; b < 6; ++b)
+        if (f & (1u << b)) atomicAdd(&st[4 + b], 1ull);
+    for (uint32_t x = 1; x <= ch; ++x) {
+        uint32_t rd = p.rec[((uint64_t)il * p.hcap + x) * 4];
+        atomicAdd(&st[10 + (rd < 64 ? rd : 64)], 1ull);
+    }
+}
+
+}  // namespace bft
+
+#include "bft_host.h"
+using bft::host_keccak;
+using bft::host_genesis_hash;
+
+struct bftsim {
+    bftsim_config cfg;
+    std::vector<uint8_t> addresses;
+    int device = 0;
+    std::string err;
+    uint8_t genesis_hash[32];
+    uint32_t genesis_seed = 0;
+    uint32_t seg = 64;
+    uint32_t hcap = 0;
+    // device buffers
+    uint64_t cap_inst = 0;
+    uint8_t* d_addr = nullptr;
+    uint8_t* d_ghash = nullptr;
+    uint32_t* d_ch = nullptr;
+    uint32_t* d_flags = nullptr;
+    uint32_t* d_ticks = nullptr;
+    uint64_t* d_views = nullptr;
+    uint32_t* d_rec = nullptr;
+    uint8_t* d_hash = nullptr;
+    unsigned long long* d_stats = nullptr;
+    uint64_t* d_trace = nullptr;
+    uint64_t* h_trace = nullptr;
+    uint32_t trace_ticks = 0;
+    uint64_t last_n = 0, last_first = 0;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    hipStream_t last_stream = nullptr;
+};
+
+static int fail(bftsim* h, int code, const std::string& msg) {
+    if (h) h->err = msg;
+    return code;
+}
+#define HIPCHECK(h, x)                                                                          \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess) return fail(h, BFTSIM_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+static void free_bufs(bftsim* h) {
+    (void)hipFree(h->d_ch); (void)hipFree(h->d_flags); (void)hipFree(h->d_ticks); (void)hipFree(h->d_views);
+    (void)hipFree(h->d_rec); (void)hipFree(h->d_hash); (void)hipFree(h->d_trace);
+    h->d_ch = h->d_flags = h->d_ticks = nullptr; h->d_views = nullptr;
+    h->d_rec = nullptr; h->d_hash = nullptr; h->d_trace = nullptr;
+    h->cap_inst = 0;
+}
+
+extern "C" {
+
+uint32_t bftsim_two_thirds_majority(uint32_t n) { return (2u * n) / 3u; }
+uint32_t bftsim_seed_from_hash(const uint8_t hash[32], uint32_t n) { return n ? bft::seed_from_hash(hash, n) : 0; }
+uint32_t bftsim_calc_proposer(const uint8_t prev_hash[32], uint32_t n, uint64_t round) {
+    if (n == 0) return 0;
+    return (uint32_t)(((uint64_t)bft::seed_from_hash(prev_hash, n) + round % n) % n);
+}
+void bftsim_keccak256(const uint8_t* data, size_t len, uint8_t out[32]) { host_keccak(data, len, out); }
+void bftsim_genesis_hash(const bftsim_config* cfg, uint8_t out[32]) { host_genesis_hash(cfg, out); }
+int bftsim_view_cmp(uint64_t h1, uint64_t r1, uint64_t h2, uint64_t r2) {
+    if (h1 != h2) return h1 < h2 ? -1 : 1;
+    if (r1 != r2) return r1 < r2 ? -1 : 1;
+    return 0;
+}
+
+const char* bftsim_last_error(bftsim_t* h) { return h ? h->err.c_str() : "null handle"; }
+
+int bftsim_create(const bftsim_config* cfg, int hip_device, bftsim_t** out) {
+    if (!cfg || !out) return BFTSIM_EINVAL;
+    *out = nullptr;
+    if (cfg->n < 1 || cfg->n > 64) return BFTSIM_EUNSUPPORTED;   // GPU path: N <= 64 this round
+    if (cfg->heights < 1 || cfg->heights > (1u << 20) || cfg->max_ticks < 1 || cfg->max_ticks > (1u << 28) ||
+        !cfg->addresses || cfg->phase_cap < 1 || cfg->phase_cap > 255 || cfg->block_period < 1)
+        return BFTSIM_EINVAL;
+    for (uint32_t i = 1; i < cfg->n; ++i)
+        if (memcmp(cfg->addresses + 20 * (i - 1), cfg->addresses + 20 * i, 20) >= 0) return BFTSIM_EINVAL;
+    bftsim* h = new bftsim();
+    h->cfg = *cfg;
+    h->addresses.assign(cfg->addresses, cfg->addresses + 20 * cfg->n);
+    h->cfg.addresses = h->addresses.data();
+    h->device = hip_device;
+    host_genesis_hash(&h->cfg, h->genesis_hash);
+    h->genesis_seed = bft::seed_from_hash(h->genesis_hash, cfg->n);
+    h->seg = bft::segment_size(cfg->n);
+    h->hcap = cfg->heights + 64;
+    *out = h;
+    hipError_t e = hipSetDevice(hip_device);
+    if (e != hipSuccess) return fail(h, BFTSIM_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    HIPCHECK(h, hipMalloc(&h->d_addr, 20 * cfg->n));
+    HIPCHECK(h, hipMemcpy(h->d_addr, h->addresses.data(), 20 * cfg->n, hipMemcpyHostToDevice));
+    HIPCHECK(h, hipMalloc(&h->d_ghash, 32));
+    HIPCHECK(h, hipMemcpy(h->d_ghash, h->genesis_hash, 32, hipMemcpyHostToDevice));
+    HIPCHECK(h, hipMalloc(&h->d_stats, 80 * sizeof(unsigned long long)));
+    for (int i = 0; i < 3; ++i) HIPCHECK(h, hipEventCreate(&h->ev[i]));
+    return BFTSIM_OK;
+}
+
+void bftsim_destroy(bftsim_t* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    free_bufs(h);
+    (void)hipFree(h->d_addr); (void)hipFree(h->d_ghash); (void)hipFree(h->d_stats);
+    for (int i = 0; i < 3; ++i) if (h->ev[i]) (void)hipEventDestroy(h->ev[i]);
+    delete h;
+}
+
+int bftsim_prepare(bftsim_t* h, uint64_t n) {
+    if (!h || n == 0 || n > (1ull << 31)) return fail(h, BFTSIM_EINVAL, "bad instance count");
+    HIPCHECK(h, hipSetDevice(h->device));
+    if (n <= h->cap_inst) return BFTSIM_OK;
+    free_bufs(h);
+    HIPCHECK(h, hipMalloc(&h->d_ch, n * 4));
+    HIPCHECK(h, hipMalloc(&h->d_flags, n * 4));
+    HIPCHECK(h, hipMalloc(&h->d_ticks, n * 4));
+    HIPCHECK(h, hipMalloc(&h->d_views, n * 8));
+    HIPCHECK(h, hipMalloc(&h->d_rec, n * h->hcap * 16));
+    HIPCHECK(h, hipMalloc(&h->d_hash, n * h->hcap * 32));
+    h->cap_inst = n;
+    return BFTSIM_OK;
+}
+
+int bftsim_set_trace(bftsim_t* h, uint64_t* host_out, uint32_t trace_ticks) {
+    if (!h) return BFTSIM_EINVAL;
+    h->h_trace = host_out;
+    h->trace_ticks = host_out ? trace_ticks : 0;
+    return BFTSIM_OK;
+}
+
+static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
+    bft::Params p = bft::params_from_config(h->cfg, h->seg, h->hcap, h->genesis_seed, first, n);
+    p.addresses = h->d_addr;
+    p.genesis_hash = h->d_ghash;
+    p.committed_height = h->d_ch;
+    p.flags = h->d_flags;
+    p.ticks = h->d_ticks;
+    p.views = h->d_views;
+    p.rec = h->d_rec;
+    p.hash = h->d_hash;
+    p.trace = h->d_trace;
+    p.trace_ticks = h->trace_ticks;
+    return p;
+}
+
+int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
+    if (!h || h->cap_inst == 0) return fail(h, BFTSIM_EINVAL, "bftsim_prepare not called");
+    uint64_t n = h->cap_inst;
+    if (first + n > (1ull << 32)) return fail(h, BFTSIM_EINVAL, "instance ids must fit in 32 bits");
+    HIPCHECK(h, hipSetDevice(h->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (h->h_trace) {
+        if (h->d_trace) (void)hipFree(h->d_trace);
+        h->d_trace = nullptr;
+        size_t tb = n * (size_t)h->trace_ticks * h->cfg.n * 8;
+        HIPCHECK(h, hipMalloc(&h->d_trace, tb));
+        HIPCHECK(h, hipMemsetAsync(h->d_trace, 0, tb, s));
+    }
+    bft::Params p = make_params(h, first, n);
+    HIPCHECK(h, hipMemsetAsync(h->d_rec, 0, n * h->hcap * 16, s));
+    uint32_t per_wave = 64u / h->seg;
+    uint32_t grid = (uint32_t)((n + per_wave - 1) / per_wave);
+    HIPCHECK(h, hipEventRecord(h->ev[0], s));
+    if (p.need_seed)
+        hipLaunchKernelGGL(bft::bft_consensus_kernel<true>, dim3(grid), dim3(64), bft::LDS_BYTES_SEED, s, p);
+    else
+        hipLaunchKernelGGL(bft::bft_consensus_kernel<false>, dim3(grid), dim3(64), bft::LDS_BYTES_POW2, s, p);
+    HIPCHECK(h, hipGetLastError());
+    HIPCHECK(h, hipEventRecord(h->ev[1], s));
+    if (!p.need_seed) {
+        uint32_t g2 = (uint32_t)((n + 63) / 64);
+        hipLaunchKernelGGL(bft::bft_hash_kernel, dim3(g2), dim3(64), 64 * bft::SCRATCH_BYTES, s, p);
+        HIPCHECK(h, hipGetLastError());
+    }
+    HIPCHECK(h, hipEventRecord(h->ev[2], s));
+    h->last_n = n;
+    h->last_first = first;
+    h->last_stream = s;
+    return BFTSIM_OK;
+}
+
+int bftsim_sync(bftsim_t* h) {
+    if (!h) return BFTSIM_EINVAL;
+    HIPCHECK(h, hipSetDevice(h->device));
+    HIPCHECK(h, hipStreamSynchronize(h->last_stream));
+    return BFTSIM_OK;
+}
+
+int bftsim_last_kernel_ms(bftsim_t* h, float* cms, float* hms) {
+    if (!h) return BFTSIM_EINVAL;
+    HIPCHECK(h, hipEventSynchronize(h->ev[2]));
+    float a = 0, b = 0;
+    HIPCHECK(h, hipEventElapsedTime(&a, h->ev[0], h->ev[1]));
+    HIPCHECK(h, hipEventElapsedTime(&b, h->ev[1], h->ev[2]));
+    if (cms) *cms = a;
+    if (hms) *hms = b;
+    return BFTSIM_OK;
+}
+
+int bftsim_fetch(bftsim_t* h, bftsim_result* out) {
+    if (!h || !out) return BFTSIM_EINVAL;
+    HIPCHECK(h, hipSetDevice(h->device));
+    HIPCHECK(h, hipStreamSynchronize(h->last_stream));
+    uint64_t n = h->last_n;
+    uint32_t H = h->cfg.heights, hc = h->hcap;
+    HIPCHECK(h, hipMemcpy(out->committed_height, h->d_ch, n * 4, hipMemcpyDeviceToHost));
+    HIPCHECK(h, hipMemcpy(out->flags, h->d_flags, n * 4, hipMemcpyDeviceToHost));
+    HIPCHECK(h, hipMemcpy(out->ticks, h->d_ticks, n * 4, hipMemcpyDeviceToHost));
+    HIPCHECK(h, hipMemcpy(out->views, h->d_views, n * 8, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> rec(n * hc * 4);
+    std::vector<uint8_t> hs(n * hc * 32);
+    HIPCHECK(h, hipMemcpy(rec.data(), h->d_rec, rec.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHECK(h, hipMemcpy(hs.data(), h->d_hash, hs.size(), hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < n; ++i) {
+        uint32_t ch = out->committed_height[i];
+        for (uint32_t x = 1; x <= H; ++x) {
+            uint64_t o = i * H + (x - 1);
+            const uint32_t* row = &rec[(i * hc + x) * 4];
+            bool ok = x <= ch;
+            out->round[o] = ok ? (uint16_t)row[0] : 0;
+            out->proposer[o] = ok ? (uint16_t)(row[1] & 0xffffu) : 0;
+            out->variant[o] = ok ? (uint8_t)((row[1] >> 16) & 1u) : 0;
+            out->time_tick[o] = ok ? row[2] : 0;
+            if (ok) memcpy(out->block_hash + o * 32, &hs[(i * hc + x) * 32], 32);
+            else memset(out->block_hash + o * 32, 0, 32);
+        }
+    }
+    if (h->h_trace && h->d_trace) {
+        size_t tb = n * (size_t)h->trace_ticks * h->cfg.n * 8;
+        HIPCHECK(h, hipMemcpy(h->h_trace, h->d_trace, tb, hipMemcpyDeviceToHost));
+    }
+    return BFTSIM_OK;
+}
+
+int bftsim_run(bftsim_t* h, uint64_t first, uint64_t n, bftsim_result* out) {
+    int rc = bftsim_prepare(h, n);
+    if (rc) return rc;
+    if (h->cap_inst != n) {          // exact-size buffers for a synchronous run
+        free_bufs(h);
+        if ((rc = bftsim_prepare(h, n))) return rc;
+    }
+    if ((rc = bftsim_launch(h, first, nullptr))) return rc;
+    return bftsim_fetch(h, out);
+}
+
+int bftsim_stats_get(bftsim_t* h, bftsim_stats* out) {
+    if (!h || !out || h->last_n == 0) return BFTSIM_EINVAL;
+    HIPCHECK(h, hipSetDevice(h->device));
+    bft::Params p = make_params(h, h->last_first, h->last_n);
+    HIPCHECK(h, hipMemsetAsync(h->d_stats, 0, 80 * 8, h->last_stream));
+    uint32_t g = (uint32_t)((h->last_n + 255) / 256);
+    hipLaunchKernelGGL(bft::bft_stats_kernel, dim3(g), dim3(256), 0, h->last_stream, p, h->d_stats);
+    HIPCHECK(h, hipGetLastError());
+    unsigned long long st[80];
+    HIPCHECK(h, hipMemcpyAsync(st, h->d_stats, sizeof st, hipMemcpyDeviceToHost, h->last_stream));
+    HIPCHECK(h, hipStreamSynchronize(h->last_stream));
+    out->instances = st[0];
+    out->committed_heights = st[1];
+    out->views = st[2];
+    out->ticks = st[3];
+    for (int i = 0; i < 6; ++i) out->flagged[i] = st[4 + i];
+    for (int i = 0; i < 65; ++i) out->round_hist[i] = st[10 + i];
+    return BFTSIM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,115 @@
+/*
+ * bftsim.h — C ABI of libbftsim, the MI355X-native batched PBFT simulator.
+ *
+ * This is the drop-in boundary for the reference's single-instance consensus path: one call runs
+ * many independent, seeded consensus-rs clusters on a gfx950 GPU. The reference interfaces it
+ * replaces (all paths in 2892931976/consensus-rs):
+ *   - `trait Backend` (src/consensus/backend.rs:45-68) + `ImplBackend::{gossip,commit,verify}`
+ *     (backend.rs:140-242): the N Cores of one cluster, their gossip and their chain commits
+ *     become one instance simulated on the GPU;
+ *   - `trait Engine` (src/consensus/consensus.rs:28-38) + `Minner` (src/minner/mod.rs:28-144):
+ *     the height driver becomes the per-instance tick loop;
+ *   - `trait ValidatorSet` / `ImplValidatorSet` (src/consensus/validator.rs:10-159): exported below
+ *     as plain functions (quorum, proposer seed, sorted set);
+ *   - the network entry `HandleMsgFn` (src/p2p/server.rs:45) / `handle_msg_middle`
+ *     (src/consensus/pbft/core/core.rs:50-116): replaced by the seeded delivery schedule
+ *     (SPEC.md §3).
+ * Conventions (mirroring the reference's `Result`): every entry returns 0 on success and a
+ * negative code on failure; `bftsim_last_error` explains the last failure. No exceptions or
+ * panics cross the ABI. A handle is not thread-safe: use one handle per host thread / GPU.
+ * Result buffers are caller-owned.
+ */
+#ifndef BFTSIM_H
+#define BFTSIM_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BFTSIM_OK 0
+#define BFTSIM_EINVAL -1      /* bad configuration / arguments */
+#define BFTSIM_EHIP -2        /* HIP runtime error */
+#define BFTSIM_ENOMEM -3
+#define BFTSIM_EUNSUPPORTED -4
+
+/* result flags (per instance) */
+#define BFTSIM_FLAG_SAFETY 1u        /* two different blocks committed at one height (frozen) */
+#define BFTSIM_FLAG_PHASE_CAP 2u     /* messages dropped at the per-tick phase cap */
+#define BFTSIM_FLAG_CORE_PANIC 4u    /* a Core panicked (core.rs:540 unwrap on no request) */
+#define BFTSIM_FLAG_OUTBOX 8u        /* a second message of one kind in one phase was dropped */
+#define BFTSIM_FLAG_TIMEOUT 16u      /* max_ticks reached before `heights` */
+#define BFTSIM_FLAG_RCS_OVERFLOW 32u /* more round-change rounds than the GPU table holds */
+
+typedef struct bftsim_config {
+    uint32_t n;                  /* validators per instance: 1..64 */
+    uint32_t heights;            /* stop once the canonical chain reaches this height */
+    uint32_t max_ticks;          /* cap on ticks (a tick = block_period = RC timeout) */
+    uint32_t block_period;       /* seconds (examples/c1.toml:6) */
+    uint64_t genesis_time;       /* examples/c1.toml:15 */
+    uint64_t seed;               /* Philox key (SPEC.md §5) */
+    uint32_t drop_ppm;           /* per-link per-phase drop probability */
+    uint32_t byz_count;          /* equivocating validators per instance (SPEC.md §6) */
+    uint32_t proposer_crash_ppm; /* per-view probability that the proposer stays silent */
+    uint32_t phase_cap;          /* max message phases per tick */
+    uint64_t silent_mask[4];     /* validators that never run */
+    const uint8_t *addresses;    /* n*20 bytes, ascending = validator index order */
+    uint8_t genesis_proposer[20];
+    uint64_t genesis_gas_used;
+} bftsim_config;
+
+typedef struct bftsim_result {   /* host buffers, caller-owned; H = config.heights */
+    uint32_t *committed_height;  /* [n_inst] canonical chain length (<= H) */
+    uint32_t *flags;             /* [n_inst] */
+    uint32_t *ticks;             /* [n_inst] ticks used */
+    uint64_t *views;             /* [n_inst] instance-rounds: sum of (commit round + 1) */
+    uint16_t *round;             /* [n_inst*H] round of the first commit of each height */
+    uint16_t *proposer;          /* [n_inst*H] proposer index of the committed block */
+    uint8_t *variant;            /* [n_inst*H] 1 = the equivocated second block */
+    uint32_t *time_tick;         /* [n_inst*H] header.time = genesis + period*(tick+1) */
+    uint8_t *block_hash;         /* [n_inst*H*32] Keccak-256 of the header (block.rs:76-80) */
+} bftsim_result;
+
+typedef struct bftsim_stats {    /* summed over the instances of the last launch */
+    uint64_t instances;
+    uint64_t committed_heights;
+    uint64_t views;              /* instance-rounds */
+    uint64_t ticks;
+    uint64_t flagged[6];         /* instances with each flag bit set */
+    uint64_t round_hist[65];     /* heights committed in round 0..63, [64] = 64+ */
+} bftsim_stats;
+
+typedef struct bftsim bftsim_t;
+
+/* lifecycle */
+int bftsim_create(const bftsim_config *cfg, int hip_device, bftsim_t **out);
+void bftsim_destroy(bftsim_t *h);
+const char *bftsim_last_error(bftsim_t *h);
+
+/* synchronous: run instances [first, first+n) and copy results to host buffers */
+int bftsim_run(bftsim_t *h, uint64_t first_instance, uint64_t n_instances, bftsim_result *out);
+
+/* device-resident API (benchmarks): allocate once, launch many times, fetch on demand */
+int bftsim_prepare(bftsim_t *h, uint64_t n_instances);
+int bftsim_launch(bftsim_t *h, uint64_t first_instance, void *hip_stream);   /* async */
+int bftsim_sync(bftsim_t *h);
+int bftsim_fetch(bftsim_t *h, bftsim_result *out);
+int bftsim_stats_get(bftsim_t *h, bftsim_stats *out);   /* device reduction + copy */
+/* per-kernel device time of the last launch, from HIP events on the launch stream (ms) */
+int bftsim_last_kernel_ms(bftsim_t *h, float *consensus_ms, float *hash_ms);
+/* optional per-tick state digests of the next launch (debug; NULL disables) */
+int bftsim_set_trace(bftsim_t *h, uint64_t *host_out, uint32_t trace_ticks);
+
+/* ValidatorSet / block helpers on the host (validator.rs, types/block.rs) */
+uint32_t bftsim_two_thirds_majority(uint32_t n);                    /* validator.rs:149-154 */
+uint32_t bftsim_seed_from_hash(const uint8_t hash[32], uint32_t n); /* validator.rs:39-48 */
+uint32_t bftsim_calc_proposer(const uint8_t prev_hash[32], uint32_t n, uint64_t round); /* :33-37,74-77 */
+void bftsim_keccak256(const uint8_t *data, size_t len, uint8_t out[32]);
+void bftsim_genesis_hash(const bftsim_config *cfg, uint8_t out[32]); /* core/genesis.rs:44-55 */
+int bftsim_view_cmp(uint64_t h1, uint64_t r1, uint64_t h2, uint64_t r2); /* consensus/types.rs:81-98 */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

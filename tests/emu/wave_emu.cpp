@@ -1,0 +1,196 @@
+// wave_emu.cpp — TEST-ONLY CPU emulation of one 64-lane wavefront running the SAME kernel body
+// (consensus-rs_amd/csrc/bft_wave.h) that the gfx950 kernel runs. Each lane is a ucontext fiber;
+// collectives (ballot, shfl_xor, sync) are rendezvous points where every live lane must arrive at
+// the same collective — a non-uniform collective aborts, which catches divergence bugs before
+// they reach the GPU. Never linked into libbftsim.
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <ucontext.h>
+
+#include <vector>
+
+#include "../../consensus-rs_amd/csrc/bft_host.h"
+#include "../../consensus-rs_amd/csrc/bft_wave.h"
+
+namespace {
+
+struct Sched {
+    ucontext_t main_ctx;
+    ucontext_t ctx[64];
+    std::vector<char> stack[64];
+    bool done[64];
+    int cur;
+    int op[64];
+    uint64_t arg[64];
+    uint64_t res[64];
+    uint64_t seq[64];
+    const bft::Params* P;
+    uint8_t* lds;
+    uint32_t wave;
+};
+thread_local Sched* g = nullptr;
+
+void yield_to_sched() { swapcontext(&g->ctx[g->cur], &g->main_ctx); }
+
+struct EmuWave {
+    static uint32_t lane() { return (uint32_t)g->cur; }
+    static uint64_t ballot(bool p) {
+        int l = g->cur;
+        g->op[l] = 1; g->arg[l] = p ? 1 : 0; g->seq[l]++;
+        yield_to_sched();
+        return g->res[l];
+    }
+    static uint32_t shfl_xor(uint32_t v, int m) {
+        int l = g->cur;
+        g->op[l] = 2; g->arg[l] = (uint64_t)v | ((uint64_t)(uint32_t)m << 32); g->seq[l]++;
+        yield_to_sched();
+        return (uint32_t)g->res[l];
+    }
+    static void sync() {
+        int l = g->cur;
+        g->op[l] = 3; g->seq[l]++;
+        yield_to_sched();
+    }
+    static uint32_t gload(const uint32_t* p) { return *p; }
+    static void gstore(uint32_t* p, uint32_t v) { *p = v; }
+};
+
+void lane_entry(int lane) {
+    if (g->P->need_seed) {
+        bft::Sim<EmuWave, true> sim(*g->P, g->lds, g->wave);
+        sim.run();
+    } else {
+        bft::Sim<EmuWave, false> sim(*g->P, g->lds, g->wave);
+        sim.run();
+    }
+    g->done[lane] = true;
+    g->op[lane] = 0;
+}
+
+int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds) {
+    Sched s;
+    g = &s;
+    s.P = &P;
+    s.lds = lds.data();
+    s.wave = wave;
+    for (int l = 0; l < 64; ++l) {
+        s.done[l] = false;
+        s.op[l] = 0;
+        s.seq[l] = 0;
+        s.stack[l].resize(256 * 1024);
+        getcontext(&s.ctx[l]);
+        s.ctx[l].uc_stack.ss_sp = s.stack[l].data();
+        s.ctx[l].uc_stack.ss_size = s.stack[l].size();
+        s.ctx[l].uc_link = &s.main_ctx;
+        makecontext(&s.ctx[l], (void (*)())lane_entry, 1, l);
+    }
+    for (;;) {
+        for (int l = 0; l < 64; ++l) {
+            if (s.done[l]) continue;
+            s.cur = l;
+            swapcontext(&s.main_ctx, &s.ctx[l]);
+        }
+        int nd = 0;
+        for (int l = 0; l < 64; ++l) nd += s.done[l];
+        if (nd == 64) break;
+        if (nd != 0) { fprintf(stderr, "emu: lanes diverged at a collective (%d done)\n", nd); return -1; }
+        int op = s.op[0];
+        for (int l = 1; l < 64; ++l)
+            if (s.op[l] != op || s.seq[l] != s.seq[0]) {
+                fprintf(stderr, "emu: non-uniform collective (lane %d op %d seq %llu vs op %d seq %llu)\n", l, s.op[l],
+                        (unsigned long long)s.seq[l], op, (unsigned long long)s.seq[0]);
+                return -1;
+            }
+        if (op == 1) {
+            uint64_t m = 0;
+            for (int l = 0; l < 64; ++l) m |= (s.arg[l] & 1ull) << l;
+            for (int l = 0; l < 64; ++l) s.res[l] = m;
+        } else if (op == 2) {
+            for (int l = 0; l < 64; ++l) {
+                int mm = (int)(s.arg[l] >> 32);
+                s.res[l] = (uint32_t)s.arg[l ^ mm];
+            }
+        }
+    }
+    g = nullptr;
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bftsim_result* out,
+                       uint64_t* trace, uint32_t trace_ticks) {
+    if (cfg->n < 1 || cfg->n > 64) return -4;
+    uint8_t gh[32];
+    bft::host_genesis_hash(cfg, gh);
+    uint32_t gseed = bft::seed_from_hash(gh, cfg->n);
+    uint32_t seg = bft::segment_size(cfg->n);
+    uint32_t hcap = cfg->heights + 64;
+    bft::Params P = bft::params_from_config(*cfg, seg, hcap, gseed, first, n);
+    std::vector<uint32_t> ch(n), flags(n), ticks(n);
+    std::vector<uint64_t> views(n);
+    std::vector<uint32_t> rec(n * hcap * 4, 0);
+    std::vector<uint8_t> hs(n * hcap * 32, 0);
+    P.addresses = cfg->addresses;
+    P.genesis_hash = gh;
+    P.committed_height = ch.data();
+    P.flags = flags.data();
+    P.ticks = ticks.data();
+    P.views = views.data();
+    P.rec = rec.data();
+    P.hash = hs.data();
+    P.trace = trace;
+    P.trace_ticks = trace ? trace_ticks : 0;
+    uint32_t per_wave = 64 / seg;
+    uint32_t waves = (uint32_t)((n + per_wave - 1) / per_wave);
+    std::vector<uint8_t> lds(bft::lds_bytes_per_wave(P.need_seed));
+    for (uint32_t w = 0; w < waves; ++w) {
+        memset(lds.data(), 0xcd, lds.size());
+        if (run_wave(P, w, lds)) return -1;
+    }
+    // power-of-two N: the hash post-pass (bft_hash_kernel) on the host
+    if (!P.need_seed) {
+        uint8_t scratch[bft::SCRATCH_BYTES];
+        for (uint64_t il = 0; il < n; ++il) {
+            uint32_t prev[8];
+            for (int i = 0; i < 8; ++i)
+                prev[i] = (uint32_t)gh[4 * i] | ((uint32_t)gh[4 * i + 1] << 8) | ((uint32_t)gh[4 * i + 2] << 16) |
+                          ((uint32_t)gh[4 * i + 3] << 24);
+            bft::Absorb ab;
+            ab.buf = scratch;
+            for (uint32_t x = 1; x <= ch[il]; ++x) {
+                const uint32_t* row = &rec[(il * hcap + x) * 4];
+                uint32_t prop = row[1] & 0xffffu, var = (row[1] >> 16) & 1u;
+                uint64_t time = cfg->genesis_time + (uint64_t)cfg->block_period * ((uint64_t)row[2] + 1ull);
+                uint8_t o[32];
+                bft::block_hash(ab, prev, cfg->addresses + 20u * prop, cfg->seed, (uint32_t)(first + il), x, prop, var,
+                                time, o);
+                memcpy(&hs[(il * hcap + x) * 32], o, 32);
+                for (int i = 0; i < 8; ++i)
+                    prev[i] = (uint32_t)o[4 * i] | ((uint32_t)o[4 * i + 1] << 8) | ((uint32_t)o[4 * i + 2] << 16) |
+                              ((uint32_t)o[4 * i + 3] << 24);
+            }
+        }
+    }
+    uint32_t H = cfg->heights;
+    for (uint64_t i = 0; i < n; ++i) {
+        out->committed_height[i] = ch[i];
+        out->flags[i] = flags[i];
+        out->ticks[i] = ticks[i];
+        out->views[i] = views[i];
+        for (uint32_t x = 1; x <= H; ++x) {
+            uint64_t o = i * H + (x - 1);
+            const uint32_t* row = &rec[(i * hcap + x) * 4];
+            bool ok = x <= ch[i];
+            out->round[o] = ok ? (uint16_t)row[0] : 0;
+            out->proposer[o] = ok ? (uint16_t)(row[1] & 0xffffu) : 0;
+            out->variant[o] = ok ? (uint8_t)((row[1] >> 16) & 1u) : 0;
+            out->time_tick[o] = ok ? row[2] : 0;
+            if (ok) memcpy(out->block_hash + o * 32, &hs[(i * hcap + x) * 32], 32);
+            else memset(out->block_hash + o * 32, 0, 32);
+        }
+    }
+    return 0;
+}

@@ -1,0 +1,54 @@
+"""ctypes wrapper of the CPU wave emulator (tests/emu/libwave_emu.so) — test-only."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "consensus-rs_amd"))
+from bftsim import _abi  # noqa: E402
+
+EMU_DIR = os.path.join(ROOT, "tests", "emu")
+LIB = os.path.join(EMU_DIR, "libwave_emu.so")
+SRCS = [os.path.join(EMU_DIR, "wave_emu.cpp")] + [
+    os.path.join(ROOT, "consensus-rs_amd", "csrc", f) for f in ("bft_wave.h", "bft_common.h", "bft_host.h")]
+
+_lib = None
+
+
+def build():
+    if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(s) for s in SRCS):
+        return
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unknown-pragmas",
+                           "-o", LIB, SRCS[0]])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = ctypes.CDLL(LIB)
+        _lib.emu_run.argtypes = [ctypes.POINTER(_abi.CConfig), ctypes.c_uint64, ctypes.c_uint64,
+                                 ctypes.POINTER(_abi.CResult), ctypes.c_void_p, ctypes.c_uint32]
+    return _lib
+
+
+def run(cfg, first, n_inst, trace_ticks=0):
+    c, keep = _abi.to_cconfig(cfg)
+    r, arrs = _abi.alloc_result(n_inst, cfg.heights)
+    tr = None
+    if trace_ticks:
+        tr = np.zeros(n_inst * trace_ticks * cfg.n, np.uint64)
+    rc = lib().emu_run(ctypes.byref(c), first, n_inst, ctypes.byref(r),
+                       tr.ctypes.data if tr is not None else None, trace_ticks)
+    del keep
+    if rc != 0:
+        raise RuntimeError(f"emu_run failed: {rc}")
+    arrs = _abi.shape_result(arrs, n_inst, cfg.heights)
+    if tr is not None:
+        arrs["trace"] = tr.reshape(n_inst, trace_ticks, cfg.n)
+    return arrs

@@ -1,0 +1,48 @@
+"""GPU parity: the HIP path (libbftsim through the C ABI) against the CPU oracle, bit for bit,
+on the same seeded schedules (SPEC.md). Sizes are chosen so the oracle finishes in seconds."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from bftsim.configs import BftConfig, cfg1, cfg2, cfg3, cfg4, cfg5
+from parity_util import assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_run(cfg, first, n, trace_ticks=0):
+    from bftsim.runtime import Simulator
+    sim = Simulator(cfg)
+    try:
+        return sim.run(first, n, trace_ticks)
+    finally:
+        sim.close()
+
+
+CASES = [
+    ("cfg1-n5", lambda: cfg1(True), 0, 1),
+    ("cfg1-n4", lambda: cfg1(False), 0, 1),
+    ("cfg2", lambda: cfg2(), 0, 256),
+    ("cfg2-tail", lambda: cfg2(), 65_000, 64),
+    ("cfg3", lambda: cfg3(), 0, 48),
+    ("cfg3-tail", lambda: cfg3(), 16_300, 16),
+    ("cfg5", lambda: cfg5(heights=300), 0, 64),
+    ("n4-byz2-unsafe", lambda: BftConfig(n=4, heights=40, seed=9, byz_count=2), 0, 64),
+    ("n7-byz3-drop", lambda: BftConfig(n=7, heights=40, seed=9, byz_count=3, drop_ppm=100_000), 0, 64),
+    ("n10-mix", lambda: BftConfig(n=10, heights=40, seed=11, byz_count=3, drop_ppm=200_000,
+                                  proposer_crash_ppm=200_000), 0, 32),
+    ("n4-cap3", lambda: BftConfig(n=4, heights=40, seed=12, drop_ppm=300_000, phase_cap=3), 0, 64),
+    ("n16-drop40", lambda: BftConfig(n=16, heights=30, seed=13, drop_ppm=400_000), 0, 16),
+    ("n5-2silent", lambda: BftConfig(n=5, heights=30, seed=14, silent=[0, 3]), 0, 8),
+    ("n64-byz21-drop5", lambda: BftConfig(n=64, heights=20, seed=15, byz_count=21, drop_ppm=50_000), 0, 4),
+    ("n1", lambda: BftConfig(n=1, heights=20), 0, 8),
+    ("n2", lambda: BftConfig(n=2, heights=20, drop_ppm=100_000), 0, 8),
+] + [(f"cfg4-n{n}", (lambda n=n: cfg4(n, heights=60)), 0, 24) for n in (4, 7, 10, 16, 31, 32, 33, 63, 64)]
+
+
+@pytest.mark.parametrize("name,mk,first,n", CASES, ids=[c[0] for c in CASES])
+def test_gpu_matches_oracle(name, mk, first, n):
+    cfg = mk()
+    ref = O.run(cfg, first, n)
+    got = gpu_run(cfg, first, n)
+    assert_same(ref, got, name)
