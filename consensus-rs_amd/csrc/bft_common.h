@@ -38,7 +38,7 @@ struct Params {
     uint32_t first_instance;
     uint32_t n_instances;
     uint32_t genesis_seed;
-    uint32_t pad0;
+    uint32_t fast;            // 1: closed-form phase fast paths (0: one message at a time)
     const uint8_t* addresses;         // n*20
     const uint8_t* genesis_hash;      // 32
     // outputs

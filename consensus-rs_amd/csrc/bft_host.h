@@ -84,6 +84,7 @@ inline Params params_from_config(const bftsim_config& c, uint32_t seg, uint32_t 
     p.first_instance = (uint32_t)first;
     p.n_instances = (uint32_t)n;
     p.genesis_seed = genesis_seed;
+    p.fast = 1;
     return p;
 }
 

@@ -66,17 +66,19 @@ constexpr uint32_t LDS_BYTES_POW2 = LDS_CHASH_OFF;
 constexpr uint32_t LDS_BYTES_SEED = LDS_SCR_OFF + 64 * SCRATCH_BYTES;
 BFT_FN uint32_t lds_bytes_per_wave(bool need_seed) { return need_seed ? LDS_BYTES_SEED : LDS_BYTES_POW2; }
 
-template <class W, bool NEED_SEED>
+template <class W, bool NEED_SEED, uint32_t S>
 struct Sim {
     const Params& P;
     uint8_t* lds;
     // identity
-    uint32_t lane, S, seg_base, me, inst_local, inst;
+    uint32_t lane, seg_base, me, inst_local, inst;
     uint64_t seg_mask;       // this segment's bits in a wave ballot
     bool is_val, running, byz, core_dead;
     // segment-uniform
     bool seg_done, frozen;
     uint32_t canon_h, done_tick, seg_flags;
+    uint64_t canon_tip;      // canonical block at canon_h (segment-uniform cache; 0 at genesis)
+    uint32_t canon_tip_seed;
     // Core + RoundState (round_state.rs:12-22)
     uint32_t h, r, st;
     bool wait;
@@ -103,7 +105,6 @@ struct Sim {
 
     BFT_FN Sim(const Params& p, uint8_t* l, uint32_t wave_global) : P(p), lds(l) {
         lane = W::lane();
-        S = p.seg;
         seg_base = lane & ~(S - 1);
         me = lane - seg_base;
         inst_local = wave_global * (64u / S) + (lane / S);
@@ -117,6 +118,8 @@ struct Sim {
         seg_done = !inst_ok;
         frozen = false;
         canon_h = 0;
+        canon_tip = 0;
+        canon_tip_seed = p.genesis_seed;
         done_tick = p.max_ticks;
         seg_flags = 0;
         h = 0; r = 0; st = ST_ACCEPT_REQUEST; wait = false;
@@ -138,9 +141,14 @@ struct Sim {
     // ---------------------------------------------------------------- global canonical table
     BFT_FN uint32_t* rec_row(uint32_t x) const { return P.rec + ((uint64_t)inst_local * P.hcap + x) * 4; }
     BFT_FN uint8_t* hash_row(uint32_t x) const { return P.hash + ((uint64_t)inst_local * P.hcap + x) * 32; }
-    BFT_FN uint32_t canon_seed(uint32_t x) const { return x == 0 ? P.genesis_seed : W::gload(rec_row(x) + 3); }
+    BFT_FN uint32_t canon_seed(uint32_t x) const {
+        if (x == 0) return P.genesis_seed;
+        if (x == canon_h) return canon_tip_seed;
+        return W::gload(rec_row(x) + 3);
+    }
     // canonical block id at x (x >= 1, must be recorded)
     BFT_FN uint64_t canon_blk(uint32_t x) const {
+        if (x == canon_h && x != 0) return canon_tip;
         uint32_t w1 = W::gload(rec_row(x) + 1);
         uint32_t T = W::gload(rec_row(x) + 2);
         return blk_make(x, w1 & 0xffffu, (w1 >> 16) & 1u, T);
@@ -202,8 +210,11 @@ struct Sim {
 
     // the tip moved to a block recorded by an earlier phase: refresh its time tick and seed
     BFT_FN void refresh_tip_from_table() {
-        uint32_t w1 = W::gload(rec_row(last) + 1);
-        (void)w1;
+        if (last == canon_h && canon_h != 0) {            // the common case: tip = canonical tip
+            last_T = (int32_t)blk_T(canon_tip);
+            last_seed = canon_tip_seed;
+            return;
+        }
         last_T = (int32_t)W::gload(rec_row(last) + 2);
         last_seed = W::gload(rec_row(last) + 3);
     }
@@ -514,9 +525,30 @@ struct Sim {
         for (uint32_t m = 1; m < S; m <<= 1) { uint32_t o = W::shfl_xor(v, m); v = v > o ? v : o; }
         return v;
     }
+    BFT_FN uint64_t seg_sum64(uint32_t v32) {
+        uint64_t v = v32;
+        for (uint32_t m = 1; m < S; m <<= 1) {
+            uint32_t lo = W::shfl_xor((uint32_t)v, m), hi = W::shfl_xor((uint32_t)(v >> 32), m);
+            v += (uint64_t)lo | ((uint64_t)hi << 32);
+        }
+        return v;
+    }
     BFT_FN uint32_t seg_or(uint32_t v) {
         for (uint32_t m = 1; m < S; m <<= 1) v |= W::shfl_xor(v, m);
         return v;
+    }
+
+    // record a new canonical height (segment leader; global stores for the outputs)
+    BFT_FN void record_canon(uint32_t x, uint64_t b, uint32_t round, uint32_t seed, const uint32_t* hs) {
+        uint32_t* row = rec_row(x);
+        W::gstore(row + 0, round);
+        W::gstore(row + 2, blk_T(b));
+        W::gstore(row + 3, seed);
+        W::gstore(row + 1, blk_prop(b) | (blk_var(b) << 16) | (1u << 24));
+        if (NEED_SEED) {
+            uint32_t* dst = (uint32_t*)hash_row(x);
+            for (int i = 0; i < 8; ++i) W::gstore(dst + i, hs[i]);
+        }
     }
 
     // first Core commits of the phase → canonical table, in lane order (oracle receiver order)
@@ -532,9 +564,43 @@ struct Sim {
         W::sync();
         uint64_t segbits = bal & seg_mask;
         uint32_t* segw = (uint32_t*)(lds + LDS_SEG_OFF) + (lane / S) * 8;
-        if (segbits != 0 && !seg_done && lane == (uint32_t)__builtin_ctzll(segbits)) {
-            // the segment leader replays the commits of this phase in lane order
+        const bool mine = segbits != 0 && !seg_done;
+        const uint32_t lead = segbits ? (uint32_t)__builtin_ctzll(segbits) : 0u;
+        // fast path: every committer of the segment commits the same height as the first one
+        const uint32_t* cl = (const uint32_t*)(lds + LDS_CMT_OFF) + lead * 8;
+        uint32_t x0 = mine ? cl[0] : 0u;
+        uint64_t b0 = mine ? ((uint64_t)cl[1] | ((uint64_t)cl[2] << 32)) : 0ull;
+        bool other_h = c && mine && commit_x != x0;
+        uint64_t mixed = W::ballot(other_h) & seg_mask;
+        bool uniform = mixed == 0;
+        // canonical block of x0 as it was before this phase (heights are recorded contiguously)
+        bool x0_known = x0 <= canon_h;
+        uint64_t ref = 0;
+        if (mine && uniform) ref = x0_known ? canon_blk(x0) : b0;
+        bool bad = mine && uniform && c && !blk_eq(commit_blk, ref);
+        uint64_t badm = W::ballot(bad) & seg_mask;
+        if (mine && uniform && lane == lead) {
+            // lanes below the first violating lane were processed before the freeze
+            bool fr = badm != 0;
             uint32_t ch = canon_h;
+            uint64_t tip = canon_tip;
+            uint32_t tseed = canon_tip_seed;
+            if (!x0_known && x0 < P.hcap && (!fr || (uint32_t)__builtin_ctzll(badm) > lead)) {
+                record_canon(x0, b0, cl[3], cl[4], (const uint32_t*)(lds + LDS_CHASH_OFF + lead * 32));
+                ch = x0; tip = b0; tseed = cl[4];
+            }
+            if (x0 >= P.hcap) fr = true;
+            segw[0] = ch;
+            segw[1] = fr ? 1u : 0u;
+            segw[2] = (uint32_t)tip;
+            segw[3] = (uint32_t)(tip >> 32);
+            segw[4] = tseed;
+        }
+        if (mine && !uniform && lane == lead) {
+            // general case: replay the commits of this phase in lane order
+            uint32_t ch = canon_h;
+            uint64_t tip = canon_tip;
+            uint32_t tseed = canon_tip_seed;
             bool fr = false;
             uint64_t bits = segbits;
             while (bits != 0) {
@@ -544,29 +610,26 @@ struct Sim {
                 uint32_t x = cj[0];
                 uint64_t b = (uint64_t)cj[1] | ((uint64_t)cj[2] << 32);
                 if (x >= P.hcap) { fr = true; break; }
-                uint32_t* row = rec_row(x);
-                uint32_t w1 = W::gload(row + 1);
-                if (w1 & (1u << 24)) {
-                    if ((w1 & 0xffffu) != blk_prop(b) || ((w1 >> 16) & 1u) != blk_var(b)) { fr = true; break; }
+                if (x <= ch) {
+                    uint64_t cb = (x == ch) ? tip : ((x == canon_h) ? canon_tip : canon_blk(x));
+                    if (!blk_eq(cb, b)) { fr = true; break; }
                 } else {
-                    W::gstore(row + 0, cj[3]);
-                    W::gstore(row + 2, blk_T(b));
-                    W::gstore(row + 3, cj[4]);
-                    W::gstore(row + 1, blk_prop(b) | (blk_var(b) << 16) | (1u << 24));
-                    if (NEED_SEED) {
-                        const uint32_t* hs = (const uint32_t*)(lds + LDS_CHASH_OFF + j * 32);
-                        uint32_t* dst = (uint32_t*)hash_row(x);
-                        for (int i = 0; i < 8; ++i) W::gstore(dst + i, hs[i]);
-                    }
-                    if (x > ch) ch = x;
+                    // x == ch + 1: heights are recorded contiguously
+                    record_canon(x, b, cj[3], cj[4], (const uint32_t*)(lds + LDS_CHASH_OFF + j * 32));
+                    ch = x; tip = b; tseed = cj[4];
                 }
             }
             segw[0] = ch;
             segw[1] = fr ? 1u : 0u;
+            segw[2] = (uint32_t)tip;
+            segw[3] = (uint32_t)(tip >> 32);
+            segw[4] = tseed;
         }
         W::sync();
-        if (segbits != 0 && !seg_done) {
+        if (mine) {
             canon_h = segw[0];
+            canon_tip = (uint64_t)segw[2] | ((uint64_t)segw[3] << 32);
+            canon_tip_seed = segw[4];
             if (segw[1]) { frozen = true; seg_flags |= FLAG_SAFETY; }
         }
         commit_x = 0;
@@ -606,6 +669,188 @@ struct Sim {
         W::sync();
     }
 
+    // ---------------------------------------------------------------- phase fast paths
+    // Segment-wide summary of one phase's messages. All masks use segment-local sender bits.
+    struct PhaseSummary {
+        uint64_t k_pp, k_pr, k_cm, k_ocm, k_rc, k_sync, k_blk;
+        uint64_t pr_v0, pr_v1, pr_w, cm_v0, cm_v1, cm_w;
+        uint32_t pr_h, pr_r, cm_h, cm_r, blk_lo, blk_hi;
+        uint64_t pr_cls, cm_cls;              // (height, proposer) class of the digests
+        bool u_pr, u_cm, u_blk;               // one view / one digest class / one range
+    };
+
+    BFT_FN uint64_t seg_bits(uint64_t bal) const {
+        return S >= 64 ? bal : ((bal >> seg_base) & ((1ull << S) - 1ull));
+    }
+
+    BFT_FN void summarize(PhaseSummary& ps) {
+        uint32_t f = nx.f;
+        ps.k_pp = seg_bits(W::ballot((f & F_PP) != 0));
+        ps.k_pr = seg_bits(W::ballot((f & F_PR) != 0));
+        ps.k_cm = seg_bits(W::ballot((f & F_CM) != 0));
+        ps.k_ocm = seg_bits(W::ballot((f & F_OCM) != 0));
+        ps.k_rc = seg_bits(W::ballot((f & F_RC) != 0));
+        ps.k_sync = seg_bits(W::ballot((f & F_SYNC) != 0));
+        ps.k_blk = seg_bits(W::ballot((f & F_BLK) != 0));
+        bool pr = (f & F_PR) != 0, cm = (f & F_CM) != 0;
+        bool prw = (f & F_PR_W) != 0, cmw = (f & F_CM_W) != 0;
+        ps.pr_w = seg_bits(W::ballot(pr && prw));
+        ps.pr_v0 = seg_bits(W::ballot(pr && !prw && blk_var(nx.pr_d) == 0));
+        ps.pr_v1 = seg_bits(W::ballot(pr && !prw && blk_var(nx.pr_d) == 1));
+        ps.cm_w = seg_bits(W::ballot(cm && cmw));
+        ps.cm_v0 = seg_bits(W::ballot(cm && !cmw && blk_var(nx.cm_d) == 0));
+        ps.cm_v1 = seg_bits(W::ballot(cm && !cmw && blk_var(nx.cm_d) == 1));
+    }
+
+    // after publish + sync: compare every sender with the first sender of its kind
+    BFT_FN void summarize_uniform(PhaseSummary& ps) {
+        const uint32_t* own = rec_lds(lane);
+        uint32_t f = own[0];
+        bool mm_pr = false, mm_cm = false, mm_blk = false;
+        ps.pr_h = ps.pr_r = ps.cm_h = ps.cm_r = ps.blk_lo = ps.blk_hi = 0;
+        ps.pr_cls = ps.cm_cls = 0;
+        if (ps.k_pr) {
+            const uint32_t* L = rec_lds(seg_base + (uint32_t)__builtin_ctzll(ps.k_pr));
+            ps.pr_h = L[5]; ps.pr_r = L[6];
+            ps.pr_cls = ((uint64_t)L[7] | ((uint64_t)L[8] << 32)) & BLK_HP_MASK;
+            uint64_t d = ((uint64_t)own[7] | ((uint64_t)own[8] << 32)) & BLK_HP_MASK;
+            mm_pr = (f & F_PR) && (own[5] != ps.pr_h || own[6] != ps.pr_r || d != ps.pr_cls);
+        }
+        if (ps.k_cm) {
+            const uint32_t* L = rec_lds(seg_base + (uint32_t)__builtin_ctzll(ps.k_cm));
+            ps.cm_h = L[9]; ps.cm_r = L[10];
+            ps.cm_cls = ((uint64_t)L[11] | ((uint64_t)L[12] << 32)) & BLK_HP_MASK;
+            uint64_t d = ((uint64_t)own[11] | ((uint64_t)own[12] << 32)) & BLK_HP_MASK;
+            mm_cm = (f & F_CM) && (own[9] != ps.cm_h || own[10] != ps.cm_r || d != ps.cm_cls);
+        }
+        if (ps.k_blk) {
+            const uint32_t* L = rec_lds(seg_base + (uint32_t)__builtin_ctzll(ps.k_blk));
+            ps.blk_lo = L[20]; ps.blk_hi = L[21];
+            mm_blk = (f & F_BLK) && (own[20] != ps.blk_lo || own[21] != ps.blk_hi);
+        }
+        ps.u_pr = seg_bits(W::ballot(mm_pr)) == 0;
+        ps.u_cm = seg_bits(W::ballot(mm_cm)) == 0;
+        ps.u_blk = seg_bits(W::ballot(mm_blk)) == 0;
+    }
+
+    // rotate a sender mask into this receiver's delivery order (position 0 = first delivered)
+    BFT_FN uint64_t rot(uint64_t m, uint32_t off) const {
+        if (off == 0) return m;
+        uint32_t n = P.n;
+        uint64_t nm = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+        return ((m >> off) | (m << (n - off))) & nm;
+    }
+    BFT_FN static uint64_t low(uint32_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1ull); }
+    // smallest position p in [0,n) with popcount(base | a & low(p+1) | b & low(p)) > q, else n
+    BFT_FN uint32_t first_over(uint64_t base, uint64_t a, uint64_t b, uint32_t q) const {
+        uint32_t n = P.n;
+        if ((uint32_t)__builtin_popcountll(base | a | (b & low(n - 1))) <= q) return n;
+        uint32_t lo = 0, hi = n - 1;                 // answer in [lo, hi]
+        while (lo < hi) {
+            uint32_t mid = (lo + hi) >> 1;
+            if ((uint32_t)__builtin_popcountll(base | (a & low(mid + 1)) | (b & low(mid))) > q) hi = mid;
+            else lo = mid + 1;
+        }
+        return lo;
+    }
+    BFT_FN static uint32_t first_at_or_after(uint64_t m, uint32_t p) {
+        uint64_t x = m & ~low(p);
+        return x ? (uint32_t)__builtin_ctzll(x) : 64u;
+    }
+
+    // digests of the class `cls` that match `target` (wildcards match both variants)
+    BFT_FN static uint64_t class_match(uint64_t cls, uint64_t v0, uint64_t v1, uint64_t w, uint64_t target) {
+        if (!blk_valid(target) || ((cls ^ target) & BLK_HP_MASK) != 0) return 0;
+        return w | (blk_var(target) ? v1 : v0);
+    }
+
+    // A phase that carries only Prepares and Commits, each kind with one view and one digest
+    // class: the sequential handlers of prepare.rs:48-66 and commit.rs:63-82, evaluated in this
+    // receiver's delivery order with prefix masks instead of one message at a time.
+    BFT_FN void deliver_prepare_commit(const PhaseSummary& ps, uint64_t mk, uint32_t off) {
+        uint64_t PRacc = 0, CMacc = 0;
+        uint64_t prd = mk & ps.k_pr, cmd = mk & ps.k_cm;
+        if (prd) {
+            int res = check_message(2, ps.pr_h);
+            if (res != 0) { if (res == 2) note_future_block(ps.pr_h); }
+            else if (ps.pr_h == h && ps.pr_r == r) PRacc = prd;
+        }
+        if (cmd) {
+            int res = check_message(3, ps.cm_h);
+            if (res != 0) { if (res == 2) note_future_block(ps.cm_h); }
+            else if (ps.cm_h == h && ps.cm_r == r) CMacc = cmd & class_match(ps.cm_cls, ps.cm_v0, ps.cm_v1, ps.cm_w, pp);
+        }
+        if (!PRacc && !CMacc) return;
+        const uint32_t q = (2u * P.n) / 3u;
+        uint32_t n = P.n;
+        uint64_t PR = rot(PRacc, off), CM = rot(CMacc, off);
+        uint64_t U0 = rot(prep | comm, off), C0 = rot(comm, off);
+        // first prepare trigger (prepare.rs:54-63)
+        uint32_t tB = 64;
+        if (PR) {
+            uint32_t pstar = first_over(U0, PR, CM, q);
+            if (pstar < n) tB = first_at_or_after(PR, pstar);
+        }
+        uint32_t tA = 64;
+        if (blk_valid(lock) && PR) {
+            uint64_t lm = rot(PRacc & class_match(ps.pr_cls, ps.pr_v0, ps.pr_v1, ps.pr_w, lock), off);
+            if (lm) tA = (uint32_t)__builtin_ctzll(lm);
+        }
+        uint32_t t1 = tA < tB ? tA : tB;
+        bool trig = t1 < 64;
+        uint32_t lastT = 0;
+        if (trig) {
+            uint64_t mpp = rot(PRacc & class_match(ps.pr_cls, ps.pr_v0, ps.pr_v1, ps.pr_w, pp), off);
+            uint64_t T = (tB < 64 ? (PR & ~low(tB)) : 0ull) | (PR & mpp & ~low(t1)) | (1ull << t1);
+            lastT = 63u - (uint32_t)__builtin_clzll(T);
+        }
+        // commit quorum events (commit.rs:75-80): CM positions from tC on
+        uint32_t tC = CM ? first_over(C0, CM, 0, q) : n;
+        bool cexists = tC < n;
+        uint32_t lastCM = CM ? 63u - (uint32_t)__builtin_clzll(CM) : 0u;
+        uint32_t s0 = st;
+        bool fires;          // some commit event runs Core::commit
+        uint32_t fin;
+        if (trig) {
+            bool after = cexists && lastCM >= (tC > lastT ? tC : lastT);
+            fin = after ? ST_COMMITTED : ST_PREPARED;
+            fires = cexists && (s0 < ST_COMMITTED || lastCM >= (tC > t1 ? tC : t1));
+        } else {
+            fires = cexists && s0 < ST_COMMITTED;
+            fin = fires ? ST_COMMITTED : s0;
+        }
+        prep |= PRacc;
+        comm |= CMacc;
+        if (trig) { lock_hash(); send_commit(); }
+        if (fires) { lock_hash(); st = ST_COMMITTED; chain_insert_core(pp); }
+        st = fin;
+    }
+
+    BFT_FN void deliver_phase(const PhaseSummary& ps, uint64_t mk, uint32_t off) {
+        bool other = (ps.k_pp | ps.k_ocm | ps.k_rc | ps.k_sync) != 0;
+        if (P.fast && !other) {
+            if (!ps.k_pr && !ps.k_cm) {
+                if (ps.k_blk && ps.u_blk) {          // block gossip with one range
+                    if (mk & ps.k_blk & ~(1ull << me)) handle_blocks(ps.blk_lo, ps.blk_hi);
+                    return;
+                }
+            } else if (!ps.k_blk && ps.u_pr && ps.u_cm) {
+                if (!core_dead) deliver_prepare_commit(ps, mk, off);
+                return;
+            }
+        }
+        // general path: every delivered non-empty sender, in rotated order, one at a time
+        uint64_t any = ps.k_pp | ps.k_pr | ps.k_cm | ps.k_ocm | ps.k_rc | ps.k_sync | ps.k_blk;
+        uint64_t c = rot(mk & any, off);
+        while (c) {
+            uint32_t pos = (uint32_t)__builtin_ctzll(c);
+            c &= c - 1;
+            uint32_t s = pos + off;
+            if (s >= P.n) s -= P.n;
+            deliver_from(s);
+        }
+    }
+
     // ---------------------------------------------------------------- the run
     BFT_FN void run() {
         if (P.byz_count > 0) init_byzantine();
@@ -625,17 +870,17 @@ struct Sim {
                     outbox_clear(nx);
                     break;
                 }
+                // segment-wide summary of what is in flight (SPEC.md §2 kinds), before publish
+                PhaseSummary ps;
+                summarize(ps);
                 publish();
                 W::sync();
+                summarize_uniform(ps);
                 if (act && seg_pending) {
                     miner_step();                             // event step
                     uint64_t mk = deliver_mask(P.seed, P.n, P.thr16, inst, (uint32_t)tick, p, me);
                     uint32_t off = delivery_offset(P.seed, P.n, inst, (uint32_t)tick, p, me);
-                    for (uint32_t k = 0; k < P.n; ++k) {
-                        uint32_t s = off + k;
-                        if (s >= P.n) s -= P.n;
-                        if ((mk >> s) & 1ull) deliver_from(s);
-                    }
+                    deliver_phase(ps, mk, off);
                 }
                 W::sync();
                 resolve_commits();
@@ -645,14 +890,18 @@ struct Sim {
                 P.trace[((uint64_t)inst_local * P.trace_ticks + (uint32_t)tick) * P.n + me] = state_digest();
             if (!seg_done && (frozen || canon_h >= P.heights)) { seg_done = true; done_tick = (uint32_t)tick + 1; }
         }
-        // outputs (segment lane 0)
+        // outputs (segment lane 0); instance-rounds = sum of (round + 1), loaded lane-parallel
         uint32_t lf = seg_or(lane_flags);
+        uint32_t chv = canon_h < P.heights ? canon_h : P.heights;
+        uint32_t part = 0;
+        if (inst_local < P.n_instances)
+            for (uint32_t x = 1 + me; x <= chv; x += S) part += W::gload(rec_row(x)) + 1u;
+        uint64_t vsum = seg_sum64(part);
         if (me == 0 && inst_local < P.n_instances) {
             uint32_t flags = lf | seg_flags;
             if (!frozen && canon_h < P.heights) flags |= FLAG_TIMEOUT;
             uint32_t chh = canon_h < P.heights ? canon_h : P.heights;
-            uint64_t views = 0;
-            for (uint32_t x = 1; x <= chh; ++x) views += (uint64_t)W::gload(rec_row(x)) + 1ull;
+            uint64_t views = vsum;
             P.committed_height[inst_local] = chh;
             P.flags[inst_local] = flags;
             P.ticks[inst_local] = done_tick;

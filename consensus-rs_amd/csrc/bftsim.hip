@@ -18,6 +18,7 @@
 #include "../../include/bftsim.h"
 #include "bft_common.h"
 #include "bft_wave.h"
+#include "bft_coop_hash.h"
 
 namespace bft {
 
@@ -26,6 +27,7 @@ struct WaveHip {
     __device__ static uint32_t lane() { return __lane_id(); }
     __device__ static uint64_t ballot(bool p) { return __ballot(p); }
     __device__ static uint32_t shfl_xor(uint32_t v, int m) { return (uint32_t)__shfl_xor((int)v, m, 64); }
+    __device__ static uint32_t shfl(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src, 64); }
     __device__ static void sync() {
         // LDS traffic of one wave is processed in order; this orders the compiler's view and
         // drains outstanding LDS operations before other lanes read what this lane wrote.
@@ -41,13 +43,31 @@ struct WaveHip {
     }
 };
 
-template <bool NEED_SEED>
+template <bool NEED_SEED, uint32_t S>
 __global__ __launch_bounds__(64) void bft_consensus_kernel(Params p) {
     extern __shared__ uint8_t lds[];
-    Sim<WaveHip, NEED_SEED> sim(p, lds, blockIdx.x);
+    Sim<WaveHip, NEED_SEED, S> sim(p, lds, blockIdx.x);
     sim.run();
 }
 
+template <bool NEED_SEED>
+static void launch_consensus(uint32_t seg, dim3 grid, size_t lds, hipStream_t s, const Params& p) {
+    switch (seg) {
+        case 4: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 4>), grid, dim3(64), lds, s, p); break;
+        case 8: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 8>), grid, dim3(64), lds, s, p); break;
+        case 16: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 16>), grid, dim3(64), lds, s, p); break;
+        case 32: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 32>), grid, dim3(64), lds, s, p); break;
+        default: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 64>), grid, dim3(64), lds, s, p); break;
+    }
+}
+
+// one wave per instance: the cooperative Keccak of bft_coop_hash.h
+__global__ __launch_bounds__(64) void bft_hash_coop_kernel(Params p) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[COOP_BUF_BYTES];
+    hash_chain_wave<WaveHip>(p, blockIdx.x, buf);
+}
+
+// one lane per instance (kept for reference / A-B timing)
 __global__ __launch_bounds__(64) void bft_hash_kernel(Params p) {
     extern __shared__ uint8_t lds[];
     uint32_t il = blockIdx.x * 64u + threadIdx.x;
@@ -259,15 +279,12 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     uint32_t per_wave = 64u / h->seg;
     uint32_t grid = (uint32_t)((n + per_wave - 1) / per_wave);
     HIPCHECK(h, hipEventRecord(h->ev[0], s));
-    if (p.need_seed)
-        hipLaunchKernelGGL(bft::bft_consensus_kernel<true>, dim3(grid), dim3(64), bft::LDS_BYTES_SEED, s, p);
-    else
-        hipLaunchKernelGGL(bft::bft_consensus_kernel<false>, dim3(grid), dim3(64), bft::LDS_BYTES_POW2, s, p);
+    if (p.need_seed) bft::launch_consensus<true>(h->seg, dim3(grid), bft::LDS_BYTES_SEED, s, p);
+    else bft::launch_consensus<false>(h->seg, dim3(grid), bft::LDS_BYTES_POW2, s, p);
     HIPCHECK(h, hipGetLastError());
     HIPCHECK(h, hipEventRecord(h->ev[1], s));
     if (!p.need_seed) {
-        uint32_t g2 = (uint32_t)((n + 63) / 64);
-        hipLaunchKernelGGL(bft::bft_hash_kernel, dim3(g2), dim3(64), 64 * bft::SCRATCH_BYTES, s, p);
+        hipLaunchKernelGGL(bft::bft_hash_coop_kernel, dim3((uint32_t)n), dim3(64), 0, s, p);
         HIPCHECK(h, hipGetLastError());
     }
     HIPCHECK(h, hipEventRecord(h->ev[2], s));

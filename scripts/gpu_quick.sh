@@ -1,0 +1,11 @@
+#!/bin/bash
+# parity (pytest -m gpu) then a short bench without the CPU leg (used through gpurun)
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -x -q -m gpu > gpurun_out/gpu_parity.log 2>&1 && \
+timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/bench.json 2> gpurun_out/bench.err
+rc=$?
+tail -3 gpurun_out/gpu_parity.log
+cat gpurun_out/bench.json
+exit $rc

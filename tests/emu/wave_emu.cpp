@@ -13,6 +13,7 @@
 
 #include "../../consensus-rs_amd/csrc/bft_host.h"
 #include "../../consensus-rs_amd/csrc/bft_wave.h"
+#include "../../consensus-rs_amd/csrc/bft_coop_hash.h"
 
 namespace {
 
@@ -29,6 +30,7 @@ struct Sched {
     const bft::Params* P;
     uint8_t* lds;
     uint32_t wave;
+    int body;   // 0 consensus, 1 hash post-pass
 };
 thread_local Sched* g = nullptr;
 
@@ -48,6 +50,12 @@ struct EmuWave {
         yield_to_sched();
         return (uint32_t)g->res[l];
     }
+    static uint32_t shfl(uint32_t v, uint32_t src) {
+        int l = g->cur;
+        g->op[l] = 4; g->arg[l] = (uint64_t)v | ((uint64_t)(src & 63u) << 32); g->seq[l]++;
+        yield_to_sched();
+        return (uint32_t)g->res[l];
+    }
     static void sync() {
         int l = g->cur;
         g->op[l] = 3; g->seq[l]++;
@@ -57,21 +65,42 @@ struct EmuWave {
     static void gstore(uint32_t* p, uint32_t v) { *p = v; }
 };
 
-void lane_entry(int lane) {
-    if (g->P->need_seed) {
-        bft::Sim<EmuWave, true> sim(*g->P, g->lds, g->wave);
-        sim.run();
-    } else {
-        bft::Sim<EmuWave, false> sim(*g->P, g->lds, g->wave);
-        sim.run();
+template <bool NS, uint32_t S>
+void run_sim() {
+    bft::Sim<EmuWave, NS, S> sim(*g->P, g->lds, g->wave);
+    sim.run();
+}
+template <bool NS>
+void run_sim_s(uint32_t seg) {
+    switch (seg) {
+        case 4: run_sim<NS, 4>(); break;
+        case 8: run_sim<NS, 8>(); break;
+        case 16: run_sim<NS, 16>(); break;
+        case 32: run_sim<NS, 32>(); break;
+        default: run_sim<NS, 64>(); break;
     }
+}
+void run_sim_seg(bool ns, uint32_t seg) {
+    if (ns) run_sim_s<true>(seg);
+    else run_sim_s<false>(seg);
+}
+
+void lane_entry(int lane) {
+    if (g->body == 1) {
+        bft::hash_chain_wave<EmuWave>(*g->P, g->wave, g->lds);
+        g->done[lane] = true;
+        g->op[lane] = 0;
+        return;
+    }
+    run_sim_seg(g->P->need_seed != 0, g->P->seg);
     g->done[lane] = true;
     g->op[lane] = 0;
 }
 
-int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds) {
+int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds, int body = 0) {
     Sched s;
     g = &s;
+    s.body = body;
     s.P = &P;
     s.lds = lds.data();
     s.wave = wave;
@@ -107,6 +136,8 @@ int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds) {
             uint64_t m = 0;
             for (int l = 0; l < 64; ++l) m |= (s.arg[l] & 1ull) << l;
             for (int l = 0; l < 64; ++l) s.res[l] = m;
+        } else if (op == 4) {
+            for (int l = 0; l < 64; ++l) s.res[l] = (uint32_t)s.arg[(int)(s.arg[l] >> 32)];
         } else if (op == 2) {
             for (int l = 0; l < 64; ++l) {
                 int mm = (int)(s.arg[l] >> 32);
@@ -129,6 +160,7 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
     uint32_t seg = bft::segment_size(cfg->n);
     uint32_t hcap = cfg->heights + 64;
     bft::Params P = bft::params_from_config(*cfg, seg, hcap, gseed, first, n);
+    if (getenv("BFT_EMU_SLOW")) P.fast = 0;
     std::vector<uint32_t> ch(n), flags(n), ticks(n);
     std::vector<uint64_t> views(n);
     std::vector<uint32_t> rec(n * hcap * 4, 0);
@@ -150,29 +182,11 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
         memset(lds.data(), 0xcd, lds.size());
         if (run_wave(P, w, lds)) return -1;
     }
-    // power-of-two N: the hash post-pass (bft_hash_kernel) on the host
+    // power-of-two N: the cooperative hash post-pass (bft_hash_coop_kernel), one wave per instance
     if (!P.need_seed) {
-        uint8_t scratch[bft::SCRATCH_BYTES];
-        for (uint64_t il = 0; il < n; ++il) {
-            uint32_t prev[8];
-            for (int i = 0; i < 8; ++i)
-                prev[i] = (uint32_t)gh[4 * i] | ((uint32_t)gh[4 * i + 1] << 8) | ((uint32_t)gh[4 * i + 2] << 16) |
-                          ((uint32_t)gh[4 * i + 3] << 24);
-            bft::Absorb ab;
-            ab.buf = scratch;
-            for (uint32_t x = 1; x <= ch[il]; ++x) {
-                const uint32_t* row = &rec[(il * hcap + x) * 4];
-                uint32_t prop = row[1] & 0xffffu, var = (row[1] >> 16) & 1u;
-                uint64_t time = cfg->genesis_time + (uint64_t)cfg->block_period * ((uint64_t)row[2] + 1ull);
-                uint8_t o[32];
-                bft::block_hash(ab, prev, cfg->addresses + 20u * prop, cfg->seed, (uint32_t)(first + il), x, prop, var,
-                                time, o);
-                memcpy(&hs[(il * hcap + x) * 32], o, 32);
-                for (int i = 0; i < 8; ++i)
-                    prev[i] = (uint32_t)o[4 * i] | ((uint32_t)o[4 * i + 1] << 8) | ((uint32_t)o[4 * i + 2] << 16) |
-                              ((uint32_t)o[4 * i + 3] << 24);
-            }
-        }
+        std::vector<uint8_t> buf(bft::COOP_BUF_BYTES + 64);
+        for (uint64_t il = 0; il < n; ++il)
+            if (run_wave(P, (uint32_t)il, buf, 1)) return -1;
     }
     uint32_t H = cfg->heights;
     for (uint64_t i = 0; i < n; ++i) {

@@ -1,0 +1,46 @@
+"""Randomized parity fuzz: CPU wave emulator (the kernel body) vs the oracle on random configs.
+Usage: python tests/fuzz_parity.py [seconds]. Test-only tool (not collected by pytest)."""
+import random
+import sys
+import time
+
+import oracle_lib as O
+import emu_lib as E
+from bftsim.configs import BftConfig
+from parity_util import mismatches
+
+
+def random_config(rng):
+    n = rng.choice([1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 16, 17, 21, 31, 32, 33, 40, 63, 64])
+    byz = rng.choice([0, 0, 0, 1, n // 3, max(0, (n - 1) // 3), n // 2])
+    drop = rng.choice([0, 0, 20_000, 100_000, 250_000, 500_000])
+    crash = rng.choice([0, 0, 100_000, 400_000])
+    cap = rng.choice([16, 16, 4, 2, 8])
+    silent = rng.sample(range(n), k=rng.choice([0, 0, 1, min(2, n)])) if n > 1 else []
+    heights = rng.choice([5, 20, 40])
+    return BftConfig(n=n, heights=heights, seed=rng.randrange(1 << 40), byz_count=byz,
+                     drop_ppm=drop, proposer_crash_ppm=crash, phase_cap=cap, silent=silent,
+                     max_ticks=heights * 4 + 16, name=f"n{n}-b{byz}-d{drop}-c{crash}-cap{cap}-s{len(silent)}")
+
+
+def main():
+    budget = float(sys.argv[1]) if len(sys.argv) > 1 else 60
+    rng = random.Random(int(sys.argv[2]) if len(sys.argv) > 2 else 1234)
+    t0, runs, fails = time.time(), 0, 0
+    while time.time() - t0 < budget:
+        cfg = random_config(rng)
+        first = rng.randrange(1 << 20)
+        n_inst = rng.choice([1, 3, 8])
+        a = O.run(cfg, first, n_inst)
+        b = E.run(cfg, first, n_inst)
+        bad = mismatches(a, b)
+        runs += 1
+        if bad:
+            fails += 1
+            print("MISMATCH", cfg, first, n_inst, bad, flush=True)
+    print(f"fuzz: {runs} configs, {fails} mismatches", flush=True)
+    sys.exit(1 if fails else 0)
+
+
+if __name__ == "__main__":
+    main()
