@@ -158,9 +158,7 @@ BFT_FN bool proposer_crashed(uint64_t seed, uint32_t thr32, uint32_t on, uint32_
 }
 
 // ---------------------------------------------------------------------------------------------
-// Keccak-256 over the MessagePack header (SPEC.md §7). The absorber keeps the 25-word state in
-// registers and stages one 136-byte rate block in a caller-provided byte buffer (LDS on the
-// device) so that variable-length encodings never index registers dynamically.
+// Keccak-256 over the MessagePack header (SPEC.md §7).
 // ---------------------------------------------------------------------------------------------
 BFT_FN uint64_t rotl64(uint64_t x, int n) { return (x << n) | (x >> (64 - n)); }
 
@@ -172,6 +170,7 @@ BFT_FN void keccak_f1600(uint64_t a[25]) {
         0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull, 0x8000000000008003ull,
         0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
         0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+#pragma unroll 1
     for (int rnd = 0; rnd < 24; ++rnd) {
         uint64_t c0 = a[0] ^ a[5] ^ a[10] ^ a[15] ^ a[20];
         uint64_t c1 = a[1] ^ a[6] ^ a[11] ^ a[16] ^ a[21];
@@ -221,76 +220,6 @@ BFT_FN void keccak_f1600(uint64_t a[25]) {
     }
 }
 
-// Streaming absorber: bytes go to buf[0..136); a full block is xored into the state.
-struct Absorb {
-    uint64_t a[25];
-    uint8_t* buf;   // 136 bytes (+8 slack)
-    uint32_t pos;
-};
-
-BFT_FN void absorb_init(Absorb& s, uint8_t* buf) {
-#pragma unroll
-    for (int i = 0; i < 25; ++i) s.a[i] = 0;
-    s.buf = buf;
-    s.pos = 0;
-}
-BFT_FN void absorb_block(Absorb& s) {
-#pragma unroll
-    for (int i = 0; i < 17; ++i) {
-        uint64_t w = 0;
-#pragma unroll
-        for (int b = 0; b < 8; ++b) w |= (uint64_t)s.buf[8 * i + b] << (8 * b);
-        s.a[i] ^= w;
-    }
-    keccak_f1600(s.a);
-    s.pos = 0;
-}
-BFT_FN void absorb_byte(Absorb& s, uint32_t byte) {
-    s.buf[s.pos] = (uint8_t)byte;
-    s.pos += 1;
-    if (s.pos == 136) absorb_block(s);
-}
-BFT_FN void absorb_finish(Absorb& s, uint8_t out[32]) {
-    // pad10*1 with the Keccak domain byte 0x01
-    uint32_t p = s.pos;
-    for (uint32_t i = p; i < 136; ++i) s.buf[i] = 0;
-    s.buf[p] ^= 0x01;
-    s.buf[135] ^= 0x80;
-    absorb_block(s);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int b = 0; b < 8; ++b) out[8 * i + b] = (uint8_t)(s.a[i] >> (8 * b));
-}
-
-// MessagePack pieces (compact uint, byte arrays as arrays of uints, fixed str8 address)
-BFT_FN void mp_uint(Absorb& s, uint64_t v) {
-    if (v < 128) { absorb_byte(s, (uint32_t)v); return; }
-    if (v < 256) { absorb_byte(s, 0xcc); absorb_byte(s, (uint32_t)v); return; }
-    if (v < 65536) { absorb_byte(s, 0xcd); absorb_byte(s, (uint32_t)(v >> 8) & 0xff); absorb_byte(s, (uint32_t)v & 0xff); return; }
-    if (v < 4294967296ull) {
-        absorb_byte(s, 0xce);
-        for (int i = 0; i < 4; ++i) absorb_byte(s, (uint32_t)(v >> (24 - 8 * i)) & 0xff);
-        return;
-    }
-    absorb_byte(s, 0xcf);
-    for (int i = 0; i < 8; ++i) absorb_byte(s, (uint32_t)(v >> (56 - 8 * i)) & 0xff);
-}
-BFT_FN void mp_u8(Absorb& s, uint32_t b) {
-    if (b < 128) absorb_byte(s, b);
-    else { absorb_byte(s, 0xcc); absorb_byte(s, b); }
-}
-BFT_FN void mp_hash_words(Absorb& s, const uint32_t w[8]) {   // 32 bytes, little-endian words
-    absorb_byte(s, 0xdc); absorb_byte(s, 0x00); absorb_byte(s, 0x20);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) mp_u8(s, (w[i] >> (8 * b)) & 0xffu);
-}
-BFT_FN void mp_zero_hash(Absorb& s) {
-    absorb_byte(s, 0xdc); absorb_byte(s, 0x00); absorb_byte(s, 0x20);
-    for (int i = 0; i < 32; ++i) absorb_byte(s, 0);
-}
 BFT_FN uint32_t hexdigit(uint32_t x) { return x < 10 ? 48u + x : 87u + x; }
 
 // tx_hash words of a candidate (SPEC.md §5, domain TX)
@@ -299,36 +228,87 @@ BFT_FN void tx_hash_words(uint64_t seed, uint32_t inst, uint32_t h, uint32_t pro
     philox(seed, inst, h, (prop << 8) | var, DOM_TX2, w + 4);
 }
 
-// Candidate block hash (SPEC.md §7): prev_hash (8 LE words), proposer address (20 bytes).
-BFT_FN void block_hash(Absorb& s, const uint32_t prev[8], const uint8_t* addr20, uint64_t seed,
-                       uint32_t inst, uint32_t h, uint32_t prop, uint32_t var, uint64_t time,
-                       uint8_t out[32]) {
-    s.pos = 0;
-#pragma unroll
-    for (int i = 0; i < 25; ++i) s.a[i] = 0;
-    absorb_byte(s, 0x9d);
-    mp_hash_words(s, prev);
-    absorb_byte(s, 0xd9); absorb_byte(s, 42); absorb_byte(s, '0'); absorb_byte(s, 'x');
-    for (int i = 0; i < 20; ++i) {
-        uint32_t b = addr20[i];
-        absorb_byte(s, hexdigit(b >> 4));
-        absorb_byte(s, hexdigit(b & 15));
+constexpr uint32_t LANE_HASH_BUF = 408;    // 3 rate blocks; the header is at most 274 bytes
+
+// one header field byte of a 32-byte hash as a MessagePack uint (0xcc prefix for >= 128)
+BFT_FN uint32_t put_u8(uint8_t* buf, uint32_t k, uint32_t b) {
+    if (b >= 128u) buf[k++] = 0xcc;
+    buf[k++] = (uint8_t)b;
+    return k;
+}
+BFT_FN uint32_t put_uint(uint8_t* buf, uint32_t k, uint64_t v) {
+    if (v < 128) { buf[k++] = (uint8_t)v; return k; }
+    if (v < 256) { buf[k++] = 0xcc; buf[k++] = (uint8_t)v; return k; }
+    if (v < 65536) { buf[k++] = 0xcd; buf[k++] = (uint8_t)(v >> 8); buf[k++] = (uint8_t)v; return k; }
+    if (v < 4294967296ull) {
+        buf[k++] = 0xce;
+        for (int i = 0; i < 4; ++i) buf[k++] = (uint8_t)(v >> (24 - 8 * i));
+        return k;
     }
-    mp_zero_hash(s);                       // root
+    buf[k++] = 0xcf;
+    for (int i = 0; i < 8; ++i) buf[k++] = (uint8_t)(v >> (56 - 8 * i));
+    return k;
+}
+
+// Keccak-256 of a candidate header (SPEC.md §7) by ONE lane: the whole MessagePack encoding is
+// written to `buf` (LANE_HASH_BUF bytes, 8-aligned; LDS on the device), then absorbed block by
+// block from a single call site, so the permutation is instantiated once (compact code).
+// prev/out: the hash as 8 little-endian words.
+BFT_FN void lane_block_hash(uint8_t* buf, const uint32_t prev[8], const uint8_t* addr20, uint64_t seed,
+                            uint32_t inst, uint32_t h, uint32_t prop, uint32_t var, uint64_t time,
+                            uint32_t out[8]) {
+    uint32_t k = 0;
+    buf[k++] = 0x9d;                                   // 13 serialized fields
+    buf[k++] = 0xdc; buf[k++] = 0x00; buf[k++] = 0x20; // prev_hash
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) k = put_u8(buf, k, (prev[i] >> (8 * b)) & 0xffu);
+    buf[k++] = 0xd9; buf[k++] = 42; buf[k++] = '0'; buf[k++] = 'x';   // proposer
+#pragma unroll 1
+    for (int i = 0; i < 20; ++i) {
+        uint32_t ab = addr20[i];
+        buf[k++] = (uint8_t)hexdigit(ab >> 4);
+        buf[k++] = (uint8_t)hexdigit(ab & 15u);
+    }
+    buf[k++] = 0xdc; buf[k++] = 0x00; buf[k++] = 0x20; // root
+#pragma unroll 1
+    for (int i = 0; i < 32; ++i) buf[k++] = 0;
     uint32_t tx[8];
     tx_hash_words(seed, inst, h, prop, var, tx);
-    mp_hash_words(s, tx);                  // tx_hash
-    mp_zero_hash(s);                       // receipt_hash
-    absorb_byte(s, 0); absorb_byte(s, 0);  // bloom, difficulty
-    mp_uint(s, h);
-    absorb_byte(s, 0); absorb_byte(s, 0);  // gas_limit, gas_used
-    mp_uint(s, time);
-    // extra = "Coinse base" (minner/mod.rs:113) as an array of 11 uints
-    const char* ex = "Coinse base";
-    absorb_byte(s, 0x9b);
-    for (int i = 0; i < 11; ++i) absorb_byte(s, (uint32_t)(uint8_t)ex[i]);
-    absorb_byte(s, 0xc0);                  // votes: None
-    absorb_finish(s, out);
+    buf[k++] = 0xdc; buf[k++] = 0x00; buf[k++] = 0x20; // tx_hash
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) k = put_u8(buf, k, (tx[i] >> (8 * b)) & 0xffu);
+    buf[k++] = 0xdc; buf[k++] = 0x00; buf[k++] = 0x20; // receipt_hash
+#pragma unroll 1
+    for (int i = 0; i < 32; ++i) buf[k++] = 0;
+    buf[k++] = 0; buf[k++] = 0;                        // bloom, difficulty
+    k = put_uint(buf, k, h);
+    buf[k++] = 0; buf[k++] = 0;                        // gas_limit, gas_used
+    k = put_uint(buf, k, time);
+    buf[k++] = 0x9b;                                   // extra = "Coinse base" (minner/mod.rs:113)
+    buf[k++] = 'C'; buf[k++] = 'o'; buf[k++] = 'i'; buf[k++] = 'n'; buf[k++] = 's'; buf[k++] = 'e';
+    buf[k++] = ' '; buf[k++] = 'b'; buf[k++] = 'a'; buf[k++] = 's'; buf[k++] = 'e';
+    buf[k++] = 0xc0;                                   // votes: None
+    const uint32_t nb = k / 136u + 1u;                 // pad10*1 with domain byte 0x01
+#pragma unroll 1
+    for (uint32_t i = k; i < 136u * nb; ++i) buf[i] = 0;
+    buf[k] ^= 0x01;
+    buf[136u * nb - 1u] ^= 0x80;
+    uint64_t a[25];
+#pragma unroll
+    for (int i = 0; i < 25; ++i) a[i] = 0;
+#pragma unroll 1
+    for (uint32_t blk = 0; blk < nb; ++blk) {
+        const uint64_t* w = (const uint64_t*)(buf + 136u * blk);
+#pragma unroll
+        for (int i = 0; i < 17; ++i) a[i] ^= w[i];
+        keccak_f1600(a);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { out[2 * i] = (uint32_t)a[i]; out[2 * i + 1] = (uint32_t)(a[i] >> 32); }
 }
 
 // randon_seed (validator.rs:39-48): (BE64(hash[0..8]) * 2^64) mod n

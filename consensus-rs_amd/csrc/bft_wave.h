@@ -19,7 +19,6 @@ namespace bft {
 
 constexpr int RCS_K = 8;                 // RoundChangeSet rounds kept per validator (LDS)
 constexpr int REC_WORDS = 22;            // LDS words per published outbox record
-constexpr int SCRATCH_BYTES = 144;       // per-lane Keccak rate buffer (136 + slack)
 
 // outbox record flags
 constexpr uint32_t F_PP = 1u, F_PP_EQ = 2u, F_PR = 4u, F_PR_W = 8u, F_CM = 16u, F_CM_W = 32u,
@@ -55,7 +54,7 @@ BFT_FN void outbox_clear(Outbox& o) {
 //   [.., + 16*8*4)                    per-segment shared words
 //   need_seed only:
 //   [.., + 64*32)                     per-lane commit hash
-//   [.., + 64*SCRATCH_BYTES)          per-lane Keccak rate buffer
+//   [.., + 64*LANE_HASH_BUF)          per-lane header buffer of lane_block_hash
 constexpr uint32_t LDS_REC_OFF = 0;
 constexpr uint32_t LDS_RC_OFF = LDS_REC_OFF + 64 * REC_WORDS * 4;
 constexpr uint32_t LDS_CMT_OFF = LDS_RC_OFF + 3 * RCS_K * 64 * 4;
@@ -63,7 +62,7 @@ constexpr uint32_t LDS_SEG_OFF = LDS_CMT_OFF + 64 * 8 * 4;
 constexpr uint32_t LDS_CHASH_OFF = LDS_SEG_OFF + 16 * 8 * 4;
 constexpr uint32_t LDS_SCR_OFF = LDS_CHASH_OFF + 64 * 32;
 constexpr uint32_t LDS_BYTES_POW2 = LDS_CHASH_OFF;
-constexpr uint32_t LDS_BYTES_SEED = LDS_SCR_OFF + 64 * SCRATCH_BYTES;
+constexpr uint32_t LDS_BYTES_SEED = LDS_SCR_OFF + 64 * LANE_HASH_BUF;
 BFT_FN uint32_t lds_bytes_per_wave(bool need_seed) { return need_seed ? LDS_BYTES_SEED : LDS_BYTES_POW2; }
 
 template <class W, bool NEED_SEED, uint32_t S>
@@ -230,16 +229,17 @@ struct Sim {
         commit_round = r;
         uint32_t sd = 0;
         if (NEED_SEED) {
-            uint32_t prev[8];
+            uint32_t prev[8], out[8];
             prev_hash_words(last, prev);
-            Absorb ab;
-            ab.buf = lds + LDS_SCR_OFF + lane * SCRATCH_BYTES;
-            uint8_t out[32];
             uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
-            block_hash(ab, prev, P.addresses + 20u * blk_prop(b), P.seed, inst, x, blk_prop(b), blk_var(b), time, out);
-            uint8_t* hs = lds + LDS_CHASH_OFF + lane * 32;
-            for (int i = 0; i < 32; ++i) hs[i] = out[i];
-            sd = seed_from_hash(out, P.n);
+            lane_block_hash(lds + LDS_SCR_OFF + lane * LANE_HASH_BUF, prev, P.addresses + 20u * blk_prop(b),
+                            P.seed, inst, x, blk_prop(b), blk_var(b), time, out);
+            uint32_t* hs = (uint32_t*)(lds + LDS_CHASH_OFF + lane * 32);
+            uint8_t hb[8];
+            for (int i = 0; i < 8; ++i) hs[i] = out[i];
+            for (int i = 0; i < 2; ++i)
+                for (int q = 0; q < 4; ++q) hb[4 * i + q] = (uint8_t)(out[i] >> (8 * q));
+            sd = seed_from_hash(hb, P.n);
         }
         commit_seed = sd;
         last = x;

@@ -67,9 +67,9 @@ __global__ __launch_bounds__(64) void bft_hash_coop_kernel(Params p) {
     hash_chain_wave<WaveHip>(p, blockIdx.x, buf);
 }
 
-// one lane per instance (kept for reference / A-B timing)
-__global__ __launch_bounds__(64) void bft_hash_kernel(Params p) {
-    extern __shared__ uint8_t lds[];
+// one lane per instance: the compact single-lane Keccak of bft_common.h
+__global__ __launch_bounds__(64) void bft_hash_lane_kernel(Params p) {
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[64 * LANE_HASH_BUF];
     uint32_t il = blockIdx.x * 64u + threadIdx.x;
     if (il >= p.n_instances) return;
     uint32_t inst = p.first_instance + il;
@@ -78,22 +78,16 @@ __global__ __launch_bounds__(64) void bft_hash_kernel(Params p) {
     for (int i = 0; i < 8; ++i)
         prev[i] = (uint32_t)p.genesis_hash[4 * i] | ((uint32_t)p.genesis_hash[4 * i + 1] << 8) |
                   ((uint32_t)p.genesis_hash[4 * i + 2] << 16) | ((uint32_t)p.genesis_hash[4 * i + 3] << 24);
-    Absorb ab;
-    ab.buf = lds + threadIdx.x * SCRATCH_BYTES;
+    uint8_t* buf = bufs + threadIdx.x * LANE_HASH_BUF;
     for (uint32_t x = 1; x <= ch; ++x) {
         const uint32_t* row = p.rec + ((uint64_t)il * p.hcap + x) * 4;
         uint32_t w1 = row[1];
         uint32_t prop = w1 & 0xffffu, var = (w1 >> 16) & 1u, T = row[2];
         uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)T + 1ull);
-        uint8_t out[32];
-        block_hash(ab, prev, p.addresses + 20u * prop, p.seed, inst, x, prop, var, time, out);
+        uint32_t out[8];
+        lane_block_hash(buf, prev, p.addresses + 20u * prop, p.seed, inst, x, prop, var, time, out);
         uint32_t* dst = (uint32_t*)(p.hash + ((uint64_t)il * p.hcap + x) * 32);
-        for (int i = 0; i < 8; ++i) {
-            uint32_t w = (uint32_t)out[4 * i] | ((uint32_t)out[4 * i + 1] << 8) | ((uint32_t)out[4 * i + 2] << 16) |
-                         ((uint32_t)out[4 * i + 3] << 24);
-            dst[i] = w;
-            prev[i] = w;
-        }
+        for (int i = 0; i < 8; ++i) { dst[i] = out[i]; prev[i] = out[i]; }
     }
 }
 
@@ -147,6 +141,7 @@ struct bftsim {
     uint64_t last_n = 0, last_first = 0;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     hipStream_t last_stream = nullptr;
+    int hash_mode = 0;   // 0: one lane per instance, 1: one wave per instance (BFTSIM_HASH=coop)
 };
 
 static int fail(bftsim* h, int code, const std::string& msg) {
@@ -203,6 +198,10 @@ int bftsim_create(const bftsim_config* cfg, int hip_device, bftsim_t** out) {
     h->genesis_seed = bft::seed_from_hash(h->genesis_hash, cfg->n);
     h->seg = bft::segment_size(cfg->n);
     h->hcap = cfg->heights + 64;
+    {
+        const char* hm = getenv("BFTSIM_HASH");
+        h->hash_mode = (hm && strcmp(hm, "coop") == 0) ? 1 : 0;
+    }
     *out = h;
     hipError_t e = hipSetDevice(hip_device);
     if (e != hipSuccess) return fail(h, BFTSIM_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
@@ -284,7 +283,10 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     HIPCHECK(h, hipGetLastError());
     HIPCHECK(h, hipEventRecord(h->ev[1], s));
     if (!p.need_seed) {
-        hipLaunchKernelGGL(bft::bft_hash_coop_kernel, dim3((uint32_t)n), dim3(64), 0, s, p);
+        if (h->hash_mode == 1)
+            hipLaunchKernelGGL(bft::bft_hash_coop_kernel, dim3((uint32_t)n), dim3(64), 0, s, p);
+        else
+            hipLaunchKernelGGL(bft::bft_hash_lane_kernel, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s, p);
         HIPCHECK(h, hipGetLastError());
     }
     HIPCHECK(h, hipEventRecord(h->ev[2], s));

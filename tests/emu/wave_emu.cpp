@@ -182,11 +182,33 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
         memset(lds.data(), 0xcd, lds.size());
         if (run_wave(P, w, lds)) return -1;
     }
-    // power-of-two N: the cooperative hash post-pass (bft_hash_coop_kernel), one wave per instance
+    // power-of-two N: the hash post-pass, as bft_hash_coop_kernel (one wave per instance,
+    // BFTSIM_HASH=coop) or bft_hash_lane_kernel (one lane per instance, default)
     if (!P.need_seed) {
-        std::vector<uint8_t> buf(bft::COOP_BUF_BYTES + 64);
-        for (uint64_t il = 0; il < n; ++il)
-            if (run_wave(P, (uint32_t)il, buf, 1)) return -1;
+        const char* hm = getenv("BFTSIM_HASH");
+        if (hm && strcmp(hm, "coop") == 0) {
+            std::vector<uint8_t> buf(bft::COOP_BUF_BYTES + 64);
+            for (uint64_t il = 0; il < n; ++il)
+                if (run_wave(P, (uint32_t)il, buf, 1)) return -1;
+        } else {
+            alignas(16) uint8_t buf[bft::LANE_HASH_BUF];
+            for (uint64_t il = 0; il < n; ++il) {
+                uint32_t prev[8];
+                for (int i = 0; i < 8; ++i)
+                    prev[i] = (uint32_t)gh[4 * i] | ((uint32_t)gh[4 * i + 1] << 8) | ((uint32_t)gh[4 * i + 2] << 16) |
+                              ((uint32_t)gh[4 * i + 3] << 24);
+                for (uint32_t x = 1; x <= ch[il]; ++x) {
+                    const uint32_t* row = &rec[(il * hcap + x) * 4];
+                    uint32_t prop = row[1] & 0xffffu, var = (row[1] >> 16) & 1u;
+                    uint64_t time = cfg->genesis_time + (uint64_t)cfg->block_period * ((uint64_t)row[2] + 1ull);
+                    uint32_t out[8];
+                    bft::lane_block_hash(buf, prev, cfg->addresses + 20u * prop, cfg->seed, (uint32_t)(first + il), x,
+                                         prop, var, time, out);
+                    memcpy(&hs[(il * hcap + x) * 32], out, 32);
+                    for (int i = 0; i < 8; ++i) prev[i] = out[i];
+                }
+            }
+        }
     }
     uint32_t H = cfg->heights;
     for (uint64_t i = 0; i < n; ++i) {
