@@ -1,0 +1,51 @@
+"""Multi-GPU plumbing: instances are independent, so ranks shard them with no data-path
+collective; only the per-run statistics are all-reduced (RCCL over xGMI with the `nccl`
+backend, gloo on CPU). SURVEY.md §8(e)."""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+STAT_KEYS = ("instances", "committed_heights", "views", "ticks")
+
+
+def weak_shard(rank: int, per_rank: int) -> Tuple[int, int]:
+    """Weak scaling: rank r simulates instance ids [r*I, (r+1)*I)."""
+    return rank * per_rank, per_rank
+
+
+def strong_shard(rank: int, world: int, total: int) -> Tuple[int, int]:
+    """Strong scaling: a fixed total split into contiguous near-equal ranges."""
+    base, rem = divmod(total, world)
+    first = rank * base + min(rank, rem)
+    return first, base + (1 if rank < rem else 0)
+
+
+def stats_vector(st: Dict) -> list:
+    return [st[k] for k in STAT_KEYS] + list(st["flagged"]) + list(st["round_hist"])
+
+
+def all_reduce_stats(st: Dict, device=None) -> Dict:
+    """Sum a bftsim_stats dict over all ranks of the default process group."""
+    import torch
+    import torch.distributed as dist
+    v = torch.tensor(stats_vector(st), dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(v)
+    v = [int(x) for x in v.tolist()]
+    out = dict(zip(STAT_KEYS, v[:4]))
+    out["flagged"] = v[4:10]
+    out["round_hist"] = v[10:75]
+    return out
+
+
+def stats_from_result(r) -> Dict:
+    """The bftsim_stats of a result dict (host arrays), as bft_stats_kernel computes it."""
+    import numpy as np
+    ch = r["committed_height"]
+    hist = [0] * 65
+    for i in range(len(ch)):
+        for x in r["round"][i][: ch[i]]:
+            hist[min(int(x), 64)] += 1
+    return dict(instances=len(ch), committed_heights=int(ch.sum()), views=int(r["views"].sum()),
+                ticks=int(r["ticks"].sum()),
+                flagged=[int(((r["flags"] >> b) & 1).sum()) for b in range(6)], round_hist=hist)

@@ -42,6 +42,8 @@ def lib():
         L.bftsim_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
         L.bftsim_two_thirds_majority.restype = ctypes.c_uint32
         L.bftsim_seed_from_hash.restype = ctypes.c_uint32
+        L.bftsim_seed_from_hash.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
+        L.bftsim_two_thirds_majority.argtypes = [ctypes.c_uint32]
         L.bftsim_calc_proposer.restype = ctypes.c_uint32
         L.bftsim_calc_proposer.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint64]
         L.bftsim_keccak256.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p]

@@ -473,14 +473,17 @@ struct Sim {
     // ---------------------------------------------------------------- phase machinery
     BFT_FN uint32_t* rec_lds(uint32_t l) const { return (uint32_t*)(lds + LDS_REC_OFF) + l * REC_WORDS; }
 
-    BFT_FN void publish() {      // nx → LDS (this lane's slot), clear nx
+    BFT_FN void publish() {      // nx → LDS (this lane's slot; only the kinds present), clear nx
         uint32_t* o = rec_lds(lane);
-        o[0] = nx.f;
-        o[1] = nx.pp_h; o[2] = nx.pp_r; o[3] = (uint32_t)nx.pp_b; o[4] = (uint32_t)(nx.pp_b >> 32);
-        o[5] = nx.pr_h; o[6] = nx.pr_r; o[7] = (uint32_t)nx.pr_d; o[8] = (uint32_t)(nx.pr_d >> 32);
-        o[9] = nx.cm_h; o[10] = nx.cm_r; o[11] = (uint32_t)nx.cm_d; o[12] = (uint32_t)(nx.cm_d >> 32);
-        o[13] = nx.ocm_h; o[14] = nx.ocm_r; o[15] = (uint32_t)nx.ocm_d; o[16] = (uint32_t)(nx.ocm_d >> 32);
-        o[17] = nx.rc_h; o[18] = nx.rc_r; o[19] = nx.sync_h; o[20] = nx.blk_lo; o[21] = nx.blk_hi;
+        const uint32_t f = nx.f;
+        o[0] = f;
+        if (f & F_PP) { o[1] = nx.pp_h; o[2] = nx.pp_r; o[3] = (uint32_t)nx.pp_b; o[4] = (uint32_t)(nx.pp_b >> 32); }
+        if (f & F_PR) { o[5] = nx.pr_h; o[6] = nx.pr_r; o[7] = (uint32_t)nx.pr_d; o[8] = (uint32_t)(nx.pr_d >> 32); }
+        if (f & F_CM) { o[9] = nx.cm_h; o[10] = nx.cm_r; o[11] = (uint32_t)nx.cm_d; o[12] = (uint32_t)(nx.cm_d >> 32); }
+        if (f & F_OCM) { o[13] = nx.ocm_h; o[14] = nx.ocm_r; o[15] = (uint32_t)nx.ocm_d; o[16] = (uint32_t)(nx.ocm_d >> 32); }
+        if (f & F_RC) { o[17] = nx.rc_h; o[18] = nx.rc_r; }
+        if (f & F_SYNC) o[19] = nx.sync_h;
+        if (f & F_BLK) { o[20] = nx.blk_lo; o[21] = nx.blk_hi; }
         outbox_clear(nx);
     }
 
@@ -683,8 +686,14 @@ struct Sim {
         return S >= 64 ? bal : ((bal >> seg_base) & ((1ull << S) - 1ull));
     }
 
+    // value of lane (seg_base + j) — j is uniform within the segment
+    BFT_FN uint32_t from_seg_lane(uint32_t v, uint32_t j) const {
+        if (S >= 64) return W::readlane(v, j);
+        return W::shfl(v, seg_base + j);
+    }
+
     BFT_FN void summarize(PhaseSummary& ps) {
-        uint32_t f = nx.f;
+        const uint32_t f = nx.f;
         ps.k_pp = seg_bits(W::ballot((f & F_PP) != 0));
         ps.k_pr = seg_bits(W::ballot((f & F_PR) != 0));
         ps.k_cm = seg_bits(W::ballot((f & F_CM) != 0));
@@ -692,45 +701,48 @@ struct Sim {
         ps.k_rc = seg_bits(W::ballot((f & F_RC) != 0));
         ps.k_sync = seg_bits(W::ballot((f & F_SYNC) != 0));
         ps.k_blk = seg_bits(W::ballot((f & F_BLK) != 0));
-        bool pr = (f & F_PR) != 0, cm = (f & F_CM) != 0;
-        bool prw = (f & F_PR_W) != 0, cmw = (f & F_CM_W) != 0;
-        ps.pr_w = seg_bits(W::ballot(pr && prw));
-        ps.pr_v0 = seg_bits(W::ballot(pr && !prw && blk_var(nx.pr_d) == 0));
-        ps.pr_v1 = seg_bits(W::ballot(pr && !prw && blk_var(nx.pr_d) == 1));
-        ps.cm_w = seg_bits(W::ballot(cm && cmw));
-        ps.cm_v0 = seg_bits(W::ballot(cm && !cmw && blk_var(nx.cm_d) == 0));
-        ps.cm_v1 = seg_bits(W::ballot(cm && !cmw && blk_var(nx.cm_d) == 1));
-    }
-
-    // after publish + sync: compare every sender with the first sender of its kind
-    BFT_FN void summarize_uniform(PhaseSummary& ps) {
-        const uint32_t* own = rec_lds(lane);
-        uint32_t f = own[0];
-        bool mm_pr = false, mm_cm = false, mm_blk = false;
+        const bool pr = (f & F_PR) != 0, cm = (f & F_CM) != 0, bk = (f & F_BLK) != 0;
+        const bool prw = (f & F_PR_W) != 0, cmw = (f & F_CM_W) != 0;
         ps.pr_h = ps.pr_r = ps.cm_h = ps.cm_r = ps.blk_lo = ps.blk_hi = 0;
         ps.pr_cls = ps.cm_cls = 0;
-        if (ps.k_pr) {
-            const uint32_t* L = rec_lds(seg_base + (uint32_t)__builtin_ctzll(ps.k_pr));
-            ps.pr_h = L[5]; ps.pr_r = L[6];
-            ps.pr_cls = ((uint64_t)L[7] | ((uint64_t)L[8] << 32)) & BLK_HP_MASK;
-            uint64_t d = ((uint64_t)own[7] | ((uint64_t)own[8] << 32)) & BLK_HP_MASK;
-            mm_pr = (f & F_PR) && (own[5] != ps.pr_h || own[6] != ps.pr_r || d != ps.pr_cls);
+        ps.pr_w = ps.pr_v0 = ps.pr_v1 = ps.cm_w = ps.cm_v0 = ps.cm_v1 = 0;
+        ps.u_pr = ps.u_cm = ps.u_blk = true;
+        // leader of each kind (the first sender of the segment) and uniformity against it
+        uint64_t any_pr = W::ballot(pr), any_cm = W::ballot(cm), any_bk = W::ballot(bk);
+        bool mm_pr = false, mm_cm = false, mm_blk = false;
+        if (any_pr) {
+            uint32_t j = ps.k_pr ? (uint32_t)__builtin_ctzll(ps.k_pr) : 0u;
+            uint64_t cls = nx.pr_d & BLK_HP_MASK;
+            ps.pr_h = from_seg_lane(nx.pr_h, j);
+            ps.pr_r = from_seg_lane(nx.pr_r, j);
+            ps.pr_cls = (uint64_t)from_seg_lane((uint32_t)cls, j) | ((uint64_t)from_seg_lane((uint32_t)(cls >> 32), j) << 32);
+            mm_pr = pr && (nx.pr_h != ps.pr_h || nx.pr_r != ps.pr_r || cls != ps.pr_cls);
+            ps.pr_w = seg_bits(W::ballot(pr && prw));
+            ps.pr_v0 = seg_bits(W::ballot(pr && !prw && blk_var(nx.pr_d) == 0));
+            ps.pr_v1 = seg_bits(W::ballot(pr && !prw && blk_var(nx.pr_d) == 1));
         }
-        if (ps.k_cm) {
-            const uint32_t* L = rec_lds(seg_base + (uint32_t)__builtin_ctzll(ps.k_cm));
-            ps.cm_h = L[9]; ps.cm_r = L[10];
-            ps.cm_cls = ((uint64_t)L[11] | ((uint64_t)L[12] << 32)) & BLK_HP_MASK;
-            uint64_t d = ((uint64_t)own[11] | ((uint64_t)own[12] << 32)) & BLK_HP_MASK;
-            mm_cm = (f & F_CM) && (own[9] != ps.cm_h || own[10] != ps.cm_r || d != ps.cm_cls);
+        if (any_cm) {
+            uint32_t j = ps.k_cm ? (uint32_t)__builtin_ctzll(ps.k_cm) : 0u;
+            uint64_t cls = nx.cm_d & BLK_HP_MASK;
+            ps.cm_h = from_seg_lane(nx.cm_h, j);
+            ps.cm_r = from_seg_lane(nx.cm_r, j);
+            ps.cm_cls = (uint64_t)from_seg_lane((uint32_t)cls, j) | ((uint64_t)from_seg_lane((uint32_t)(cls >> 32), j) << 32);
+            mm_cm = cm && (nx.cm_h != ps.cm_h || nx.cm_r != ps.cm_r || cls != ps.cm_cls);
+            ps.cm_w = seg_bits(W::ballot(cm && cmw));
+            ps.cm_v0 = seg_bits(W::ballot(cm && !cmw && blk_var(nx.cm_d) == 0));
+            ps.cm_v1 = seg_bits(W::ballot(cm && !cmw && blk_var(nx.cm_d) == 1));
         }
-        if (ps.k_blk) {
-            const uint32_t* L = rec_lds(seg_base + (uint32_t)__builtin_ctzll(ps.k_blk));
-            ps.blk_lo = L[20]; ps.blk_hi = L[21];
-            mm_blk = (f & F_BLK) && (own[20] != ps.blk_lo || own[21] != ps.blk_hi);
+        if (any_bk) {
+            uint32_t j = ps.k_blk ? (uint32_t)__builtin_ctzll(ps.k_blk) : 0u;
+            ps.blk_lo = from_seg_lane(nx.blk_lo, j);
+            ps.blk_hi = from_seg_lane(nx.blk_hi, j);
+            mm_blk = bk && (nx.blk_lo != ps.blk_lo || nx.blk_hi != ps.blk_hi);
         }
-        ps.u_pr = seg_bits(W::ballot(mm_pr)) == 0;
-        ps.u_cm = seg_bits(W::ballot(mm_cm)) == 0;
-        ps.u_blk = seg_bits(W::ballot(mm_blk)) == 0;
+        if (any_pr | any_cm | any_bk) {
+            ps.u_pr = seg_bits(W::ballot(mm_pr)) == 0;
+            ps.u_cm = seg_bits(W::ballot(mm_cm)) == 0;
+            ps.u_blk = seg_bits(W::ballot(mm_blk)) == 0;
+        }
     }
 
     // rotate a sender mask into this receiver's delivery order (position 0 = first delivered)
@@ -785,40 +797,49 @@ struct Sim {
         uint32_t n = P.n;
         uint64_t PR = rot(PRacc, off), CM = rot(CMacc, off);
         uint64_t U0 = rot(prep | comm, off), C0 = rot(comm, off);
-        // first prepare trigger (prepare.rs:54-63)
-        uint32_t tB = 64;
-        if (PR) {
-            uint32_t pstar = first_over(U0, PR, CM, q);
-            if (pstar < n) tB = first_at_or_after(PR, pstar);
-        }
-        uint32_t tA = 64;
-        if (blk_valid(lock) && PR) {
-            uint64_t lm = rot(PRacc & class_match(ps.pr_cls, ps.pr_v0, ps.pr_v1, ps.pr_w, lock), off);
-            if (lm) tA = (uint32_t)__builtin_ctzll(lm);
-        }
-        uint32_t t1 = tA < tB ? tA : tB;
-        bool trig = t1 < 64;
-        uint32_t lastT = 0;
+        const uint32_t lastPR = PR ? 63u - (uint32_t)__builtin_clzll(PR) : 0u;
+        const uint32_t lastCM = CM ? 63u - (uint32_t)__builtin_clzll(CM) : 0u;
+        // prepare triggers (prepare.rs:54-63). B fires at some prepare iff it fires at the last
+        // one (|prep ∪ commit| only grows); commits of the last prepare's sender come after it.
+        const bool trigB = PR && (uint32_t)__builtin_popcountll(U0 | PR | (CM & low(lastPR))) > q;
+        uint64_t lm = 0;
+        if (blk_valid(lock) && PR) lm = rot(PRacc & class_match(ps.pr_cls, ps.pr_v0, ps.pr_v1, ps.pr_w, lock), off);
+        const bool trig = trigB || lm != 0;
+        // commit quorum events (commit.rs:75-80) exist iff the final count is over q
+        const bool cexists = CM && (uint32_t)__builtin_popcountll(C0 | CM) > q;
+        uint32_t lastT = 0, t1 = 64;
         if (trig) {
-            uint64_t mpp = rot(PRacc & class_match(ps.pr_cls, ps.pr_v0, ps.pr_v1, ps.pr_w, pp), off);
-            uint64_t T = (tB < 64 ? (PR & ~low(tB)) : 0ull) | (PR & mpp & ~low(t1)) | (1ull << t1);
-            lastT = 63u - (uint32_t)__builtin_clzll(T);
+            if (lm) t1 = (uint32_t)__builtin_ctzll(lm);
+            if (trigB) {
+                lastT = lastPR;                                 // every prepare from tB on
+            } else {
+                // lock-match triggers only: the first one locks pp, later ones match pp
+                uint64_t mpp = rot(PRacc & class_match(ps.pr_cls, ps.pr_v0, ps.pr_v1, ps.pr_w, pp), off);
+                uint64_t T = (mpp & ~low(t1)) | (1ull << t1);
+                lastT = 63u - (uint32_t)__builtin_clzll(T);
+            }
         }
-        // commit quorum events (commit.rs:75-80): CM positions from tC on
-        uint32_t tC = CM ? first_over(C0, CM, 0, q) : n;
-        bool cexists = tC < n;
-        uint32_t lastCM = CM ? 63u - (uint32_t)__builtin_clzll(CM) : 0u;
-        uint32_t s0 = st;
+        const uint32_t s0 = st;
         bool fires;          // some commit event runs Core::commit
         uint32_t fin;
         if (trig) {
-            bool after = cexists && lastCM >= (tC > lastT ? tC : lastT);
-            fin = after ? ST_COMMITTED : ST_PREPARED;
-            fires = cexists && (s0 < ST_COMMITTED || lastCM >= (tC > t1 ? tC : t1));
+            fin = (cexists && lastCM >= lastT) ? ST_COMMITTED : ST_PREPARED;
+            if (s0 < ST_COMMITTED) {
+                fires = cexists;
+            } else {
+                // already committed: a re-commit needs a commit event after the first trigger
+                if (trigB) {
+                    uint32_t pstar = first_over(U0, PR, CM, q);
+                    uint32_t tB = first_at_or_after(PR, pstar);
+                    if (tB < t1) t1 = tB;
+                }
+                fires = cexists && lastCM >= t1;
+            }
         } else {
             fires = cexists && s0 < ST_COMMITTED;
             fin = fires ? ST_COMMITTED : s0;
         }
+        (void)n;
         prep |= PRacc;
         comm |= CMacc;
         if (trig) { lock_hash(); send_commit(); }
@@ -875,7 +896,6 @@ struct Sim {
                 summarize(ps);
                 publish();
                 W::sync();
-                summarize_uniform(ps);
                 if (act && seg_pending) {
                     miner_step();                             // event step
                     uint64_t mk = deliver_mask(P.seed, P.n, P.thr16, inst, (uint32_t)tick, p, me);

@@ -28,6 +28,9 @@ struct WaveHip {
     __device__ static uint64_t ballot(bool p) { return __ballot(p); }
     __device__ static uint32_t shfl_xor(uint32_t v, int m) { return (uint32_t)__shfl_xor((int)v, m, 64); }
     __device__ static uint32_t shfl(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src, 64); }
+    __device__ static uint32_t readlane(uint32_t v, uint32_t l) {      // l wave-uniform
+        return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_amdgcn_readfirstlane((int)l));
+    }
     __device__ static void sync() {
         // LDS traffic of one wave is processed in order; this orders the compiler's view and
         // drains outstanding LDS operations before other lanes read what this lane wrote.

@@ -56,6 +56,7 @@ struct EmuWave {
         yield_to_sched();
         return (uint32_t)g->res[l];
     }
+    static uint32_t readlane(uint32_t v, uint32_t src) { return shfl(v, src); }
     static void sync() {
         int l = g->cur;
         g->op[l] = 3; g->seq[l]++;

@@ -51,6 +51,11 @@ def lib():
         _lib.orc_two_thirds_majority.restype = ctypes.c_uint32
         _lib.orc_seed_from_hash.restype = ctypes.c_uint32
         _lib.orc_encode_header.restype = ctypes.c_size_t
+        _lib.orc_encode_header.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                           ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                           ctypes.c_char_p, ctypes.c_size_t]
+        _lib.orc_seed_from_hash.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
+        _lib.orc_two_thirds_majority.argtypes = [ctypes.c_uint32]
     return _lib
 
 

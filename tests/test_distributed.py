@@ -1,0 +1,63 @@
+"""Multi-rank path on CPU (gloo, world_size 2): ranks shard instances with no data-path
+collective and all-reduce the statistics; the reduced stats equal a single-process run."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from bftsim.distributed import strong_shard, weak_shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "consensus-rs_amd"))
+    import torch.distributed as dist
+    import oracle_lib as O
+    from bftsim.configs import cfg2
+    from bftsim.distributed import all_reduce_stats, stats_from_result, weak_shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    first, n = weak_shard(rank, 8)
+    st = stats_from_result(O.run(cfg2(heights=15), first, n))
+    tot = all_reduce_stats(st)
+    if rank == 0:
+        q.put(tot)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_helpers():
+    assert weak_shard(3, 100) == (300, 100)
+    parts = [strong_shard(r, 3, 10) for r in range(3)]
+    assert parts == [(0, 4), (4, 3), (7, 3)]
+    assert sum(n for _, n in parts) == 10
+
+
+def test_gloo_world2_stats_equal_single_process():
+    import oracle_lib as O
+    from bftsim.configs import cfg2
+    from bftsim.distributed import stats_from_result
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    tot = q.get(timeout=120)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    single = stats_from_result(O.run(cfg2(heights=15), 0, 16))
+    assert tot == single

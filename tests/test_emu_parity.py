@@ -1,0 +1,43 @@
+"""The HIP kernel body (bft_wave.h, bft_coop_hash.h) run by the CPU wave emulator against the
+oracle, bit for bit: both hash post-passes, closed-form fast paths on and off, all segment sizes."""
+import pytest
+
+import oracle_lib as O
+import emu_lib as E
+from bftsim.configs import BftConfig, cfg1, cfg2, cfg3, cfg4, cfg5
+from parity_util import assert_same
+
+CASES = [
+    ("cfg1-n5", lambda: cfg1(True, heights=40), 0, 1),
+    ("cfg2", lambda: cfg2(heights=25), 0, 16),
+    ("cfg3", lambda: cfg3(heights=10), 0, 2),
+    ("cfg4-n10", lambda: cfg4(10, heights=25), 3, 8),
+    ("cfg4-n33", lambda: cfg4(33, heights=15), 3, 2),
+    ("cfg5", lambda: cfg5(heights=40), 0, 8),
+    ("n7-byz3-drop", lambda: BftConfig(n=7, heights=25, seed=9, byz_count=3, drop_ppm=100_000), 0, 8),
+    ("n4-cap2-drop30", lambda: BftConfig(n=4, heights=25, seed=12, drop_ppm=300_000, phase_cap=2), 0, 16),
+    ("n16-crash-drop", lambda: BftConfig(n=16, heights=15, seed=21, drop_ppm=150_000,
+                                         proposer_crash_ppm=300_000), 0, 4),
+]
+
+
+@pytest.mark.parametrize("name,mk,first,n", CASES, ids=[c[0] for c in CASES])
+def test_emulated_kernel_matches_oracle(name, mk, first, n):
+    cfg = mk()
+    assert_same(O.run(cfg, first, n), E.run(cfg, first, n), name)
+
+
+@pytest.mark.parametrize("mode", ["coop", "lane"])
+def test_both_hash_postpasses(mode, monkeypatch):
+    monkeypatch.setenv("BFTSIM_HASH", mode)
+    cfg = cfg2(heights=15)
+    assert_same(O.run(cfg, 100, 4), E.run(cfg, 100, 4), mode)
+
+
+def test_fast_paths_off_is_identical(monkeypatch):
+    cfg = BftConfig(n=8, heights=20, seed=33, drop_ppm=120_000, byz_count=2)
+    fast = E.run(cfg, 0, 8)
+    monkeypatch.setenv("BFT_EMU_SLOW", "1")
+    slow = E.run(cfg, 0, 8)
+    assert_same(fast, slow, "fast vs one-message-at-a-time")
+    assert_same(O.run(cfg, 0, 8), slow, "oracle vs slow")
