@@ -12,7 +12,7 @@ from . import _abi
 from .configs import BftConfig
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "build", "libbftsim.so")
+LIB_PATH = os.environ.get("BFTSIM_LIB") or os.path.join(PKG_DIR, "build", "libbftsim.so")
 
 _lib = None
 

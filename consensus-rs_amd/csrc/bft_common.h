@@ -51,6 +51,7 @@ struct Params {
     uint64_t* trace;                  // optional [n_inst][trace_ticks][n] state digests
     uint32_t trace_ticks;
     uint32_t pad1;
+    uint64_t* stamps;                 // diagnostic builds only (BFT_STAMPS): [waves][8] cycles per section
 };
 
 // flags (same bits as the oracle)

@@ -101,6 +101,13 @@ struct Sim {
     uint32_t commit_x, commit_round, commit_seed;
     uint64_t commit_blk;
     uint32_t lane_flags;
+#ifdef BFT_STAMPS
+    uint64_t st_acc[12];
+    uint64_t st_t;
+#define BFT_STAMP(k) do { uint64_t t_ = W::clock(); st_acc[k] += t_ - st_t; st_t = t_; } while (0)
+#else
+#define BFT_STAMP(k) do { } while (0)
+#endif
 
     BFT_FN Sim(const Params& p, uint8_t* l, uint32_t wave_global) : P(p), lds(l) {
         lane = W::lane();
@@ -853,10 +860,12 @@ struct Sim {
             if (!ps.k_pr && !ps.k_cm) {
                 if (ps.k_blk && ps.u_blk) {          // block gossip with one range
                     if (mk & ps.k_blk & ~(1ull << me)) handle_blocks(ps.blk_lo, ps.blk_hi);
+                    BFT_STAMP(8);
                     return;
                 }
             } else if (!ps.k_blk && ps.u_pr && ps.u_cm) {
                 if (!core_dead) deliver_prepare_commit(ps, mk, off);
+                BFT_STAMP(9);
                 return;
             }
         }
@@ -870,15 +879,22 @@ struct Sim {
             if (s >= P.n) s -= P.n;
             deliver_from(s);
         }
+        BFT_STAMP(10);
     }
 
     // ---------------------------------------------------------------- the run
     BFT_FN void run() {
+#ifdef BFT_STAMPS
+        for (int k = 0; k < 12; ++k) st_acc[k] = 0;
+        st_t = W::clock();
+#endif
         if (P.byz_count > 0) init_byzantine();
         for (tick = 0; tick < (int32_t)P.max_ticks; ++tick) {
             if (W::ballot(!seg_done) == 0) break;
             bool act = running && !seg_done;
+            BFT_STAMP(7);
             if (act) t_step();
+            BFT_STAMP(0);
             for (uint32_t p = 0;; ++p) {
                 bool pend_l = act && !frozen && pending_local();
                 uint64_t bal = W::ballot(pend_l);
@@ -892,24 +908,35 @@ struct Sim {
                     break;
                 }
                 // segment-wide summary of what is in flight (SPEC.md §2 kinds), before publish
+                BFT_STAMP(7);
                 PhaseSummary ps;
                 summarize(ps);
+                BFT_STAMP(1);
                 publish();
                 W::sync();
+                BFT_STAMP(2);
                 if (act && seg_pending) {
                     miner_step();                             // event step
                     uint64_t mk = deliver_mask(P.seed, P.n, P.thr16, inst, (uint32_t)tick, p, me);
                     uint32_t off = delivery_offset(P.seed, P.n, inst, (uint32_t)tick, p, me);
+                    BFT_STAMP(5);
                     deliver_phase(ps, mk, off);
                 }
                 W::sync();
+                BFT_STAMP(3);
                 resolve_commits();
+                BFT_STAMP(4);
                 if (frozen) act = false;
             }
             if (P.trace && is_val && !seg_done && (uint32_t)tick < P.trace_ticks)
                 P.trace[((uint64_t)inst_local * P.trace_ticks + (uint32_t)tick) * P.n + me] = state_digest();
             if (!seg_done && (frozen || canon_h >= P.heights)) { seg_done = true; done_tick = (uint32_t)tick + 1; }
         }
+#ifdef BFT_STAMPS
+        BFT_STAMP(7);
+        if (lane == 0 && P.stamps)
+            for (int k = 0; k < 12; ++k) P.stamps[(uint64_t)(inst_local / (64u / S)) * 12 + k] = st_acc[k];
+#endif
         // outputs (segment lane 0); instance-rounds = sum of (round + 1), loaded lane-parallel
         uint32_t lf = seg_or(lane_flags);
         uint32_t chv = canon_h < P.heights ? canon_h : P.heights;

@@ -31,12 +31,13 @@ struct WaveHip {
     __device__ static uint32_t readlane(uint32_t v, uint32_t l) {      // l wave-uniform
         return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_amdgcn_readfirstlane((int)l));
     }
+    __device__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
     __device__ static void sync() {
-        // LDS traffic of one wave is processed in order; this orders the compiler's view and
-        // drains outstanding LDS operations before other lanes read what this lane wrote.
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        // Intra-wave LDS hand-off: the LDS executes one wave's DS instructions in program order,
+        // so a later ds_read of any lane sees every earlier ds_write of the wave. Only the
+        // compiler must not move memory operations across this point (no s_waitcnt needed).
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        asm volatile("" ::: "memory");
     }
     __device__ static uint32_t gload(const uint32_t* p) {
         return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -165,7 +166,25 @@ static void free_bufs(bftsim* h) {
     h->cap_inst = 0;
 }
 
+#ifdef BFT_STAMPS
+static uint64_t* g_stamps = nullptr;
+static uint64_t g_stamp_waves = 0;
+#endif
+
 extern "C" {
+
+#ifdef BFT_STAMPS
+// diagnostic builds only: per-section cycle sums of the last launch, summed over waves
+int bftsim_debug_stamps(uint64_t out[12]) {
+    std::vector<uint64_t> v(g_stamp_waves * 12);
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (hipMemcpy(v.data(), g_stamps, v.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return -2;
+    for (int k = 0; k < 12; ++k) out[k] = 0;
+    for (uint64_t w = 0; w < g_stamp_waves; ++w)
+        for (int k = 0; k < 12; ++k) out[k] += v[w * 12 + k];
+    return 0;
+}
+#endif
 
 uint32_t bftsim_two_thirds_majority(uint32_t n) { return (2u * n) / 3u; }
 uint32_t bftsim_seed_from_hash(const uint8_t hash[32], uint32_t n) { return n ? bft::seed_from_hash(hash, n) : 0; }
@@ -277,6 +296,18 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         HIPCHECK(h, hipMemsetAsync(h->d_trace, 0, tb, s));
     }
     bft::Params p = make_params(h, first, n);
+#ifdef BFT_STAMPS
+    {
+        static uint64_t* d_st = nullptr;
+        static uint64_t cap = 0;
+        uint64_t waves = (n + (64 / h->seg) - 1) / (64 / h->seg);
+        if (waves > cap) { (void)hipFree(d_st); HIPCHECK(h, hipMalloc(&d_st, waves * 96)); cap = waves; }
+        HIPCHECK(h, hipMemsetAsync(d_st, 0, waves * 96, s));
+        p.stamps = d_st;
+        g_stamps = d_st;
+        g_stamp_waves = waves;
+    }
+#endif
     HIPCHECK(h, hipMemsetAsync(h->d_rec, 0, n * h->hcap * 16, s));
     uint32_t per_wave = 64u / h->seg;
     uint32_t grid = (uint32_t)((n + per_wave - 1) / per_wave);

@@ -57,6 +57,7 @@ struct EmuWave {
         return (uint32_t)g->res[l];
     }
     static uint32_t readlane(uint32_t v, uint32_t src) { return shfl(v, src); }
+    static uint64_t clock() { return 0; }
     static void sync() {
         int l = g->cur;
         g->op[l] = 3; g->seq[l]++;
