@@ -96,21 +96,29 @@ __global__ __launch_bounds__(64) void bft_hash_lane_kernel(Params p) {
 }
 
 // totals: [0] instances [1] committed [2] views [3] ticks [4..9] flag counts [10..74] round hist
+// block-level reduction in LDS, then one global atomic per counter per block
 __global__ __launch_bounds__(256) void bft_stats_kernel(Params p, unsigned long long* st) {
+    __shared__ unsigned long long acc[80];
+    for (uint32_t k = threadIdx.x; k < 80; k += 256) acc[k] = 0;
+    __syncthreads();
     uint32_t il = blockIdx.x * 256u + threadIdx.x;
-    if (il >= p.n_instances) return;
-    uint32_t ch = p.committed_height[il];
-    atomicAdd(&st[0], 1ull);
-    atomicAdd(&st[1], (unsigned long long)ch);
-    atomicAdd(&st[2], (unsigned long long)p.views[il]);
-    atomicAdd(&st[3], (unsigned long long)p.ticks[il]);
-    uint32_t f = p.flags[il];
-    for (int b = 0; b < 6; ++b)
-        if (f & (1u << b)) atomicAdd(&st[4 + b], 1ull);
-    for (uint32_t x = 1; x <= ch; ++x) {
-        uint32_t rd = p.rec[((uint64_t)il * p.hcap + x) * 4];
-        atomicAdd(&st[10 + (rd < 64 ? rd : 64)], 1ull);
+    if (il < p.n_instances) {
+        uint32_t ch = p.committed_height[il];
+        atomicAdd(&acc[0], 1ull);
+        atomicAdd(&acc[1], (unsigned long long)ch);
+        atomicAdd(&acc[2], (unsigned long long)p.views[il]);
+        atomicAdd(&acc[3], (unsigned long long)p.ticks[il]);
+        uint32_t f = p.flags[il];
+        for (int b = 0; b < 6; ++b)
+            if (f & (1u << b)) atomicAdd(&acc[4 + b], 1ull);
+        for (uint32_t x = 1; x <= ch; ++x) {
+            uint32_t rd = p.rec[((uint64_t)il * p.hcap + x) * 4];
+            atomicAdd(&acc[10 + (rd < 64 ? rd : 64)], 1ull);
+        }
     }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < 75; k += 256)
+        if (acc[k]) atomicAdd(&st[k], acc[k]);
 }
 
 }  // namespace bft

@@ -1017,3 +1017,65 @@ int orc_run_threads(const orc_config *cfg, uint64_t first_instance, uint64_t n_i
     if (seconds) *seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
     return 0;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Size-independent check: re-derive every committed header from its record (proposer, variant,
+ * time tick) and the previous hash, Keccak it, compare with the reported block hash. Returns the
+ * number of instances whose chain does not verify. Multithreaded; test infrastructure only.      */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+    const orc_config *cfg;
+    uint64_t first, n;
+    const orc_result *res;
+    uint64_t *next, *bad;
+    pthread_mutex_t *mu;
+} vjob;
+
+static int verify_one(const orc_config *cfg, uint32_t inst, const orc_result *res, uint64_t i) {
+    uint32_t H = cfg->heights;
+    uint8_t prev[32], buf[512], tx[32], out[32];
+    orc_genesis_hash(cfg, prev);
+    uint32_t ch = res->committed_height[i];
+    if (ch > H) return 1;
+    for (uint32_t x = 1; x <= ch; ++x) {
+        uint64_t o = i * H + (x - 1);
+        uint32_t prop = res->proposer[o];
+        if (prop >= cfg->n) return 1;
+        orc_tx_hash(cfg->seed, inst, x, prop, res->variant[o], tx);
+        uint64_t time = cfg->genesis_time + (uint64_t)cfg->block_period * ((uint64_t)res->time_tick[o] + 1);
+        size_t len = orc_encode_header(buf, prev, cfg->addresses + 20u * prop, tx, x, 0, 0, time, CAND_EXTRA, 11);
+        orc_keccak256(buf, len, out);
+        if (memcmp(out, res->block_hash + o * 32, 32) != 0) return 1;
+        memcpy(prev, out, 32);
+    }
+    return 0;
+}
+
+static void *vworker(void *arg) {
+    vjob *j = (vjob *)arg;
+    for (;;) {
+        pthread_mutex_lock(j->mu);
+        uint64_t i = *j->next;
+        *j->next += 1;
+        pthread_mutex_unlock(j->mu);
+        if (i >= j->n) break;
+        if (verify_one(j->cfg, (uint32_t)(j->first + i), j->res, i)) {
+            pthread_mutex_lock(j->mu);
+            *j->bad += 1;
+            pthread_mutex_unlock(j->mu);
+        }
+    }
+    return NULL;
+}
+
+uint64_t orc_verify_chains(const orc_config *cfg, uint64_t first, uint64_t n, const orc_result *res, int threads) {
+    if (threads < 1) threads = 1;
+    pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+    uint64_t next = 0, bad = 0;
+    vjob j = {cfg, first, n, res, &next, &bad, &mu};
+    for (int i = 0; i < threads; ++i) pthread_create(&th[i], NULL, vworker, &j);
+    for (int i = 0; i < threads; ++i) pthread_join(th[i], NULL);
+    free(th);
+    return bad;
+}

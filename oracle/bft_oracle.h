@@ -81,6 +81,10 @@ int orc_run(const orc_config *cfg, uint64_t first_instance, uint64_t n_instances
 int orc_run_threads(const orc_config *cfg, uint64_t first_instance, uint64_t n_instances,
                     const orc_result *res, int threads, double *seconds);
 
+/* number of instances whose committed header chain does not re-hash to the reported hashes */
+uint64_t orc_verify_chains(const orc_config *cfg, uint64_t first, uint64_t n, const orc_result *res,
+                           int threads);
+
 /* per-tick state digest of one instance (debug/parity localisation):
  * for each tick t < max_rec, out[t*n + v] = packed state of validator v at the end of tick t */
 int orc_trace(const orc_config *cfg, uint64_t instance, uint64_t *out, uint32_t max_rec);

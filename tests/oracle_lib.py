@@ -108,6 +108,26 @@ def run(cfg: BftConfig, first: int, n_inst: int, threads: int = 1):
     return arrs
 
 
+def verify_chains(cfg: BftConfig, first: int, res: dict, threads: int = 8) -> int:
+    """Re-hash every committed header chain of a result dict (any producer); returns the number
+    of instances that do not verify."""
+    n = len(res["committed_height"])
+    c, keep = to_orc(cfg)
+    arrs = {k: np.ascontiguousarray(res[k]).reshape(-1) for k in (
+        "committed_height", "flags", "ticks", "views", "round", "proposer", "variant", "time_tick",
+        "block_hash")}
+    r = OrcResult()
+    for k, a in arrs.items():
+        setattr(r, k, a.ctypes.data)
+    L = lib()
+    L.orc_verify_chains.restype = ctypes.c_uint64
+    L.orc_verify_chains.argtypes = [ctypes.POINTER(OrcConfig), ctypes.c_uint64, ctypes.c_uint64,
+                                    ctypes.POINTER(OrcResult), ctypes.c_int]
+    bad = L.orc_verify_chains(ctypes.byref(c), first, n, ctypes.byref(r), threads)
+    del keep
+    return int(bad)
+
+
 def trace(cfg: BftConfig, instance: int, max_rec: int = 512):
     c, keep = to_orc(cfg)
     out = np.zeros(max_rec * cfg.n, np.uint64)
