@@ -20,8 +20,8 @@ namespace bft {
 // Parameters of one launch (plain data, copied by value into the kernel argument buffer).
 // ---------------------------------------------------------------------------------------------
 struct Params {
-    uint32_t n;               // validators per instance (1..64 on the GPU path)
-    uint32_t seg;             // lanes per instance segment: power of two >= n
+    uint32_t n;               // validators per instance (1..256)
+    uint32_t seg;             // lanes per instance segment: power of two >= n (> 64: one workgroup)
     uint32_t heights;         // H
     uint32_t hcap;            // rows per instance in the record tables (H + margin)
     uint32_t max_ticks;
@@ -34,7 +34,7 @@ struct Params {
     uint32_t crash_on;
     uint32_t phase_cap;
     uint32_t need_seed;       // N not a power of two: proposer seeds need block hashes in-kernel
-    uint64_t silent_mask;
+    uint64_t silent_mask[4];
     uint32_t first_instance;
     uint32_t n_instances;
     uint32_t genesis_seed;
@@ -90,6 +90,95 @@ BFT_FN bool digest_match(uint64_t d, bool wild, uint64_t t) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Sender bitmaps of NW 64-bit words (MessageManage / RoundChangeSet sets, a5/a7 of SURVEY §8):
+// bit s = validator s. NW = 1 for N <= 64 (the code below then reduces to plain uint64_t
+// arithmetic); 2 or 4 for N <= 128 / 256. Word selection by a per-lane index is a select chain,
+// never a dynamically indexed register array (which would go to scratch).
+// ---------------------------------------------------------------------------------------------
+template <int NW>
+struct Bits {
+    uint64_t w[NW];
+    BFT_FN static Bits zero() { Bits b; for (int k = 0; k < NW; ++k) b.w[k] = 0; return b; }
+    BFT_FN static Bits from(uint64_t x) { Bits b = zero(); b.w[0] = x; return b; }
+    BFT_FN static Bits from(const Bits& x) { return x; }
+    BFT_FN static Bits low(uint32_t n) {          // bits [0, n), n <= 64*NW
+        Bits b;
+        for (int k = 0; k < NW; ++k) {
+            uint32_t lo = 64u * (uint32_t)k;
+            b.w[k] = n >= lo + 64u ? ~0ull : (n <= lo ? 0ull : ((1ull << (n - lo)) - 1ull));
+        }
+        return b;
+    }
+    BFT_FN static Bits bit(uint32_t i) {
+        Bits b;
+        for (int k = 0; k < NW; ++k) b.w[k] = ((i >> 6) == (uint32_t)k) ? (1ull << (i & 63u)) : 0ull;
+        return b;
+    }
+    BFT_FN uint64_t word(int i) const {          // 0 outside [0, NW)
+        uint64_t x = 0;
+        for (int k = 0; k < NW; ++k) x = (i == k) ? w[k] : x;
+        return x;
+    }
+    BFT_FN bool get(uint32_t i) const { return (word((int)(i >> 6)) >> (i & 63u)) & 1ull; }
+    BFT_FN void set(uint32_t i) { for (int k = 0; k < NW; ++k) if ((i >> 6) == (uint32_t)k) w[k] |= 1ull << (i & 63u); }
+    BFT_FN bool any() const { uint64_t x = 0; for (int k = 0; k < NW; ++k) x |= w[k]; return x != 0; }
+    BFT_FN bool none() const { return !any(); }
+    BFT_FN uint32_t popc() const {
+        uint32_t c = 0;
+        for (int k = 0; k < NW; ++k) c += (uint32_t)__builtin_popcountll(w[k]);
+        return c;
+    }
+    BFT_FN uint32_t ctz() const {                // lowest set bit, 64*NW if none
+        uint32_t r = 64u * NW;
+        for (int k = NW - 1; k >= 0; --k) r = w[k] ? 64u * (uint32_t)k + (uint32_t)__builtin_ctzll(w[k]) : r;
+        return r;
+    }
+    BFT_FN uint32_t hibit() const {              // highest set bit, 0 if none
+        uint32_t r = 0;
+        for (int k = 0; k < NW; ++k) r = w[k] ? 64u * (uint32_t)k + 63u - (uint32_t)__builtin_clzll(w[k]) : r;
+        return r;
+    }
+    BFT_FN void clear_lowest() {
+        bool done = false;
+        for (int k = 0; k < NW; ++k) {
+            bool t = !done && w[k] != 0;
+            w[k] = t ? (w[k] & (w[k] - 1ull)) : w[k];
+            done = done || t;
+        }
+    }
+    BFT_FN Bits shr(uint32_t s) const {          // s in [0, 64*NW]
+        if (NW == 1) { Bits b; b.w[0] = s >= 64u ? 0ull : (w[0] >> s); return b; }
+        Bits b;
+        int q = (int)(s >> 6);
+        uint32_t r = s & 63u;
+        for (int j = 0; j < NW; ++j) {
+            uint64_t lo = word(j + q), hi = word(j + q + 1);
+            b.w[j] = r ? ((lo >> r) | (hi << (64u - r))) : lo;
+        }
+        return b;
+    }
+    BFT_FN Bits shl(uint32_t s) const {          // s in [0, 64*NW]
+        if (NW == 1) { Bits b; b.w[0] = s >= 64u ? 0ull : (w[0] << s); return b; }
+        Bits b;
+        int q = (int)(s >> 6);
+        uint32_t r = s & 63u;
+        for (int j = 0; j < NW; ++j) {
+            uint64_t lo = word(j - q), lo2 = word(j - q - 1);
+            b.w[j] = r ? ((lo << r) | (lo2 >> (64u - r))) : lo;
+        }
+        return b;
+    }
+    BFT_FN Bits operator&(const Bits& o) const { Bits b; for (int k = 0; k < NW; ++k) b.w[k] = w[k] & o.w[k]; return b; }
+    BFT_FN Bits operator|(const Bits& o) const { Bits b; for (int k = 0; k < NW; ++k) b.w[k] = w[k] | o.w[k]; return b; }
+    BFT_FN Bits operator^(const Bits& o) const { Bits b; for (int k = 0; k < NW; ++k) b.w[k] = w[k] ^ o.w[k]; return b; }
+    BFT_FN Bits operator~() const { Bits b; for (int k = 0; k < NW; ++k) b.w[k] = ~w[k]; return b; }
+    BFT_FN Bits& operator|=(const Bits& o) { for (int k = 0; k < NW; ++k) w[k] |= o.w[k]; return *this; }
+    BFT_FN Bits& operator&=(const Bits& o) { for (int k = 0; k < NW; ++k) w[k] &= o.w[k]; return *this; }
+    BFT_FN bool operator==(const Bits& o) const { uint64_t x = 0; for (int k = 0; k < NW; ++k) x |= w[k] ^ o.w[k]; return x == 0; }
+    BFT_FN bool operator!=(const Bits& o) const { return !(*this == o); }
+};
+
+// ---------------------------------------------------------------------------------------------
 // Seeded randomness (SPEC.md §3, §5)
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t DOM_DROP = 1, DOM_SPLIT = 2, DOM_CRASH = 3, DOM_BYZ = 4, DOM_TX = 5, DOM_TX2 = 6;
@@ -126,21 +215,27 @@ BFT_FN uint32_t delivery_offset(uint64_t seed, uint32_t n, uint32_t inst, uint32
 }
 
 // N-bit delivery mask of receiver `recv` for (tick, phase); self always delivered.
-BFT_FN uint64_t deliver_mask(uint64_t seed, uint32_t n, uint32_t thr16, uint32_t inst, uint32_t tick,
+template <int NW>
+BFT_FN Bits<NW> deliver_mask(uint64_t seed, uint32_t n, uint32_t thr16, uint32_t inst, uint32_t tick,
                              uint32_t phase, uint32_t recv) {
-    uint64_t all = (n >= 64) ? ~0ull : ((1ull << n) - 1ull);
+    Bits<NW> all = Bits<NW>::low(n);
     if (thr16 == 0) return all;
-    uint64_t m = 0;
+    Bits<NW> m = Bits<NW>::zero();
     for (uint32_t j = 0; 8 * j < n; ++j) {
         uint32_t w[4];
         philox(seed, inst, tick, (phase << 24) | (recv << 8) | j, DOM_DROP, w);
+        uint64_t byte = 0;
 #pragma unroll
         for (uint32_t i = 0; i < 8; ++i) {
             uint32_t u = (w[i >> 1] >> (16 * (i & 1))) & 0xffffu;
-            if (u >= thr16) m |= 1ull << (8 * j + i);
+            if (u >= thr16) byte |= 1ull << i;
         }
+        for (int k = 0; k < NW; ++k)
+            if ((j >> 3) == (uint32_t)k) m.w[k] |= byte << (8u * (j & 7u));
     }
-    return (m & all) | (1ull << recv);
+    m &= all;
+    m.set(recv);
+    return m;
 }
 
 BFT_FN uint32_t split_bit(uint64_t seed, uint32_t inst, uint32_t h, uint32_t r, uint32_t v) {

@@ -80,7 +80,7 @@ inline Params params_from_config(const bftsim_config& c, uint32_t seg, uint32_t 
     p.crash_on = c.proposer_crash_ppm ? 1u : 0u;
     p.phase_cap = c.phase_cap;
     p.need_seed = (c.n & (c.n - 1)) != 0 ? 1u : 0u;
-    p.silent_mask = c.silent_mask[0];
+    for (int k = 0; k < 4; ++k) p.silent_mask[k] = c.silent_mask[k];
     p.first_instance = (uint32_t)first;
     p.n_instances = (uint32_t)n;
     p.genesis_seed = genesis_seed;

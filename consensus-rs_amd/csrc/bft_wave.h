@@ -1,10 +1,13 @@
-// bft_wave.h — the batched PBFT core: one wavefront simulates 64/S instances, one lane per
-// validator (lane = reference `Core` actor, src/consensus/pbft/core/core.rs:119-140).
+// bft_wave.h — the batched PBFT core: one wavefront simulates 64/S instances (S <= 64), or one
+// workgroup of S = 128 / 256 lanes simulates one instance; one lane per validator (lane =
+// reference `Core` actor, src/consensus/pbft/core/core.rs:119-140).
 //
-// The body is written once against a tiny wave-ops interface W (HIP intrinsics on gfx950, a
-// fiber emulator on the CPU for the tests). Rules that keep it correct on both:
-//   * collectives (W::ballot, W::shfl_xor, W::sync) are only called from wave-uniform control
-//     flow; the message handlers below are per-lane code and never call them;
+// The body is written once against a tiny ops interface W (wave intrinsics, or LDS-exchanged
+// workgroup collectives for S > 64, on gfx950; a fiber emulator on the CPU for the tests). Rules
+// that keep it correct on all of them:
+//   * collectives (ballot, shfl_xor, bcast, group reductions, sync) are only called from
+//     segment-uniform control flow; the message handlers below are per-lane code and never
+//     call them;
 //   * a phase's outbox is published to LDS, then W::sync(), then receivers gather senders'
 //     records in their own rotated order (SPEC.md §3) and run the reference handlers one message
 //     at a time (SPEC.md §2). Everything they send goes to the per-lane `nx` outbox for the next
@@ -17,7 +20,6 @@
 
 namespace bft {
 
-constexpr int RCS_K = 8;                 // RoundChangeSet rounds kept per validator (LDS)
 constexpr int REC_WORDS = 22;            // LDS words per published outbox record
 
 // outbox record flags
@@ -46,32 +48,53 @@ BFT_FN void outbox_clear(Outbox& o) {
     o.blk_lo = o.blk_hi = 0;
 }
 
-// LDS layout of one wave:
-//   [0, 64*REC_WORDS*4)               published outbox records (one per lane)
-//   [.., + 3*RCS_K*64*4)              RoundChangeSet, SoA [k][lane]: round, bitmap lo, bitmap hi
-//   [.., + 64*8*4)                    per-lane commit hand-off {x, blk lo, blk hi, round, seed}
+// LDS layout of one wave (S <= 64, L = 64 lanes) or one workgroup (S > 64, L = S lanes):
+//   [0, L*REC_WORDS*4)                published outbox records (one per lane)
+//   [.., + K*(1+2*NW)*L*4)            RoundChangeSet, SoA: K round words [k][lane], then the
+//                                     sender bitmaps as 2*NW 32-bit words [k][j][lane]
+//   [.., + L*8*4)                     per-lane commit hand-off {x, blk lo, blk hi, round, seed}
 //                                     (also the Fisher-Yates scratch at init)
-//   [.., + 16*8*4)                    per-segment shared words
+//   [.., + 512)                       per-segment shared words (8 per segment for S <= 64; 16 words
+//                                     + the group-collective slots at +256 for S > 64)
 //   need_seed only:
-//   [.., + 64*32)                     per-lane commit hash
-//   [.., + 64*LANE_HASH_BUF)          per-lane header buffer of lane_block_hash
-constexpr uint32_t LDS_REC_OFF = 0;
-constexpr uint32_t LDS_RC_OFF = LDS_REC_OFF + 64 * REC_WORDS * 4;
-constexpr uint32_t LDS_CMT_OFF = LDS_RC_OFF + 3 * RCS_K * 64 * 4;
-constexpr uint32_t LDS_SEG_OFF = LDS_CMT_OFF + 64 * 8 * 4;
-constexpr uint32_t LDS_CHASH_OFF = LDS_SEG_OFF + 16 * 8 * 4;
-constexpr uint32_t LDS_SCR_OFF = LDS_CHASH_OFF + 64 * 32;
-constexpr uint32_t LDS_BYTES_POW2 = LDS_CHASH_OFF;
-constexpr uint32_t LDS_BYTES_SEED = LDS_SCR_OFF + 64 * LANE_HASH_BUF;
-BFT_FN uint32_t lds_bytes_per_wave(bool need_seed) { return need_seed ? LDS_BYTES_SEED : LDS_BYTES_POW2; }
+//   [.., + L*32)                      per-lane commit hash
+//   [.., + 64*LANE_HASH_BUF)          per-lane header buffer of lane_block_hash (S <= 64; the
+//                                     workgroup kernels use a private buffer)
+template <uint32_t S>
+struct Layout {
+    static constexpr uint32_t L = S > 64 ? S : 64;
+    static constexpr int NW = S > 64 ? (int)(S / 64) : 1;
+    static constexpr int K = S > 64 ? 4 : 8;          // RoundChangeSet rounds kept per validator
+    static constexpr uint32_t REC_OFF = 0;
+    static constexpr uint32_t RC_OFF = REC_OFF + L * REC_WORDS * 4;
+    static constexpr uint32_t CMT_OFF = RC_OFF + (uint32_t)K * (1u + 2u * NW) * L * 4;
+    static constexpr uint32_t SEG_OFF = CMT_OFF + L * 8 * 4;
+    static constexpr uint32_t GRP_OFF = SEG_OFF + 256;
+    static constexpr uint32_t CHASH_OFF = SEG_OFF + 512;
+    static constexpr uint32_t SCR_OFF = CHASH_OFF + L * 32;
+    static constexpr uint32_t BYTES_POW2 = CHASH_OFF;
+    static constexpr uint32_t BYTES_SEED = S > 64 ? SCR_OFF : SCR_OFF + 64 * LANE_HASH_BUF;
+    static constexpr uint32_t bytes(bool need_seed) { return need_seed ? BYTES_SEED : BYTES_POW2; }
+};
+BFT_FN uint32_t lds_bytes(uint32_t seg, bool need_seed) {
+    return seg == 256 ? Layout<256>::bytes(need_seed) : seg == 128 ? Layout<128>::bytes(need_seed)
+                                                                 : Layout<64>::bytes(need_seed);
+}
 
 template <class W, bool NEED_SEED, uint32_t S>
 struct Sim {
+    using LY = Layout<S>;
+    static constexpr int NW = LY::NW;
+    static constexpr int RCS_K = LY::K;
+    static constexpr uint32_t LDS_REC_OFF = LY::REC_OFF, LDS_RC_OFF = LY::RC_OFF, LDS_CMT_OFF = LY::CMT_OFF,
+                              LDS_SEG_OFF = LY::SEG_OFF, LDS_CHASH_OFF = LY::CHASH_OFF, LDS_SCR_OFF = LY::SCR_OFF;
+    using M = Bits<NW>;
     const Params& P;
     uint8_t* lds;
+    W wv;                    // collectives (stateful for the workgroup flavour)
     // identity
     uint32_t lane, seg_base, me, inst_local, inst;
-    uint64_t seg_mask;       // this segment's bits in a wave ballot
+    M seg_mask;              // this segment's bits in a ballot
     bool is_val, running, byz, core_dead;
     // segment-uniform
     bool seg_done, frozen;
@@ -82,7 +105,7 @@ struct Sim {
     uint32_t h, r, st;
     bool wait;
     uint64_t lock, pp, pend;
-    uint64_t prep, comm;
+    M prep, comm;            // MessageManage sender sets (protocol/mod.rs:176-209)
     uint32_t n_rcs;          // RoundChangeSet entries (the table itself lives in LDS)
     uint32_t proposer;       // 0xffffffff = None
     // chain tip
@@ -104,21 +127,22 @@ struct Sim {
 #ifdef BFT_STAMPS
     uint64_t st_acc[12];
     uint64_t st_t;
-#define BFT_STAMP(k) do { uint64_t t_ = W::clock(); st_acc[k] += t_ - st_t; st_t = t_; } while (0)
+#define BFT_STAMP(k) do { uint64_t t_ = wv.clock(); st_acc[k] += t_ - st_t; st_t = t_; } while (0)
 #else
 #define BFT_STAMP(k) do { } while (0)
 #endif
 
     BFT_FN Sim(const Params& p, uint8_t* l, uint32_t wave_global) : P(p), lds(l) {
-        lane = W::lane();
-        seg_base = lane & ~(S - 1);
+        wv.init(lds + LY::GRP_OFF);
+        lane = wv.lane();
+        seg_base = S >= 64 ? 0u : (lane & ~(S - 1));
         me = lane - seg_base;
-        inst_local = wave_global * (64u / S) + (lane / S);
+        inst_local = S >= 64 ? wave_global : wave_global * (64u / S) + (lane / S);
         inst = p.first_instance + inst_local;
-        seg_mask = (S >= 64) ? ~0ull : (((1ull << S) - 1ull) << seg_base);
+        seg_mask = S >= 64 ? M::low(S) : M::from(((1ull << (S & 63u)) - 1ull) << seg_base);
         bool inst_ok = inst_local < p.n_instances;
         is_val = inst_ok && me < p.n;
-        running = is_val && !((p.silent_mask >> me) & 1ull);
+        running = is_val && !((p.silent_mask[(me >> 6) & 3u] >> (me & 63u)) & 1ull);
         byz = false;
         core_dead = false;
         seg_done = !inst_ok;
@@ -130,7 +154,7 @@ struct Sim {
         seg_flags = 0;
         h = 0; r = 0; st = ST_ACCEPT_REQUEST; wait = false;
         lock = pp = pend = BLK_NONE;
-        prep = comm = 0;
+        prep = comm = M::zero();
         n_rcs = 0;
         proposer = 0xffffffffu;
         last = 0; last_seed = p.genesis_seed; last_T = -1;
@@ -150,13 +174,13 @@ struct Sim {
     BFT_FN uint32_t canon_seed(uint32_t x) const {
         if (x == 0) return P.genesis_seed;
         if (x == canon_h) return canon_tip_seed;
-        return W::gload(rec_row(x) + 3);
+        return wv.gload(rec_row(x) + 3);
     }
     // canonical block id at x (x >= 1, must be recorded)
     BFT_FN uint64_t canon_blk(uint32_t x) const {
         if (x == canon_h && x != 0) return canon_tip;
-        uint32_t w1 = W::gload(rec_row(x) + 1);
-        uint32_t T = W::gload(rec_row(x) + 2);
+        uint32_t w1 = wv.gload(rec_row(x) + 1);
+        uint32_t T = wv.gload(rec_row(x) + 2);
         return blk_make(x, w1 & 0xffffu, (w1 >> 16) & 1u, T);
     }
     BFT_FN void prev_hash_words(uint32_t x, uint32_t w[8]) const {   // hash of canonical block x
@@ -167,7 +191,7 @@ struct Sim {
             return;
         }
         const uint32_t* p = (const uint32_t*)hash_row(x);
-        for (int i = 0; i < 8; ++i) w[i] = W::gload(p + i);
+        for (int i = 0; i < 8; ++i) w[i] = wv.gload(p + i);
     }
 
     // ---------------------------------------------------------------- outbox (backend.rs:140-160)
@@ -221,8 +245,8 @@ struct Sim {
             last_seed = canon_tip_seed;
             return;
         }
-        last_T = (int32_t)W::gload(rec_row(last) + 2);
-        last_seed = W::gload(rec_row(last) + 3);
+        last_T = (int32_t)wv.gload(rec_row(last) + 2);
+        last_seed = wv.gload(rec_row(last) + 3);
     }
 
     // Chain::insert_block for a Core commit (core/chain.rs:45-71 via backend.rs:163-200)
@@ -239,8 +263,14 @@ struct Sim {
             uint32_t prev[8], out[8];
             prev_hash_words(last, prev);
             uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
-            lane_block_hash(lds + LDS_SCR_OFF + lane * LANE_HASH_BUF, prev, P.addresses + 20u * blk_prop(b),
-                            P.seed, inst, x, blk_prop(b), blk_var(b), time, out);
+            if (S > 64) {
+                alignas(8) uint8_t pbuf[LANE_HASH_BUF];      // private (scratch): LDS is kept for the tables
+                lane_block_hash(pbuf, prev, P.addresses + 20u * blk_prop(b), P.seed, inst, x, blk_prop(b),
+                                blk_var(b), time, out);
+            } else {
+                lane_block_hash(lds + LDS_SCR_OFF + lane * LANE_HASH_BUF, prev, P.addresses + 20u * blk_prop(b),
+                                P.seed, inst, x, blk_prop(b), blk_var(b), time, out);
+            }
             uint32_t* hs = (uint32_t*)(lds + LDS_CHASH_OFF + lane * 32);
             uint8_t hb[8];
             for (int i = 0; i < 8; ++i) hs[i] = out[i];
@@ -329,16 +359,24 @@ struct Sim {
         out_round_change(h, round);
     }
     // RoundChangeSet table in LDS, SoA [k][lane] (conflict-free per-lane access)
-    BFT_FN uint32_t* rc_round_p(uint32_t k) const { return (uint32_t*)(lds + LDS_RC_OFF) + k * 64 + lane; }
-    BFT_FN uint32_t* rc_lo_p(uint32_t k) const { return (uint32_t*)(lds + LDS_RC_OFF) + (RCS_K + k) * 64 + lane; }
-    BFT_FN uint32_t* rc_hi_p(uint32_t k) const { return (uint32_t*)(lds + LDS_RC_OFF) + (2 * RCS_K + k) * 64 + lane; }
-    BFT_FN uint64_t rc_set_at(uint32_t k) const { return (uint64_t)*rc_lo_p(k) | ((uint64_t)*rc_hi_p(k) << 32); }
+    BFT_FN uint32_t* rc_round_p(uint32_t k) const { return (uint32_t*)(lds + LDS_RC_OFF) + k * LY::L + lane; }
+    BFT_FN uint32_t* rc_word_p(uint32_t k, uint32_t j) const {
+        return (uint32_t*)(lds + LDS_RC_OFF) + (RCS_K + k * 2u * NW + j) * LY::L + lane;
+    }
+    BFT_FN M rc_set_at(uint32_t k) const {
+        M m;
+        for (int j = 0; j < NW; ++j) m.w[j] = (uint64_t)*rc_word_p(k, 2 * j) | ((uint64_t)*rc_word_p(k, 2 * j + 1) << 32);
+        return m;
+    }
+    BFT_FN void rc_set_store(uint32_t k, const M& m) {
+        for (int j = 0; j < NW; ++j) { *rc_word_p(k, 2 * j) = (uint32_t)m.w[j]; *rc_word_p(k, 2 * j + 1) = (uint32_t)(m.w[j] >> 32); }
+    }
 
     BFT_FN uint32_t rcs_max_round() const {                                  // round_change_set.rs:64-74
         uint32_t mx = 0;
         int total = 0;
         for (uint32_t i = 0; i < n_rcs; ++i) {               // ascending rounds (canonical order)
-            int len = __builtin_popcountll(rc_set_at(i));
+            int len = (int)rc_set_at(i).popc();
             uint32_t rd = *rc_round_p(i);
             if (len >= total && rd > mx) { mx = rd; total = len; }
         }
@@ -351,18 +389,15 @@ struct Sim {
             if (n_rcs == (uint32_t)RCS_K) { lane_flags |= FLAG_RCS_OVERFLOW; return 0; }
             for (uint32_t i = n_rcs; i > pos; --i) {
                 *rc_round_p(i) = *rc_round_p(i - 1);
-                *rc_lo_p(i) = *rc_lo_p(i - 1);
-                *rc_hi_p(i) = *rc_hi_p(i - 1);
+                for (uint32_t j = 0; j < 2u * NW; ++j) *rc_word_p(i, j) = *rc_word_p(i - 1, j);
             }
             *rc_round_p(pos) = round;
-            *rc_lo_p(pos) = 0;
-            *rc_hi_p(pos) = 0;
+            rc_set_store(pos, M::zero());
             n_rcs += 1;
         }
-        uint64_t set = rc_set_at(pos) | (1ull << sender);
-        *rc_lo_p(pos) = (uint32_t)set;
-        *rc_hi_p(pos) = (uint32_t)(set >> 32);
-        return __builtin_popcountll(set);
+        M set = rc_set_at(pos) | M::bit(sender);
+        rc_set_store(pos, set);
+        return (int)set.popc();
     }
     BFT_FN void send_next_round_change() {                                   // round_change.rs:26-36
         uint32_t round = rcs_max_round();
@@ -376,7 +411,7 @@ struct Sim {
         r = 0;
         n_rcs = 0;
         lock = pp = pend = BLK_NONE;
-        prep = comm = 0;
+        prep = comm = M::zero();
         proposer = (last_seed + 0u) % P.n;
         wait = false;
         st = ST_ACCEPT_REQUEST;
@@ -388,7 +423,7 @@ struct Sim {
         if (last_height > h) return;
         n_rcs = 0;
         if (!blk_valid(lock)) pp = BLK_NONE;
-        prep = comm = 0;
+        prep = comm = M::zero();
         r = round;
         proposer = (last_seed + round) % P.n;
         wait = false;
@@ -453,17 +488,17 @@ struct Sim {
         int res = check_message(2, vh);
         if (res != 0) { if (res == 2) note_future_block(vh); return; }
         if (vh != h || vr != r) return;
-        prep |= 1ull << src;
+        prep.set(src);
         if (blk_valid(lock) && digest_match(d, wild, lock)) { lock_hash(); st = ST_PREPARED; send_commit(); }
-        if ((uint32_t)__builtin_popcountll(prep | comm) > (2u * P.n) / 3u) { lock_hash(); st = ST_PREPARED; send_commit(); }
+        if ((prep | comm).popc() > (2u * P.n) / 3u) { lock_hash(); st = ST_PREPARED; send_commit(); }
     }
 
     BFT_FN void handle_commit(uint32_t src, uint32_t vh, uint32_t vr, uint64_t d, bool wild) {    // commit.rs:63-111
         int res = check_message(3, vh);
         if (res != 0) { if (res == 2) note_future_block(vh); return; }
         if (!digest_match(d, wild, pp) || vh != h || vr != r) return;
-        comm |= 1ull << src;
-        if ((uint32_t)__builtin_popcountll(comm) > (2u * P.n) / 3u && st < ST_COMMITTED) { lock_hash(); core_commit(); }
+        comm.set(src);
+        if (comm.popc() > (2u * P.n) / 3u && st < ST_COMMITTED) { lock_hash(); core_commit(); }
     }
 
     BFT_FN void handle_round_change(uint32_t src, uint32_t vh, uint32_t mr) {   // round_change.rs:65-98
@@ -530,72 +565,84 @@ struct Sim {
         if (!core_dead && timer_tick == tick) { timer_tick = -1; handle_timer_event(); }
     }
 
-    // segment reductions (butterfly inside the segment)
+    // segment collectives: ballots as sender bitmaps; reductions (butterfly inside a wave
+    // segment, LDS-combined per-wave partials for a workgroup segment)
+    BFT_FN M ballot(bool p) { return M::from(wv.ballot(p)); }
+    BFT_FN void sync() { wv.sync(); }
     BFT_FN uint32_t seg_max(uint32_t v) {
-        for (uint32_t m = 1; m < S; m <<= 1) { uint32_t o = W::shfl_xor(v, m); v = v > o ? v : o; }
-        return v;
+        if constexpr (S > 64) { return wv.grp_max(v); }
+        else {
+            for (uint32_t m = 1; m < S; m <<= 1) { uint32_t o = wv.shfl_xor(v, m); v = v > o ? v : o; }
+            return v;
+        }
     }
     BFT_FN uint64_t seg_sum64(uint32_t v32) {
-        uint64_t v = v32;
-        for (uint32_t m = 1; m < S; m <<= 1) {
-            uint32_t lo = W::shfl_xor((uint32_t)v, m), hi = W::shfl_xor((uint32_t)(v >> 32), m);
-            v += (uint64_t)lo | ((uint64_t)hi << 32);
+        if constexpr (S > 64) { return wv.grp_sum64(v32); }
+        else {
+            uint64_t v = v32;
+            for (uint32_t m = 1; m < S; m <<= 1) {
+                uint32_t lo = wv.shfl_xor((uint32_t)v, m), hi = wv.shfl_xor((uint32_t)(v >> 32), m);
+                v += (uint64_t)lo | ((uint64_t)hi << 32);
+            }
+            return v;
         }
-        return v;
     }
     BFT_FN uint32_t seg_or(uint32_t v) {
-        for (uint32_t m = 1; m < S; m <<= 1) v |= W::shfl_xor(v, m);
-        return v;
+        if constexpr (S > 64) { return wv.grp_or(v); }
+        else {
+            for (uint32_t m = 1; m < S; m <<= 1) v |= wv.shfl_xor(v, m);
+            return v;
+        }
     }
 
     // record a new canonical height (segment leader; global stores for the outputs)
     BFT_FN void record_canon(uint32_t x, uint64_t b, uint32_t round, uint32_t seed, const uint32_t* hs) {
         uint32_t* row = rec_row(x);
-        W::gstore(row + 0, round);
-        W::gstore(row + 2, blk_T(b));
-        W::gstore(row + 3, seed);
-        W::gstore(row + 1, blk_prop(b) | (blk_var(b) << 16) | (1u << 24));
+        wv.gstore(row + 0, round);
+        wv.gstore(row + 2, blk_T(b));
+        wv.gstore(row + 3, seed);
+        wv.gstore(row + 1, blk_prop(b) | (blk_var(b) << 16) | (1u << 24));
         if (NEED_SEED) {
             uint32_t* dst = (uint32_t*)hash_row(x);
-            for (int i = 0; i < 8; ++i) W::gstore(dst + i, hs[i]);
+            for (int i = 0; i < 8; ++i) wv.gstore(dst + i, hs[i]);
         }
     }
 
     // first Core commits of the phase → canonical table, in lane order (oracle receiver order)
     BFT_FN void resolve_commits() {
         bool c = commit_x != 0;
-        uint64_t bal = W::ballot(c);
-        if (bal == 0) return;
+        M bal = ballot(c);
+        if (bal.none()) return;
         uint32_t* cm = (uint32_t*)(lds + LDS_CMT_OFF) + lane * 8;
         if (c) {
             cm[0] = commit_x; cm[1] = (uint32_t)commit_blk; cm[2] = (uint32_t)(commit_blk >> 32);
             cm[3] = commit_round; cm[4] = commit_seed;
         }
-        W::sync();
-        uint64_t segbits = bal & seg_mask;
+        sync();
+        M segbits = bal & seg_mask;
         uint32_t* segw = (uint32_t*)(lds + LDS_SEG_OFF) + (lane / S) * 8;
-        const bool mine = segbits != 0 && !seg_done;
-        const uint32_t lead = segbits ? (uint32_t)__builtin_ctzll(segbits) : 0u;
+        const bool mine = segbits.any() && !seg_done;
+        const uint32_t lead = segbits.any() ? segbits.ctz() : 0u;
         // fast path: every committer of the segment commits the same height as the first one
         const uint32_t* cl = (const uint32_t*)(lds + LDS_CMT_OFF) + lead * 8;
         uint32_t x0 = mine ? cl[0] : 0u;
         uint64_t b0 = mine ? ((uint64_t)cl[1] | ((uint64_t)cl[2] << 32)) : 0ull;
         bool other_h = c && mine && commit_x != x0;
-        uint64_t mixed = W::ballot(other_h) & seg_mask;
-        bool uniform = mixed == 0;
+        M mixed = ballot(other_h) & seg_mask;
+        bool uniform = mixed.none();
         // canonical block of x0 as it was before this phase (heights are recorded contiguously)
         bool x0_known = x0 <= canon_h;
         uint64_t ref = 0;
         if (mine && uniform) ref = x0_known ? canon_blk(x0) : b0;
         bool bad = mine && uniform && c && !blk_eq(commit_blk, ref);
-        uint64_t badm = W::ballot(bad) & seg_mask;
+        M badm = ballot(bad) & seg_mask;
         if (mine && uniform && lane == lead) {
             // lanes below the first violating lane were processed before the freeze
-            bool fr = badm != 0;
+            bool fr = badm.any();
             uint32_t ch = canon_h;
             uint64_t tip = canon_tip;
             uint32_t tseed = canon_tip_seed;
-            if (!x0_known && x0 < P.hcap && (!fr || (uint32_t)__builtin_ctzll(badm) > lead)) {
+            if (!x0_known && x0 < P.hcap && (!fr || badm.ctz() > lead)) {
                 record_canon(x0, b0, cl[3], cl[4], (const uint32_t*)(lds + LDS_CHASH_OFF + lead * 32));
                 ch = x0; tip = b0; tseed = cl[4];
             }
@@ -612,10 +659,10 @@ struct Sim {
             uint64_t tip = canon_tip;
             uint32_t tseed = canon_tip_seed;
             bool fr = false;
-            uint64_t bits = segbits;
-            while (bits != 0) {
-                uint32_t j = (uint32_t)__builtin_ctzll(bits);
-                bits &= bits - 1;
+            M bits = segbits;
+            while (bits.any()) {
+                uint32_t j = bits.ctz();
+                bits.clear_lowest();
                 const uint32_t* cj = (const uint32_t*)(lds + LDS_CMT_OFF) + j * 8;
                 uint32_t x = cj[0];
                 uint64_t b = (uint64_t)cj[1] | ((uint64_t)cj[2] << 32);
@@ -635,7 +682,7 @@ struct Sim {
             segw[3] = (uint32_t)(tip >> 32);
             segw[4] = tseed;
         }
-        W::sync();
+        sync();
         if (mine) {
             canon_h = segw[0];
             canon_tip = (uint64_t)segw[2] | ((uint64_t)segw[3] << 32);
@@ -643,7 +690,7 @@ struct Sim {
             if (segw[1]) { frozen = true; seg_flags |= FLAG_SAFETY; }
         }
         commit_x = 0;
-        W::sync();
+        sync();
     }
 
     BFT_FN uint64_t state_digest() const {
@@ -651,179 +698,181 @@ struct Sim {
                ((uint64_t)(wait ? 1 : 0) << 27) | ((uint64_t)(last & 0xffffu) << 28) |
                ((uint64_t)(blk_valid(lock) ? 1 : 0) << 44) | ((uint64_t)(blk_valid(pp) ? 1 : 0) << 45) |
                ((uint64_t)(blk_valid(pend) ? 1 : 0) << 46) | ((uint64_t)(core_dead ? 1 : 0) << 47) |
-               ((uint64_t)(__builtin_popcountll(prep) & 0xff) << 48) |
-               ((uint64_t)(__builtin_popcountll(comm) & 0xff) << 56);
+               ((uint64_t)(prep.popc() & 0xffu) << 48) |
+               ((uint64_t)(comm.popc() & 0xffu) << 56);
     }
 
     BFT_FN void init_byzantine() {       // partial Fisher-Yates by the segment's lane 0 (SPEC.md §5)
         uint8_t* perm = lds + LDS_CMT_OFF + seg_base;                   // segment scratch (S bytes)
         uint32_t* segw = (uint32_t*)(lds + LDS_SEG_OFF) + (lane / S) * 8;
+        const uint32_t mw = NW == 1 ? 2u : 8u;                            // mask words in segw
         if (me == 0 && !seg_done) {
             uint32_t n = P.n;
             for (uint32_t i = 0; i < n; ++i) perm[i] = (uint8_t)i;
-            uint64_t mask = 0;
+            M mask = M::zero();
             uint32_t f = P.byz_count < n ? P.byz_count : n;
             for (uint32_t i = 0; i < f; ++i) {
                 uint32_t w[4];
                 philox(P.seed, inst, i, 0, DOM_BYZ, w);
                 uint32_t j = i + w[0] % (n - i);
                 uint8_t t = perm[i]; perm[i] = perm[j]; perm[j] = t;
-                mask |= 1ull << perm[i];
+                mask.set(perm[i]);
             }
-            segw[2] = (uint32_t)mask;
-            segw[3] = (uint32_t)(mask >> 32);
+            for (int k = 0; k < NW; ++k) { segw[mw + 2 * k] = (uint32_t)mask.w[k]; segw[mw + 2 * k + 1] = (uint32_t)(mask.w[k] >> 32); }
         }
-        W::sync();
-        uint64_t mask = (uint64_t)segw[2] | ((uint64_t)segw[3] << 32);
-        byz = is_val && !seg_done && ((mask >> me) & 1ull);
-        W::sync();
+        sync();
+        M mask;
+        for (int k = 0; k < NW; ++k) mask.w[k] = (uint64_t)segw[mw + 2 * k] | ((uint64_t)segw[mw + 2 * k + 1] << 32);
+        byz = is_val && !seg_done && mask.get(me);
+        sync();
     }
 
     // ---------------------------------------------------------------- phase fast paths
     // Segment-wide summary of one phase's messages. All masks use segment-local sender bits.
     struct PhaseSummary {
-        uint64_t k_pp, k_pr, k_cm, k_ocm, k_rc, k_sync, k_blk;
-        uint64_t pr_v0, pr_v1, pr_w, cm_v0, cm_v1, cm_w;
+        M k_pp, k_pr, k_cm, k_ocm, k_rc, k_sync, k_blk;
+        M pr_v0, pr_v1, pr_w, cm_v0, cm_v1, cm_w;
         uint32_t pr_h, pr_r, cm_h, cm_r, blk_lo, blk_hi;
         uint64_t pr_cls, cm_cls;              // (height, proposer) class of the digests
         bool u_pr, u_cm, u_blk;               // one view / one digest class / one range
     };
 
-    BFT_FN uint64_t seg_bits(uint64_t bal) const {
-        return S >= 64 ? bal : ((bal >> seg_base) & ((1ull << S) - 1ull));
+    BFT_FN M seg_bits(const M& bal) const {
+        if constexpr (S >= 64) return bal;
+        else return M::from((bal.w[0] >> seg_base) & ((1ull << S) - 1ull));
     }
 
     // value of lane (seg_base + j) — j is uniform within the segment
-    BFT_FN uint32_t from_seg_lane(uint32_t v, uint32_t j) const {
-        if (S >= 64) return W::readlane(v, j);
-        return W::shfl(v, seg_base + j);
+    BFT_FN uint32_t from_seg_lane(uint32_t v, uint32_t j) {
+        if constexpr (S > 64) return wv.bcast(v, j);
+        else if constexpr (S == 64) return wv.readlane(v, j);
+        else return wv.shfl(v, seg_base + j);
     }
 
     BFT_FN void summarize(PhaseSummary& ps) {
         const uint32_t f = nx.f;
-        ps.k_pp = seg_bits(W::ballot((f & F_PP) != 0));
-        ps.k_pr = seg_bits(W::ballot((f & F_PR) != 0));
-        ps.k_cm = seg_bits(W::ballot((f & F_CM) != 0));
-        ps.k_ocm = seg_bits(W::ballot((f & F_OCM) != 0));
-        ps.k_rc = seg_bits(W::ballot((f & F_RC) != 0));
-        ps.k_sync = seg_bits(W::ballot((f & F_SYNC) != 0));
-        ps.k_blk = seg_bits(W::ballot((f & F_BLK) != 0));
+        ps.k_pp = seg_bits(ballot((f & F_PP) != 0));
+        ps.k_pr = seg_bits(ballot((f & F_PR) != 0));
+        ps.k_cm = seg_bits(ballot((f & F_CM) != 0));
+        ps.k_ocm = seg_bits(ballot((f & F_OCM) != 0));
+        ps.k_rc = seg_bits(ballot((f & F_RC) != 0));
+        ps.k_sync = seg_bits(ballot((f & F_SYNC) != 0));
+        ps.k_blk = seg_bits(ballot((f & F_BLK) != 0));
         const bool pr = (f & F_PR) != 0, cm = (f & F_CM) != 0, bk = (f & F_BLK) != 0;
         const bool prw = (f & F_PR_W) != 0, cmw = (f & F_CM_W) != 0;
         ps.pr_h = ps.pr_r = ps.cm_h = ps.cm_r = ps.blk_lo = ps.blk_hi = 0;
         ps.pr_cls = ps.cm_cls = 0;
-        ps.pr_w = ps.pr_v0 = ps.pr_v1 = ps.cm_w = ps.cm_v0 = ps.cm_v1 = 0;
+        ps.pr_w = ps.pr_v0 = ps.pr_v1 = ps.cm_w = ps.cm_v0 = ps.cm_v1 = M::zero();
         ps.u_pr = ps.u_cm = ps.u_blk = true;
         // leader of each kind (the first sender of the segment) and uniformity against it
-        uint64_t any_pr = W::ballot(pr), any_cm = W::ballot(cm), any_bk = W::ballot(bk);
+        bool any_pr = ballot(pr).any(), any_cm = ballot(cm).any(), any_bk = ballot(bk).any();
         bool mm_pr = false, mm_cm = false, mm_blk = false;
         if (any_pr) {
-            uint32_t j = ps.k_pr ? (uint32_t)__builtin_ctzll(ps.k_pr) : 0u;
+            uint32_t j = ps.k_pr.any() ? ps.k_pr.ctz() : 0u;
             uint64_t cls = nx.pr_d & BLK_HP_MASK;
             ps.pr_h = from_seg_lane(nx.pr_h, j);
             ps.pr_r = from_seg_lane(nx.pr_r, j);
             ps.pr_cls = (uint64_t)from_seg_lane((uint32_t)cls, j) | ((uint64_t)from_seg_lane((uint32_t)(cls >> 32), j) << 32);
             mm_pr = pr && (nx.pr_h != ps.pr_h || nx.pr_r != ps.pr_r || cls != ps.pr_cls);
-            ps.pr_w = seg_bits(W::ballot(pr && prw));
-            ps.pr_v0 = seg_bits(W::ballot(pr && !prw && blk_var(nx.pr_d) == 0));
-            ps.pr_v1 = seg_bits(W::ballot(pr && !prw && blk_var(nx.pr_d) == 1));
+            ps.pr_w = seg_bits(ballot(pr && prw));
+            ps.pr_v0 = seg_bits(ballot(pr && !prw && blk_var(nx.pr_d) == 0));
+            ps.pr_v1 = seg_bits(ballot(pr && !prw && blk_var(nx.pr_d) == 1));
         }
         if (any_cm) {
-            uint32_t j = ps.k_cm ? (uint32_t)__builtin_ctzll(ps.k_cm) : 0u;
+            uint32_t j = ps.k_cm.any() ? ps.k_cm.ctz() : 0u;
             uint64_t cls = nx.cm_d & BLK_HP_MASK;
             ps.cm_h = from_seg_lane(nx.cm_h, j);
             ps.cm_r = from_seg_lane(nx.cm_r, j);
             ps.cm_cls = (uint64_t)from_seg_lane((uint32_t)cls, j) | ((uint64_t)from_seg_lane((uint32_t)(cls >> 32), j) << 32);
             mm_cm = cm && (nx.cm_h != ps.cm_h || nx.cm_r != ps.cm_r || cls != ps.cm_cls);
-            ps.cm_w = seg_bits(W::ballot(cm && cmw));
-            ps.cm_v0 = seg_bits(W::ballot(cm && !cmw && blk_var(nx.cm_d) == 0));
-            ps.cm_v1 = seg_bits(W::ballot(cm && !cmw && blk_var(nx.cm_d) == 1));
+            ps.cm_w = seg_bits(ballot(cm && cmw));
+            ps.cm_v0 = seg_bits(ballot(cm && !cmw && blk_var(nx.cm_d) == 0));
+            ps.cm_v1 = seg_bits(ballot(cm && !cmw && blk_var(nx.cm_d) == 1));
         }
         if (any_bk) {
-            uint32_t j = ps.k_blk ? (uint32_t)__builtin_ctzll(ps.k_blk) : 0u;
+            uint32_t j = ps.k_blk.any() ? ps.k_blk.ctz() : 0u;
             ps.blk_lo = from_seg_lane(nx.blk_lo, j);
             ps.blk_hi = from_seg_lane(nx.blk_hi, j);
             mm_blk = bk && (nx.blk_lo != ps.blk_lo || nx.blk_hi != ps.blk_hi);
         }
         if (any_pr | any_cm | any_bk) {
-            ps.u_pr = seg_bits(W::ballot(mm_pr)) == 0;
-            ps.u_cm = seg_bits(W::ballot(mm_cm)) == 0;
-            ps.u_blk = seg_bits(W::ballot(mm_blk)) == 0;
+            ps.u_pr = seg_bits(ballot(mm_pr)).none();
+            ps.u_cm = seg_bits(ballot(mm_cm)).none();
+            ps.u_blk = seg_bits(ballot(mm_blk)).none();
         }
     }
 
     // rotate a sender mask into this receiver's delivery order (position 0 = first delivered)
-    BFT_FN uint64_t rot(uint64_t m, uint32_t off) const {
+    BFT_FN M rot(const M& m, uint32_t off) const {
         if (off == 0) return m;
         uint32_t n = P.n;
-        uint64_t nm = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
-        return ((m >> off) | (m << (n - off))) & nm;
+        return (m.shr(off) | m.shl(n - off)) & M::low(n);
     }
-    BFT_FN static uint64_t low(uint32_t k) { return k >= 64 ? ~0ull : ((1ull << k) - 1ull); }
+    BFT_FN static M low(uint32_t k) { return M::low(k); }
     // smallest position p in [0,n) with popcount(base | a & low(p+1) | b & low(p)) > q, else n
-    BFT_FN uint32_t first_over(uint64_t base, uint64_t a, uint64_t b, uint32_t q) const {
+    BFT_FN uint32_t first_over(const M& base, const M& a, const M& b, uint32_t q) const {
         uint32_t n = P.n;
-        if ((uint32_t)__builtin_popcountll(base | a | (b & low(n - 1))) <= q) return n;
+        if ((base | a | (b & low(n - 1))).popc() <= q) return n;
         uint32_t lo = 0, hi = n - 1;                 // answer in [lo, hi]
         while (lo < hi) {
             uint32_t mid = (lo + hi) >> 1;
-            if ((uint32_t)__builtin_popcountll(base | (a & low(mid + 1)) | (b & low(mid))) > q) hi = mid;
+            if ((base | (a & low(mid + 1)) | (b & low(mid))).popc() > q) hi = mid;
             else lo = mid + 1;
         }
         return lo;
     }
-    BFT_FN static uint32_t first_at_or_after(uint64_t m, uint32_t p) {
-        uint64_t x = m & ~low(p);
-        return x ? (uint32_t)__builtin_ctzll(x) : 64u;
+    BFT_FN static uint32_t first_at_or_after(const M& m, uint32_t p) {
+        M x = m & ~low(p);
+        return x.any() ? x.ctz() : 64u * NW;
     }
 
     // digests of the class `cls` that match `target` (wildcards match both variants)
-    BFT_FN static uint64_t class_match(uint64_t cls, uint64_t v0, uint64_t v1, uint64_t w, uint64_t target) {
-        if (!blk_valid(target) || ((cls ^ target) & BLK_HP_MASK) != 0) return 0;
+    BFT_FN static M class_match(uint64_t cls, const M& v0, const M& v1, const M& w, uint64_t target) {
+        if (!blk_valid(target) || ((cls ^ target) & BLK_HP_MASK) != 0) return M::zero();
         return w | (blk_var(target) ? v1 : v0);
     }
 
     // A phase that carries only Prepares and Commits, each kind with one view and one digest
     // class: the sequential handlers of prepare.rs:48-66 and commit.rs:63-82, evaluated in this
     // receiver's delivery order with prefix masks instead of one message at a time.
-    BFT_FN void deliver_prepare_commit(const PhaseSummary& ps, uint64_t mk, uint32_t off) {
-        uint64_t PRacc = 0, CMacc = 0;
-        uint64_t prd = mk & ps.k_pr, cmd = mk & ps.k_cm;
-        if (prd) {
+    BFT_FN void deliver_prepare_commit(const PhaseSummary& ps, const M& mk, uint32_t off) {
+        M PRacc = M::zero(), CMacc = M::zero();
+        M prd = mk & ps.k_pr, cmd = mk & ps.k_cm;
+        if (prd.any()) {
             int res = check_message(2, ps.pr_h);
             if (res != 0) { if (res == 2) note_future_block(ps.pr_h); }
             else if (ps.pr_h == h && ps.pr_r == r) PRacc = prd;
         }
-        if (cmd) {
+        if (cmd.any()) {
             int res = check_message(3, ps.cm_h);
             if (res != 0) { if (res == 2) note_future_block(ps.cm_h); }
             else if (ps.cm_h == h && ps.cm_r == r) CMacc = cmd & class_match(ps.cm_cls, ps.cm_v0, ps.cm_v1, ps.cm_w, pp);
         }
-        if (!PRacc && !CMacc) return;
+        if (PRacc.none() && CMacc.none()) return;
         const uint32_t q = (2u * P.n) / 3u;
         uint32_t n = P.n;
-        uint64_t PR = rot(PRacc, off), CM = rot(CMacc, off);
-        uint64_t U0 = rot(prep | comm, off), C0 = rot(comm, off);
-        const uint32_t lastPR = PR ? 63u - (uint32_t)__builtin_clzll(PR) : 0u;
-        const uint32_t lastCM = CM ? 63u - (uint32_t)__builtin_clzll(CM) : 0u;
+        M PR = rot(PRacc, off), CM = rot(CMacc, off);
+        M U0 = rot(prep | comm, off), C0 = rot(comm, off);
+        const uint32_t lastPR = PR.hibit();
+        const uint32_t lastCM = CM.hibit();
         // prepare triggers (prepare.rs:54-63). B fires at some prepare iff it fires at the last
         // one (|prep ∪ commit| only grows); commits of the last prepare's sender come after it.
-        const bool trigB = PR && (uint32_t)__builtin_popcountll(U0 | PR | (CM & low(lastPR))) > q;
-        uint64_t lm = 0;
-        if (blk_valid(lock) && PR) lm = rot(PRacc & class_match(ps.pr_cls, ps.pr_v0, ps.pr_v1, ps.pr_w, lock), off);
-        const bool trig = trigB || lm != 0;
+        const bool trigB = PR.any() && (U0 | PR | (CM & low(lastPR))).popc() > q;
+        M lm = M::zero();
+        if (blk_valid(lock) && PR.any()) lm = rot(PRacc & class_match(ps.pr_cls, ps.pr_v0, ps.pr_v1, ps.pr_w, lock), off);
+        const bool trig = trigB || lm.any();
         // commit quorum events (commit.rs:75-80) exist iff the final count is over q
-        const bool cexists = CM && (uint32_t)__builtin_popcountll(C0 | CM) > q;
-        uint32_t lastT = 0, t1 = 64;
+        const bool cexists = CM.any() && (C0 | CM).popc() > q;
+        uint32_t lastT = 0, t1 = 64u * NW;
         if (trig) {
-            if (lm) t1 = (uint32_t)__builtin_ctzll(lm);
+            if (lm.any()) t1 = lm.ctz();
             if (trigB) {
                 lastT = lastPR;                                 // every prepare from tB on
             } else {
                 // lock-match triggers only: the first one locks pp, later ones match pp
-                uint64_t mpp = rot(PRacc & class_match(ps.pr_cls, ps.pr_v0, ps.pr_v1, ps.pr_w, pp), off);
-                uint64_t T = (mpp & ~low(t1)) | (1ull << t1);
-                lastT = 63u - (uint32_t)__builtin_clzll(T);
+                M mpp = rot(PRacc & class_match(ps.pr_cls, ps.pr_v0, ps.pr_v1, ps.pr_w, pp), off);
+                M T = (mpp & ~low(t1)) | M::bit(t1);
+                lastT = T.hibit();
             }
         }
         const uint32_t s0 = st;
@@ -854,27 +903,27 @@ struct Sim {
         st = fin;
     }
 
-    BFT_FN void deliver_phase(const PhaseSummary& ps, uint64_t mk, uint32_t off) {
-        bool other = (ps.k_pp | ps.k_ocm | ps.k_rc | ps.k_sync) != 0;
+    BFT_FN void deliver_phase(const PhaseSummary& ps, const M& mk, uint32_t off) {
+        bool other = (ps.k_pp | ps.k_ocm | ps.k_rc | ps.k_sync).any();
         if (P.fast && !other) {
-            if (!ps.k_pr && !ps.k_cm) {
-                if (ps.k_blk && ps.u_blk) {          // block gossip with one range
-                    if (mk & ps.k_blk & ~(1ull << me)) handle_blocks(ps.blk_lo, ps.blk_hi);
+            if (ps.k_pr.none() && ps.k_cm.none()) {
+                if (ps.k_blk.any() && ps.u_blk) {          // block gossip with one range
+                    if ((mk & ps.k_blk & ~M::bit(me)).any()) handle_blocks(ps.blk_lo, ps.blk_hi);
                     BFT_STAMP(8);
                     return;
                 }
-            } else if (!ps.k_blk && ps.u_pr && ps.u_cm) {
+            } else if (ps.k_blk.none() && ps.u_pr && ps.u_cm) {
                 if (!core_dead) deliver_prepare_commit(ps, mk, off);
                 BFT_STAMP(9);
                 return;
             }
         }
         // general path: every delivered non-empty sender, in rotated order, one at a time
-        uint64_t any = ps.k_pp | ps.k_pr | ps.k_cm | ps.k_ocm | ps.k_rc | ps.k_sync | ps.k_blk;
-        uint64_t c = rot(mk & any, off);
-        while (c) {
-            uint32_t pos = (uint32_t)__builtin_ctzll(c);
-            c &= c - 1;
+        M any = ps.k_pp | ps.k_pr | ps.k_cm | ps.k_ocm | ps.k_rc | ps.k_sync | ps.k_blk;
+        M c = rot(mk & any, off);
+        while (c.any()) {
+            uint32_t pos = c.ctz();
+            c.clear_lowest();
             uint32_t s = pos + off;
             if (s >= P.n) s -= P.n;
             deliver_from(s);
@@ -886,24 +935,24 @@ struct Sim {
     BFT_FN void run() {
 #ifdef BFT_STAMPS
         for (int k = 0; k < 12; ++k) st_acc[k] = 0;
-        st_t = W::clock();
+        st_t = wv.clock();
 #endif
         if (P.byz_count > 0) init_byzantine();
         for (tick = 0; tick < (int32_t)P.max_ticks; ++tick) {
-            if (W::ballot(!seg_done) == 0) break;
+            if (ballot(!seg_done).none()) break;
             bool act = running && !seg_done;
             BFT_STAMP(7);
             if (act) t_step();
             BFT_STAMP(0);
             for (uint32_t p = 0;; ++p) {
                 bool pend_l = act && !frozen && pending_local();
-                uint64_t bal = W::ballot(pend_l);
-                if (bal == 0) break;
-                bool seg_pending = (bal & seg_mask) != 0;
+                M bal = ballot(pend_l);
+                if (bal.none()) break;
+                bool seg_pending = (bal & seg_mask).any();
                 if (p >= P.phase_cap) {
                     // messages still in flight are dropped (SPEC.md §2)
-                    uint64_t inflight = W::ballot(act && nx.f != 0);
-                    if ((inflight & seg_mask) != 0 && !seg_done) seg_flags |= FLAG_PHASE_CAP;
+                    M inflight = ballot(act && nx.f != 0);
+                    if ((inflight & seg_mask).any() && !seg_done) seg_flags |= FLAG_PHASE_CAP;
                     outbox_clear(nx);
                     break;
                 }
@@ -913,16 +962,16 @@ struct Sim {
                 summarize(ps);
                 BFT_STAMP(1);
                 publish();
-                W::sync();
+                sync();
                 BFT_STAMP(2);
                 if (act && seg_pending) {
                     miner_step();                             // event step
-                    uint64_t mk = deliver_mask(P.seed, P.n, P.thr16, inst, (uint32_t)tick, p, me);
+                    M mk = deliver_mask<NW>(P.seed, P.n, P.thr16, inst, (uint32_t)tick, p, me);
                     uint32_t off = delivery_offset(P.seed, P.n, inst, (uint32_t)tick, p, me);
                     BFT_STAMP(5);
                     deliver_phase(ps, mk, off);
                 }
-                W::sync();
+                sync();
                 BFT_STAMP(3);
                 resolve_commits();
                 BFT_STAMP(4);
@@ -935,14 +984,14 @@ struct Sim {
 #ifdef BFT_STAMPS
         BFT_STAMP(7);
         if (lane == 0 && P.stamps)
-            for (int k = 0; k < 12; ++k) P.stamps[(uint64_t)(inst_local / (64u / S)) * 12 + k] = st_acc[k];
+            for (int k = 0; k < 12; ++k) P.stamps[(uint64_t)(S >= 64 ? inst_local : inst_local / (64u / S)) * 12 + k] = st_acc[k];
 #endif
         // outputs (segment lane 0); instance-rounds = sum of (round + 1), loaded lane-parallel
         uint32_t lf = seg_or(lane_flags);
         uint32_t chv = canon_h < P.heights ? canon_h : P.heights;
         uint32_t part = 0;
         if (inst_local < P.n_instances)
-            for (uint32_t x = 1 + me; x <= chv; x += S) part += W::gload(rec_row(x)) + 1u;
+            for (uint32_t x = 1 + me; x <= chv; x += S) part += wv.gload(rec_row(x)) + 1u;
         uint64_t vsum = seg_sum64(part);
         if (me == 0 && inst_local < P.n_instances) {
             uint32_t flags = lf | seg_flags;

@@ -1,7 +1,8 @@
 // bftsim.hip — gfx950 kernels and the C ABI of libbftsim (include/bftsim.h).
 //
 // Kernels:
-//   bft_consensus_kernel  one 64-lane wave per 64/S instances, lane = validator (bft_wave.h);
+//   bft_consensus_kernel  one 64-lane wave per 64/S instances (N <= 64), or one workgroup of
+//                         S = 128 / 256 lanes per instance (N <= 256); lane = validator (bft_wave.h);
 //   bft_hash_kernel       one lane per instance: Keccak-256 of every committed header, chained
 //                         through prev_hash (power-of-two N, where proposer seeds are always 0
 //                         and the consensus kernel does not need hashes);
@@ -24,6 +25,7 @@ namespace bft {
 
 // ------------------------------------------------------------------------------ wave ops (gfx950)
 struct WaveHip {
+    __device__ void init(uint8_t*) {}
     __device__ static uint32_t lane() { return __lane_id(); }
     __device__ static uint64_t ballot(bool p) { return __ballot(p); }
     __device__ static uint32_t shfl_xor(uint32_t v, int m) { return (uint32_t)__shfl_xor((int)v, m, 64); }
@@ -47,22 +49,120 @@ struct WaveHip {
     }
 };
 
+// ------------------------------------------------------------- workgroup ops (S = 64*NW lanes)
+// One instance per workgroup of NW waves. A collective = per-wave partial (ballot / butterfly)
+// written to an LDS slot by each wave's lane 0, one s_barrier, every lane combines the NW
+// partials. The slots alternate between two parities: a slot is rewritten only after the next
+// collective's barrier, which every lane reaches after finishing its reads of this one.
+template <int NW>
+struct GroupHip {
+    uint64_t* slot;       // LDS: [2 parities][4 words]
+    uint32_t par;
+    __device__ void init(uint8_t* p) { slot = (uint64_t*)p; par = 0; }
+    __device__ uint32_t lane() const { return threadIdx.x; }
+    __device__ uint64_t* cur() const { return slot + par * 4u; }
+    __device__ Bits<NW> ballot(bool p) {
+        uint64_t b = __ballot(p);
+        uint64_t* s = cur();
+        if (__lane_id() == 0) s[threadIdx.x >> 6] = b;
+        __syncthreads();
+        Bits<NW> r;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) r.w[k] = s[k];
+        par ^= 1u;
+        return r;
+    }
+    __device__ uint32_t bcast(uint32_t v, uint32_t j) {     // value of lane j (j uniform)
+        uint64_t* s = cur();
+        if (threadIdx.x == j) s[0] = v;
+        __syncthreads();
+        uint32_t r = (uint32_t)s[0];
+        par ^= 1u;
+        return r;
+    }
+    __device__ uint32_t grp_max(uint32_t v) {
+        for (int m = 1; m < 64; m <<= 1) { uint32_t o = (uint32_t)__shfl_xor((int)v, m, 64); v = v > o ? v : o; }
+        uint64_t* s = cur();
+        if (__lane_id() == 0) s[threadIdx.x >> 6] = v;
+        __syncthreads();
+        uint32_t r = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) r = (uint32_t)s[k] > r ? (uint32_t)s[k] : r;
+        par ^= 1u;
+        return r;
+    }
+    __device__ uint32_t grp_or(uint32_t v) {
+        for (int m = 1; m < 64; m <<= 1) v |= (uint32_t)__shfl_xor((int)v, m, 64);
+        uint64_t* s = cur();
+        if (__lane_id() == 0) s[threadIdx.x >> 6] = v;
+        __syncthreads();
+        uint32_t r = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) r |= (uint32_t)s[k];
+        par ^= 1u;
+        return r;
+    }
+    __device__ uint64_t grp_sum64(uint32_t v32) {
+        uint64_t v = v32;
+        for (int m = 1; m < 64; m <<= 1) {
+            uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+            v += (uint64_t)lo | ((uint64_t)hi << 32);
+        }
+        uint64_t* s = cur();
+        if (__lane_id() == 0) s[threadIdx.x >> 6] = v;
+        __syncthreads();
+        uint64_t r = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) r += s[k];
+        par ^= 1u;
+        return r;
+    }
+    __device__ void sync() { __syncthreads(); par ^= 1u; }
+    __device__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
+    __device__ static uint32_t gload(const uint32_t* p) {
+        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ static void gstore(uint32_t* p, uint32_t v) {
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+};
+
 template <bool NEED_SEED, uint32_t S>
-__global__ __launch_bounds__(64) void bft_consensus_kernel(Params p) {
+__global__ __launch_bounds__(S > 64 ? S : 64) void bft_consensus_kernel(Params p) {
     extern __shared__ uint8_t lds[];
-    Sim<WaveHip, NEED_SEED, S> sim(p, lds, blockIdx.x);
-    sim.run();
+    if constexpr (S > 64) {
+        Sim<GroupHip<(int)(S / 64)>, NEED_SEED, S> sim(p, lds, blockIdx.x);
+        sim.run();
+    } else {
+        Sim<WaveHip, NEED_SEED, S> sim(p, lds, blockIdx.x);
+        sim.run();
+    }
 }
 
 template <bool NEED_SEED>
-static void launch_consensus(uint32_t seg, dim3 grid, size_t lds, hipStream_t s, const Params& p) {
+static hipError_t launch_consensus(uint32_t seg, dim3 grid, size_t lds, hipStream_t s, const Params& p) {
     switch (seg) {
+        case 128: {
+            hipError_t e = hipFuncSetAttribute((const void*)bft_consensus_kernel<NEED_SEED, 128>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 128>), grid, dim3(128), lds, s, p);
+            break;
+        }
+        case 256: {
+            hipError_t e = hipFuncSetAttribute((const void*)bft_consensus_kernel<NEED_SEED, 256>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 256>), grid, dim3(256), lds, s, p);
+            break;
+        }
         case 4: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 4>), grid, dim3(64), lds, s, p); break;
         case 8: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 8>), grid, dim3(64), lds, s, p); break;
         case 16: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 16>), grid, dim3(64), lds, s, p); break;
         case 32: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 32>), grid, dim3(64), lds, s, p); break;
         default: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 64>), grid, dim3(64), lds, s, p); break;
     }
+    return hipGetLastError();
 }
 
 // one wave per instance: the cooperative Keccak of bft_coop_hash.h
@@ -213,7 +313,7 @@ const char* bftsim_last_error(bftsim_t* h) { return h ? h->err.c_str() : "null h
 int bftsim_create(const bftsim_config* cfg, int hip_device, bftsim_t** out) {
     if (!cfg || !out) return BFTSIM_EINVAL;
     *out = nullptr;
-    if (cfg->n < 1 || cfg->n > 64) return BFTSIM_EUNSUPPORTED;   // GPU path: N <= 64 this round
+    if (cfg->n < 1 || cfg->n > 256) return BFTSIM_EUNSUPPORTED;
     if (cfg->heights < 1 || cfg->heights > (1u << 20) || cfg->max_ticks < 1 || cfg->max_ticks > (1u << 28) ||
         !cfg->addresses || cfg->phase_cap < 1 || cfg->phase_cap > 255 || cfg->block_period < 1)
         return BFTSIM_EINVAL;
@@ -308,7 +408,8 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     {
         static uint64_t* d_st = nullptr;
         static uint64_t cap = 0;
-        uint64_t waves = (n + (64 / h->seg) - 1) / (64 / h->seg);
+        uint64_t per = h->seg > 64 ? 1 : 64 / h->seg;
+        uint64_t waves = (n + per - 1) / per;
         if (waves > cap) { (void)hipFree(d_st); HIPCHECK(h, hipMalloc(&d_st, waves * 96)); cap = waves; }
         HIPCHECK(h, hipMemsetAsync(d_st, 0, waves * 96, s));
         p.stamps = d_st;
@@ -317,12 +418,12 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     }
 #endif
     HIPCHECK(h, hipMemsetAsync(h->d_rec, 0, n * h->hcap * 16, s));
-    uint32_t per_wave = 64u / h->seg;
-    uint32_t grid = (uint32_t)((n + per_wave - 1) / per_wave);
+    uint32_t per_block = h->seg > 64 ? 1u : 64u / h->seg;      // instances per workgroup
+    uint32_t grid = (uint32_t)((n + per_block - 1) / per_block);
+    size_t lds = bft::lds_bytes(h->seg, p.need_seed != 0);
     HIPCHECK(h, hipEventRecord(h->ev[0], s));
-    if (p.need_seed) bft::launch_consensus<true>(h->seg, dim3(grid), bft::LDS_BYTES_SEED, s, p);
-    else bft::launch_consensus<false>(h->seg, dim3(grid), bft::LDS_BYTES_POW2, s, p);
-    HIPCHECK(h, hipGetLastError());
+    if (p.need_seed) HIPCHECK(h, bft::launch_consensus<true>(h->seg, dim3(grid), lds, s, p));
+    else HIPCHECK(h, bft::launch_consensus<false>(h->seg, dim3(grid), lds, s, p));
     HIPCHECK(h, hipEventRecord(h->ev[1], s));
     if (!p.need_seed) {
         if (h->hash_mode == 1)

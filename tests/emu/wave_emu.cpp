@@ -1,5 +1,6 @@
-// wave_emu.cpp — TEST-ONLY CPU emulation of one 64-lane wavefront running the SAME kernel body
-// (consensus-rs_amd/csrc/bft_wave.h) that the gfx950 kernel runs. Each lane is a ucontext fiber;
+// wave_emu.cpp — TEST-ONLY CPU emulation of one 64-lane wavefront (or one workgroup of S = 128 /
+// 256 lanes for N > 64) running the SAME kernel body (consensus-rs_amd/csrc/bft_wave.h) that the
+// gfx950 kernel runs. Each lane is a ucontext fiber;
 // collectives (ballot, shfl_xor, sync) are rendezvous points where every live lane must arrive at
 // the same collective — a non-uniform collective aborts, which catches divergence bugs before
 // they reach the GPU. Never linked into libbftsim.
@@ -17,16 +18,19 @@
 
 namespace {
 
+constexpr int MAXL = 256;
 struct Sched {
     ucontext_t main_ctx;
-    ucontext_t ctx[64];
-    std::vector<char> stack[64];
-    bool done[64];
+    ucontext_t ctx[MAXL];
+    std::vector<char> stack[MAXL];
+    bool done[MAXL];
+    int nl;           // lanes: 64, or S for a workgroup segment
     int cur;
-    int op[64];
-    uint64_t arg[64];
-    uint64_t res[64];
-    uint64_t seq[64];
+    int op[MAXL];
+    uint64_t arg[MAXL];
+    uint64_t res[MAXL];
+    uint64_t res4[4];  // workgroup ballot words
+    uint64_t seq[MAXL];
     const bft::Params* P;
     uint8_t* lds;
     uint32_t wave;
@@ -36,7 +40,15 @@ thread_local Sched* g = nullptr;
 
 void yield_to_sched() { swapcontext(&g->ctx[g->cur], &g->main_ctx); }
 
+uint64_t collective(int op, uint64_t arg) {
+    int l = g->cur;
+    g->op[l] = op; g->arg[l] = arg; g->seq[l]++;
+    yield_to_sched();
+    return g->res[l];
+}
+
 struct EmuWave {
+    void init(uint8_t*) {}
     static uint32_t lane() { return (uint32_t)g->cur; }
     static uint64_t ballot(bool p) {
         int l = g->cur;
@@ -67,10 +79,36 @@ struct EmuWave {
     static void gstore(uint32_t* p, uint32_t v) { *p = v; }
 };
 
+// the workgroup flavour (S = 64*NW lanes): same collectives as GroupHip in bftsim.hip
+template <int NW>
+struct EmuGroup {
+    void init(uint8_t*) {}
+    static uint32_t lane() { return (uint32_t)g->cur; }
+    bft::Bits<NW> ballot(bool p) {
+        collective(1, p ? 1 : 0);
+        bft::Bits<NW> r;
+        for (int k = 0; k < NW; ++k) r.w[k] = g->res4[k];
+        return r;
+    }
+    uint32_t bcast(uint32_t v, uint32_t j) { return (uint32_t)collective(5, (uint64_t)v | ((uint64_t)j << 32)); }
+    uint32_t grp_max(uint32_t v) { return (uint32_t)collective(6, v); }
+    uint32_t grp_or(uint32_t v) { return (uint32_t)collective(7, v); }
+    uint64_t grp_sum64(uint32_t v) { return collective(8, v); }
+    void sync() { collective(3, 0); }
+    static uint64_t clock() { return 0; }
+    static uint32_t gload(const uint32_t* p) { return *p; }
+    static void gstore(uint32_t* p, uint32_t v) { *p = v; }
+};
+
 template <bool NS, uint32_t S>
 void run_sim() {
-    bft::Sim<EmuWave, NS, S> sim(*g->P, g->lds, g->wave);
-    sim.run();
+    if constexpr (S > 64) {
+        bft::Sim<EmuGroup<(int)(S / 64)>, NS, S> sim(*g->P, g->lds, g->wave);
+        sim.run();
+    } else {
+        bft::Sim<EmuWave, NS, S> sim(*g->P, g->lds, g->wave);
+        sim.run();
+    }
 }
 template <bool NS>
 void run_sim_s(uint32_t seg) {
@@ -79,6 +117,8 @@ void run_sim_s(uint32_t seg) {
         case 8: run_sim<NS, 8>(); break;
         case 16: run_sim<NS, 16>(); break;
         case 32: run_sim<NS, 32>(); break;
+        case 128: run_sim<NS, 128>(); break;
+        case 256: run_sim<NS, 256>(); break;
         default: run_sim<NS, 64>(); break;
     }
 }
@@ -99,14 +139,15 @@ void lane_entry(int lane) {
     g->op[lane] = 0;
 }
 
-int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds, int body = 0) {
-    Sched s;
+int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds, int body = 0, int nl = 64) {
+    static thread_local Sched s;
     g = &s;
+    s.nl = nl;
     s.body = body;
     s.P = &P;
     s.lds = lds.data();
     s.wave = wave;
-    for (int l = 0; l < 64; ++l) {
+    for (int l = 0; l < nl; ++l) {
         s.done[l] = false;
         s.op[l] = 0;
         s.seq[l] = 0;
@@ -118,26 +159,41 @@ int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds, int
         makecontext(&s.ctx[l], (void (*)())lane_entry, 1, l);
     }
     for (;;) {
-        for (int l = 0; l < 64; ++l) {
+        for (int l = 0; l < nl; ++l) {
             if (s.done[l]) continue;
             s.cur = l;
             swapcontext(&s.main_ctx, &s.ctx[l]);
         }
         int nd = 0;
-        for (int l = 0; l < 64; ++l) nd += s.done[l];
-        if (nd == 64) break;
+        for (int l = 0; l < nl; ++l) nd += s.done[l];
+        if (nd == nl) break;
         if (nd != 0) { fprintf(stderr, "emu: lanes diverged at a collective (%d done)\n", nd); return -1; }
         int op = s.op[0];
-        for (int l = 1; l < 64; ++l)
+        for (int l = 1; l < nl; ++l)
             if (s.op[l] != op || s.seq[l] != s.seq[0]) {
                 fprintf(stderr, "emu: non-uniform collective (lane %d op %d seq %llu vs op %d seq %llu)\n", l, s.op[l],
                         (unsigned long long)s.seq[l], op, (unsigned long long)s.seq[0]);
                 return -1;
             }
         if (op == 1) {
-            uint64_t m = 0;
-            for (int l = 0; l < 64; ++l) m |= (s.arg[l] & 1ull) << l;
-            for (int l = 0; l < 64; ++l) s.res[l] = m;
+            uint64_t m4[4] = {0, 0, 0, 0};
+            for (int l = 0; l < nl; ++l) m4[l >> 6] |= (s.arg[l] & 1ull) << (l & 63);
+            for (int k = 0; k < 4; ++k) s.res4[k] = m4[k];
+            for (int l = 0; l < nl; ++l) s.res[l] = m4[0];
+        } else if (op == 5) {
+            uint32_t j = (uint32_t)(s.arg[0] >> 32);
+            for (int l = 1; l < nl; ++l)
+                if ((uint32_t)(s.arg[l] >> 32) != j) { fprintf(stderr, "emu: non-uniform bcast source\n"); return -1; }
+            for (int l = 0; l < nl; ++l) s.res[l] = (uint32_t)s.arg[j];
+        } else if (op >= 6 && op <= 8) {
+            uint64_t r = 0;
+            for (int l = 0; l < nl; ++l) {
+                uint64_t v = (uint32_t)s.arg[l];
+                if (op == 6) r = v > r ? v : r;
+                else if (op == 7) r |= v;
+                else r += v;
+            }
+            for (int l = 0; l < nl; ++l) s.res[l] = r;
         } else if (op == 4) {
             for (int l = 0; l < 64; ++l) s.res[l] = (uint32_t)s.arg[(int)(s.arg[l] >> 32)];
         } else if (op == 2) {
@@ -155,7 +211,7 @@ int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds, int
 
 extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bftsim_result* out,
                        uint64_t* trace, uint32_t trace_ticks) {
-    if (cfg->n < 1 || cfg->n > 64) return -4;
+    if (cfg->n < 1 || cfg->n > 256) return -4;
     uint8_t gh[32];
     bft::host_genesis_hash(cfg, gh);
     uint32_t gseed = bft::seed_from_hash(gh, cfg->n);
@@ -177,12 +233,12 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
     P.hash = hs.data();
     P.trace = trace;
     P.trace_ticks = trace ? trace_ticks : 0;
-    uint32_t per_wave = 64 / seg;
+    uint32_t per_wave = seg > 64 ? 1 : 64 / seg;
     uint32_t waves = (uint32_t)((n + per_wave - 1) / per_wave);
-    std::vector<uint8_t> lds(bft::lds_bytes_per_wave(P.need_seed));
+    std::vector<uint8_t> lds(bft::lds_bytes(seg, P.need_seed != 0));
     for (uint32_t w = 0; w < waves; ++w) {
         memset(lds.data(), 0xcd, lds.size());
-        if (run_wave(P, w, lds)) return -1;
+        if (run_wave(P, w, lds, 0, seg > 64 ? (int)seg : 64)) return -1;
     }
     // power-of-two N: the hash post-pass, as bft_hash_coop_kernel (one wave per instance,
     // BFTSIM_HASH=coop) or bft_hash_lane_kernel (one lane per instance, default)

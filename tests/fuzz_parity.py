@@ -1,5 +1,6 @@
 """Randomized parity fuzz: CPU wave emulator (the kernel body) vs the oracle on random configs.
-Usage: python tests/fuzz_parity.py [seconds]. Test-only tool (not collected by pytest)."""
+Usage: python tests/fuzz_parity.py [seconds] [rng seed] [big]. `big` draws N in 65..256 (the
+workgroup-segment kernels). Test-only tool (not collected by pytest)."""
 import random
 import sys
 import time
@@ -10,8 +11,11 @@ from bftsim.configs import BftConfig
 from parity_util import mismatches
 
 
-def random_config(rng):
-    n = rng.choice([1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 16, 17, 21, 31, 32, 33, 40, 63, 64])
+def random_config(rng, big=False):
+    if big:
+        n = rng.choice([65, 66, 80, 100, 127, 128, 129, 150, 200, 255, 256])
+    else:
+        n = rng.choice([1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 16, 17, 21, 31, 32, 33, 40, 63, 64])
     byz = rng.choice([0, 0, 0, 1, n // 3, max(0, (n - 1) // 3), n // 2])
     drop = rng.choice([0, 0, 20_000, 100_000, 250_000, 500_000])
     crash = rng.choice([0, 0, 100_000, 400_000])
@@ -26,11 +30,12 @@ def random_config(rng):
 def main():
     budget = float(sys.argv[1]) if len(sys.argv) > 1 else 60
     rng = random.Random(int(sys.argv[2]) if len(sys.argv) > 2 else 1234)
+    big = len(sys.argv) > 3 and sys.argv[3] == "big"
     t0, runs, fails = time.time(), 0, 0
     while time.time() - t0 < budget:
-        cfg = random_config(rng)
+        cfg = random_config(rng, big)
         first = rng.randrange(1 << 20)
-        n_inst = rng.choice([1, 3, 8])
+        n_inst = rng.choice([1, 2] if big else [1, 3, 8])
         a = O.run(cfg, first, n_inst)
         b = E.run(cfg, first, n_inst)
         bad = mismatches(a, b)

@@ -38,8 +38,8 @@ def test_create_rejects_bad_configs_without_gpu():
     h = ctypes.c_void_p()
     cc.n = 0
     assert L.bftsim_create(ctypes.byref(cc), 0, ctypes.byref(h)) < 0
-    cc.n = 65
-    assert L.bftsim_create(ctypes.byref(cc), 0, ctypes.byref(h)) == -4      # N > 64: unsupported on GPU
+    cc.n = 257
+    assert L.bftsim_create(ctypes.byref(cc), 0, ctypes.byref(h)) == -4      # N > 256: unsupported
     cc.n = 64
     cc.phase_cap = 0
     assert L.bftsim_create(ctypes.byref(cc), 0, ctypes.byref(h)) < 0

@@ -18,6 +18,13 @@ CASES = [
     ("n4-cap2-drop30", lambda: BftConfig(n=4, heights=25, seed=12, drop_ppm=300_000, phase_cap=2), 0, 16),
     ("n16-crash-drop", lambda: BftConfig(n=16, heights=15, seed=21, drop_ppm=150_000,
                                          proposer_crash_ppm=300_000), 0, 4),
+    # workgroup segments (N > 64: 2 or 4 waves per instance, multi-word sender bitmaps)
+    ("cfg4-n65", lambda: cfg4(65, heights=10), 5, 2),
+    ("cfg4-n100", lambda: cfg4(100, heights=8), 0, 1),
+    ("cfg4-n256", lambda: cfg4(256, heights=6), 2, 1),
+    ("n130-byz43-drop", lambda: BftConfig(n=130, heights=8, seed=31, byz_count=43, drop_ppm=100_000), 0, 1),
+    ("n200-silent-crash", lambda: BftConfig(n=200, heights=6, seed=32, silent=[0, 77, 199],
+                                            proposer_crash_ppm=300_000), 0, 1),
 ]
 
 

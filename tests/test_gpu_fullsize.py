@@ -68,6 +68,18 @@ def test_cfg4_sweep_4096(nv):
     _full_parity(cfg, r, 0, 4096)
 
 
+@pytest.mark.parametrize("nv", [65, 100, 128, 200, 256])
+def test_cfg4_large_n(nv):
+    # N > 64 (workgroup segments): whole-output oracle parity on 512 instances, 100 heights
+    cfg = cfg4(nv)
+    sim = _sim(cfg)
+    r = sim.run(0, 512)
+    sim.close()
+    assert (r["committed_height"] == 100).all()
+    assert O.verify_chains(cfg, 0, r, threads=16) == 0
+    _full_parity(cfg, r, 0, 512)
+
+
 def test_determinism_shards_and_stats():
     cfg = cfg2(heights=40)
     sim = _sim(cfg)

@@ -37,7 +37,13 @@ CASES = [
     ("n64-byz21-drop5", lambda: BftConfig(n=64, heights=20, seed=15, byz_count=21, drop_ppm=50_000), 0, 4),
     ("n1", lambda: BftConfig(n=1, heights=20), 0, 8),
     ("n2", lambda: BftConfig(n=2, heights=20, drop_ppm=100_000), 0, 8),
-] + [(f"cfg4-n{n}", (lambda n=n: cfg4(n, heights=60)), 0, 24) for n in (4, 7, 10, 16, 31, 32, 33, 63, 64)]
+    # N > 64: one workgroup of 128 / 256 lanes per instance
+    ("n100-byz33-drop10", lambda: BftConfig(n=100, heights=30, seed=16, byz_count=33, drop_ppm=100_000), 0, 8),
+    ("n256-byz85", lambda: BftConfig(n=256, heights=20, seed=17, byz_count=85), 0, 4),
+    ("n129-silent-crash", lambda: BftConfig(n=129, heights=30, seed=18, silent=[0, 64, 128],
+                                            proposer_crash_ppm=300_000, drop_ppm=20_000), 0, 8),
+] + [(f"cfg4-n{n}", (lambda n=n: cfg4(n, heights=60)), 0, 24)
+     for n in (4, 7, 10, 16, 31, 32, 33, 63, 64, 65, 100, 128, 200, 256)]
 
 
 @pytest.mark.parametrize("name,mk,first,n", CASES, ids=[c[0] for c in CASES])
