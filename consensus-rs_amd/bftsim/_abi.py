@@ -28,7 +28,8 @@ class CResult(ctypes.Structure):
 class CStats(ctypes.Structure):
     _fields_ = [("instances", ctypes.c_uint64), ("committed_heights", ctypes.c_uint64),
                 ("views", ctypes.c_uint64), ("ticks", ctypes.c_uint64),
-                ("flagged", ctypes.c_uint64 * 6), ("round_hist", ctypes.c_uint64 * 65)]
+                ("flagged", ctypes.c_uint64 * 7), ("round_hist", ctypes.c_uint64 * 65),
+                ("latency_hist", ctypes.c_uint64 * 65)]
 
 
 def to_cconfig(cfg: BftConfig):

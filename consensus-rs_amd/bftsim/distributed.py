@@ -20,32 +20,44 @@ def strong_shard(rank: int, world: int, total: int) -> Tuple[int, int]:
     return first, base + (1 if rank < rem else 0)
 
 
+N_FLAGS = 7
+
+
 def stats_vector(st: Dict) -> list:
-    return [st[k] for k in STAT_KEYS] + list(st["flagged"]) + list(st["round_hist"])
+    return ([st[k] for k in STAT_KEYS] + list(st["flagged"]) + list(st["round_hist"]) +
+            list(st.get("latency_hist", [0] * 65)))
 
 
 def all_reduce_stats(st: Dict, device=None) -> Dict:
-    """Sum a bftsim_stats dict over all ranks of the default process group."""
+    """Sum a bftsim_stats dict (totals + the rounds-to-commit and commit-latency histograms) over
+    all ranks of the default process group: one int64 all-reduce of 145 words."""
     import torch
     import torch.distributed as dist
-    v = torch.tensor(stats_vector(st), dtype=torch.float64, device=device)
+    v = torch.tensor(stats_vector(st), dtype=torch.int64, device=device)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(v)
     v = [int(x) for x in v.tolist()]
     out = dict(zip(STAT_KEYS, v[:4]))
-    out["flagged"] = v[4:10]
-    out["round_hist"] = v[10:75]
+    f0 = 4 + N_FLAGS
+    out["flagged"] = v[4:f0]
+    out["round_hist"] = v[f0:f0 + 65]
+    out["latency_hist"] = v[f0 + 65:f0 + 130]
     return out
 
 
 def stats_from_result(r) -> Dict:
     """The bftsim_stats of a result dict (host arrays), as bft_stats_kernel computes it."""
-    import numpy as np
     ch = r["committed_height"]
-    hist = [0] * 65
-    for i in range(len(ch)):
-        for x in r["round"][i][: ch[i]]:
-            hist[min(int(x), 64)] += 1
-    return dict(instances=len(ch), committed_heights=int(ch.sum()), views=int(r["views"].sum()),
-                ticks=int(r["ticks"].sum()),
-                flagged=[int(((r["flags"] >> b) & 1).sum()) for b in range(6)], round_hist=hist)
+    if "round" in r:
+        hist = [0] * 65
+        for i in range(len(ch)):
+            for x in r["round"][i][: ch[i]]:
+                hist[min(int(x), 64)] += 1
+    else:                              # a streamed result carries its histograms
+        hist = [int(x) for x in r["round_hist"]]
+    out = dict(instances=len(ch), committed_heights=int(ch.sum()), views=int(r["views"].sum()),
+               ticks=int(r["ticks"].sum()),
+               flagged=[int(((r["flags"] >> b) & 1).sum()) for b in range(N_FLAGS)], round_hist=hist)
+    if "latency_hist" in r:            # commit ticks are not per-height rows: taken from the producer
+        out["latency_hist"] = [int(x) for x in r["latency_hist"]]
+    return out

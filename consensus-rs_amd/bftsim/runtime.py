@@ -40,6 +40,8 @@ def lib():
         L.bftsim_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
                                             ctypes.POINTER(ctypes.c_float)]
         L.bftsim_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
+        L.bftsim_set_window.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        L.bftsim_fetch_summary.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5
         L.bftsim_two_thirds_majority.restype = ctypes.c_uint32
         L.bftsim_seed_from_hash.restype = ctypes.c_uint32
         L.bftsim_seed_from_hash.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
@@ -96,7 +98,35 @@ class Simulator:
         arrs = _abi.shape_result(arrs, n, self.cfg.heights)
         if tr is not None:
             arrs["trace"] = tr.reshape(n, trace_ticks, self.cfg.n)
+        st = self.stats()
+        arrs["round_hist"] = np.array(st["round_hist"], np.uint64)
+        arrs["latency_hist"] = np.array(st["latency_hist"], np.uint64)
         return arrs
+
+    def set_window(self, window: int):
+        """Keep a ring of `window` canonical rows per instance (0: every height); see bftsim.h."""
+        _check(self.h, lib().bftsim_set_window(self.h, window), "bftsim_set_window")
+
+    def fetch_summary(self, n: int, tips: bool = True):
+        out = dict(committed_height=np.zeros(n, np.uint32), flags=np.zeros(n, np.uint32),
+                   ticks=np.zeros(n, np.uint32), views=np.zeros(n, np.uint64))
+        if tips:
+            out["tip_hash"] = np.zeros((n, 32), np.uint8)
+        _check(self.h, lib().bftsim_fetch_summary(
+            self.h, out["committed_height"].ctypes.data, out["flags"].ctypes.data, out["ticks"].ctypes.data,
+            out["views"].ctypes.data, out["tip_hash"].ctypes.data if tips else None), "bftsim_fetch_summary")
+        return out
+
+    def run_stream(self, first: int, n: int, window: int = 256):
+        """Windowed run (long horizons): per-instance outputs, tip hashes and histograms."""
+        self.set_window(window)
+        self.prepare(n)
+        self.launch(first)
+        out = self.fetch_summary(n)
+        st = self.stats()
+        out["round_hist"] = np.array(st["round_hist"], np.uint64)
+        out["latency_hist"] = np.array(st["latency_hist"], np.uint64)
+        return out
 
     # device-resident path (bench)
     def prepare(self, n: int):
@@ -118,4 +148,5 @@ class Simulator:
         s = _abi.CStats()
         _check(self.h, lib().bftsim_stats_get(self.h, ctypes.byref(s)), "bftsim_stats_get")
         return dict(instances=s.instances, committed_heights=s.committed_heights, views=s.views,
-                    ticks=s.ticks, flagged=list(s.flagged), round_hist=list(s.round_hist))
+                    ticks=s.ticks, flagged=list(s.flagged), round_hist=list(s.round_hist),
+                    latency_hist=list(s.latency_hist))

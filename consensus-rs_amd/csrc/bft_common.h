@@ -23,7 +23,7 @@ struct Params {
     uint32_t n;               // validators per instance (1..256)
     uint32_t seg;             // lanes per instance segment: power of two >= n (> 64: one workgroup)
     uint32_t heights;         // H
-    uint32_t hcap;            // rows per instance in the record tables (H + margin)
+    uint32_t hcap;            // height limit of the record tables (H + margin): x >= hcap freezes
     uint32_t max_ticks;
     uint32_t block_period;
     uint64_t genesis_time;
@@ -52,11 +52,15 @@ struct Params {
     uint32_t trace_ticks;
     uint32_t pad1;
     uint64_t* stamps;                 // diagnostic builds only (BFT_STAMPS): [waves][8] cycles per section
+    uint64_t* hist;                   // [130] summed rounds-to-commit (65) + commit-latency (65) bins
+    uint32_t window_mask;             // 0: rec/hash rows for every height; else ring of window_mask+1 rows
+    uint32_t rows;                    // rec/hash rows per instance (hcap, or the ring size)
 };
 
 // flags (same bits as the oracle)
 constexpr uint32_t FLAG_SAFETY = 1u, FLAG_PHASE_CAP = 2u, FLAG_CORE_PANIC = 4u, FLAG_OUTBOX = 8u,
-                   FLAG_TIMEOUT = 16u, FLAG_RCS_OVERFLOW = 32u;
+                   FLAG_TIMEOUT = 16u, FLAG_RCS_OVERFLOW = 32u, FLAG_WINDOW = 64u;
+constexpr uint32_t HIST_BINS = 130;      // [0,65) rounds-to-commit, [65,130) commit latency (ticks)
 
 // State (src/protocol/mod.rs:25-30)
 constexpr uint32_t ST_ACCEPT_REQUEST = 1, ST_PREPREPARED = 2, ST_PREPARED = 3, ST_COMMITTED = 4;
@@ -102,6 +106,7 @@ struct Bits {
     BFT_FN static Bits from(uint64_t x) { Bits b = zero(); b.w[0] = x; return b; }
     BFT_FN static Bits from(const Bits& x) { return x; }
     BFT_FN static Bits low(uint32_t n) {          // bits [0, n), n <= 64*NW
+        if (NW == 1) { Bits b; b.w[0] = n >= 64u ? ~0ull : ((1ull << n) - 1ull); return b; }
         Bits b;
         for (int k = 0; k < NW; ++k) {
             uint32_t lo = 64u * (uint32_t)k;
@@ -127,6 +132,10 @@ struct Bits {
         uint32_t c = 0;
         for (int k = 0; k < NW; ++k) c += (uint32_t)__builtin_popcountll(w[k]);
         return c;
+    }
+    BFT_FN uint32_t ctz_nz() const {             // lowest set bit; the set must be non-empty
+        if (NW == 1) return (uint32_t)__builtin_ctzll(w[0]);
+        return ctz();
     }
     BFT_FN uint32_t ctz() const {                // lowest set bit, 64*NW if none
         uint32_t r = 64u * NW;
@@ -205,13 +214,16 @@ BFT_FN uint32_t lowbias32(uint32_t x) {
     return x;
 }
 
-// first sender of the receiver's rotated delivery order (SPEC.md §3)
+// first sender of the receiver's rotated delivery order (SPEC.md §3); the hash chain is split so
+// the kernel computes the per-instance and per-tick parts once
+BFT_FN uint32_t offset_inst_part(uint64_t seed, uint32_t inst) { return lowbias32(inst ^ (uint32_t)seed); }
+BFT_FN uint32_t offset_tick_part(uint32_t inst_part, uint32_t tick) { return lowbias32(inst_part ^ tick); }
+BFT_FN uint32_t offset_from_parts(uint64_t seed, uint32_t n, uint32_t tick_part, uint32_t phase, uint32_t recv) {
+    return mulhi32(lowbias32(tick_part ^ ((phase << 16) | recv) ^ (uint32_t)(seed >> 32)), n);
+}
 BFT_FN uint32_t delivery_offset(uint64_t seed, uint32_t n, uint32_t inst, uint32_t tick, uint32_t phase,
                                 uint32_t recv) {
-    uint32_t h = lowbias32(inst ^ (uint32_t)seed);
-    h = lowbias32(h ^ tick);
-    h = lowbias32(h ^ ((phase << 16) | recv) ^ (uint32_t)(seed >> 32));
-    return mulhi32(h, n);
+    return offset_from_parts(seed, n, offset_tick_part(offset_inst_part(seed, inst), tick), phase, recv);
 }
 
 // N-bit delivery mask of receiver `recv` for (tick, phase); self always delivered.
@@ -258,7 +270,72 @@ BFT_FN bool proposer_crashed(uint64_t seed, uint32_t thr32, uint32_t on, uint32_
 // ---------------------------------------------------------------------------------------------
 BFT_FN uint64_t rotl64(uint64_t x, int n) { return (x << n) | (x >> (64 - n)); }
 
-BFT_FN void keccak_f1600(uint64_t a[25]) {
+BFT_FN void keccak_f1600_u64(uint64_t a[25]);
+#if defined(__HIP_DEVICE_COMPILE__)
+__host__ inline void keccak_f1600(uint64_t a[25]) { keccak_f1600_u64(a); }
+// gfx950 form: the state as 32-bit halves; rotations are two v_alignbit_b32 (funnel shifts),
+// the theta parities two 3-input XORs (v_bitop3_b32 0x96) per half, chi one v_bitop3_b32 per half.
+__device__ inline uint32_t xor3_32(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+template <int N>
+__device__ inline void rotl_halves(uint32_t lo, uint32_t hi, uint32_t& ol, uint32_t& oh) {
+    if constexpr (N == 0) { ol = lo; oh = hi; }
+    else if constexpr (N == 32) { ol = hi; oh = lo; }
+    else if constexpr (N < 32) { oh = __builtin_amdgcn_alignbit(hi, lo, 32 - N); ol = __builtin_amdgcn_alignbit(lo, hi, 32 - N); }
+    else { oh = __builtin_amdgcn_alignbit(lo, hi, 64 - N); ol = __builtin_amdgcn_alignbit(hi, lo, 64 - N); }
+}
+__device__ inline void keccak_f1600(uint64_t a[25]) {
+    const uint32_t RCL[24] = {
+        0x00000001u, 0x00008082u, 0x0000808Au, 0x80008000u, 0x0000808Bu, 0x80000001u, 0x80008081u, 0x00008009u,
+        0x0000008Au, 0x00000088u, 0x80008009u, 0x8000000Au, 0x8000808Bu, 0x0000008Bu, 0x00008089u, 0x00008003u,
+        0x00008002u, 0x00000080u, 0x0000800Au, 0x8000000Au, 0x80008081u, 0x00008080u, 0x80000001u, 0x80008008u};
+    const uint32_t RCH[24] = {
+        0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0u, 0u, 0u, 0x80000000u,
+        0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u};
+    uint32_t L[25], H[25];
+#pragma unroll
+    for (int i = 0; i < 25; ++i) { L[i] = (uint32_t)a[i]; H[i] = (uint32_t)(a[i] >> 32); }
+#pragma unroll 1
+    for (int rnd = 0; rnd < 24; ++rnd) {
+        uint32_t cl[5], ch[5], dl[5], dh[5], bl[25], bh[25];
+#pragma unroll
+        for (int x = 0; x < 5; ++x) {
+            cl[x] = xor3_32(xor3_32(L[x], L[x + 5], L[x + 10]), L[x + 15], L[x + 20]);
+            ch[x] = xor3_32(xor3_32(H[x], H[x + 5], H[x + 10]), H[x + 15], H[x + 20]);
+        }
+#pragma unroll
+        for (int x = 0; x < 5; ++x) {
+            uint32_t rl, rh;
+            rotl_halves<1>(cl[(x + 1) % 5], ch[(x + 1) % 5], rl, rh);
+            dl[x] = cl[(x + 4) % 5] ^ rl;
+            dh[x] = ch[(x + 4) % 5] ^ rh;
+        }
+        // theta + rho + pi: b[y + 5*((2x+3y)%5)] = rotl(a[x+5y] ^ d[x], r[x+5y])
+#define BFT_RHO(i, n, j) rotl_halves<n>(L[i] ^ dl[(i) % 5], H[i] ^ dh[(i) % 5], bl[j], bh[j]);
+        BFT_RHO(0, 0, 0) BFT_RHO(1, 1, 10) BFT_RHO(2, 62, 20) BFT_RHO(3, 28, 5) BFT_RHO(4, 27, 15)
+        BFT_RHO(5, 36, 16) BFT_RHO(6, 44, 1) BFT_RHO(7, 6, 11) BFT_RHO(8, 55, 21) BFT_RHO(9, 20, 6)
+        BFT_RHO(10, 3, 7) BFT_RHO(11, 10, 17) BFT_RHO(12, 43, 2) BFT_RHO(13, 25, 12) BFT_RHO(14, 39, 22)
+        BFT_RHO(15, 41, 23) BFT_RHO(16, 45, 8) BFT_RHO(17, 15, 18) BFT_RHO(18, 21, 3) BFT_RHO(19, 8, 13)
+        BFT_RHO(20, 18, 14) BFT_RHO(21, 2, 24) BFT_RHO(22, 61, 9) BFT_RHO(23, 56, 19) BFT_RHO(24, 14, 4)
+#undef BFT_RHO
+        // chi
+#pragma unroll
+        for (int y = 0; y < 5; ++y)
+#pragma unroll
+            for (int x = 0; x < 5; ++x) {
+                L[5 * y + x] = bl[5 * y + x] ^ (~bl[5 * y + (x + 1) % 5] & bl[5 * y + (x + 2) % 5]);
+                H[5 * y + x] = bh[5 * y + x] ^ (~bh[5 * y + (x + 1) % 5] & bh[5 * y + (x + 2) % 5]);
+            }
+        L[0] ^= RCL[rnd];
+        H[0] ^= RCH[rnd];
+    }
+#pragma unroll
+    for (int i = 0; i < 25; ++i) a[i] = (uint64_t)L[i] | ((uint64_t)H[i] << 32);
+}
+#else
+BFT_FN void keccak_f1600(uint64_t a[25]) { keccak_f1600_u64(a); }
+#endif
+// the plain 64-bit form (host code, the CPU emulator)
+BFT_FN void keccak_f1600_u64(uint64_t a[25]) {
     const uint64_t RC[24] = {
         0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull,
         0x000000000000808Bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,

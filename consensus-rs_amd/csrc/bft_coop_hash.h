@@ -194,14 +194,14 @@ BFT_FN void hash_chain_wave(const Params& p, uint32_t il, uint8_t* buf) {
         for (int b = 0; b < 8; ++b) prev |= (uint64_t)g[b] << (8 * b);
     }
     for (uint32_t x = 1; x <= ch; ++x) {
-        const uint32_t* row = p.rec + ((uint64_t)il * p.hcap + x) * 4;
+        const uint32_t* row = p.rec + ((uint64_t)il * p.rows + x) * 4;
         uint32_t w1 = row[1];
         uint32_t prop = w1 & 0xffffu, var = (w1 >> 16) & 1u, T = row[2];
         uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)T + 1ull);
         uint64_t a;
         Coop<W>::header_hash(a, prev, buf, lane, p.addresses + 20u * prop, p.seed, inst, x, prop, var, time);
         if ((lane & 7u) == 0 && lane < 32u) {
-            uint32_t* dst = (uint32_t*)(p.hash + ((uint64_t)il * p.hcap + x) * 32) + 2u * (lane >> 3);
+            uint32_t* dst = (uint32_t*)(p.hash + ((uint64_t)il * p.rows + x) * 32) + 2u * (lane >> 3);
             dst[0] = (uint32_t)a;
             dst[1] = (uint32_t)(a >> 32);
         }

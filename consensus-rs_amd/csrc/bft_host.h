@@ -70,6 +70,7 @@ inline Params params_from_config(const bftsim_config& c, uint32_t seg, uint32_t 
     p.seg = seg;
     p.heights = c.heights;
     p.hcap = hcap;
+    p.rows = hcap;
     p.max_ticks = c.max_ticks;
     p.block_period = c.block_period;
     p.genesis_time = c.genesis_time;

@@ -20,6 +20,14 @@
 
 namespace bft {
 
+// build-time variants for A/B measurements (the defaults are the product)
+#ifndef BFT_PP_PATH
+#define BFT_PP_PATH 0          // single-Preprepare phases through the summary instead of LDS records
+#endif
+#ifndef BFT_LAZY_PUBLISH
+#define BFT_LAZY_PUBLISH 1     // publish outbox records to LDS only for general-path phases
+#endif
+
 constexpr int REC_WORDS = 22;            // LDS words per published outbox record
 
 // outbox record flags
@@ -101,6 +109,8 @@ struct Sim {
     uint32_t canon_h, done_tick, seg_flags;
     uint64_t canon_tip;      // canonical block at canon_h (segment-uniform cache; 0 at genesis)
     uint32_t canon_tip_seed;
+    uint32_t canon_tick;     // tick that recorded canon_h (commit-latency histogram)
+    uint64_t views_acc;      // instance-rounds of the recorded heights <= H
     // Core + RoundState (round_state.rs:12-22)
     uint32_t h, r, st;
     bool wait;
@@ -122,6 +132,7 @@ struct Sim {
     Outbox nx;
     // Core commit of this phase (for canonical resolution)
     uint32_t commit_x, commit_round, commit_seed;
+    uint32_t off_inst, off_tick;     // hoisted parts of delivery_offset (SPEC.md §3)
     uint64_t commit_blk;
     uint32_t lane_flags;
 #ifdef BFT_STAMPS
@@ -150,6 +161,8 @@ struct Sim {
         canon_h = 0;
         canon_tip = 0;
         canon_tip_seed = p.genesis_seed;
+        canon_tick = 0;
+        views_acc = 0;
         done_tick = p.max_ticks;
         seg_flags = 0;
         h = 0; r = 0; st = ST_ACCEPT_REQUEST; wait = false;
@@ -166,30 +179,43 @@ struct Sim {
         outbox_clear(nx);
         commit_x = 0; commit_round = 0; commit_seed = 0; commit_blk = 0;
         lane_flags = 0;
+        off_inst = offset_inst_part(p.seed, inst);
+        off_tick = 0;
     }
 
     // ---------------------------------------------------------------- global canonical table
-    BFT_FN uint32_t* rec_row(uint32_t x) const { return P.rec + ((uint64_t)inst_local * P.hcap + x) * 4; }
-    BFT_FN uint8_t* hash_row(uint32_t x) const { return P.hash + ((uint64_t)inst_local * P.hcap + x) * 32; }
-    BFT_FN uint32_t canon_seed(uint32_t x) const {
+    // row of height x: every height (window_mask == 0), or a ring of the last window_mask+1 heights
+    BFT_FN uint64_t row_of(uint32_t x) const {
+        return (uint64_t)inst_local * P.rows + (P.window_mask ? (x & P.window_mask) : x);
+    }
+    BFT_FN uint32_t* rec_row(uint32_t x) const { return P.rec + row_of(x) * 4; }
+    BFT_FN uint8_t* hash_row(uint32_t x) const { return P.hash + row_of(x) * 32; }
+    // a lookup of canonical height x older than the ring holds
+    BFT_FN void check_window(uint32_t x) {
+        if (P.window_mask && x + P.window_mask < canon_h) lane_flags |= FLAG_WINDOW;
+    }
+    BFT_FN uint32_t canon_seed(uint32_t x) {
         if (x == 0) return P.genesis_seed;
         if (x == canon_h) return canon_tip_seed;
+        check_window(x);
         return wv.gload(rec_row(x) + 3);
     }
     // canonical block id at x (x >= 1, must be recorded)
-    BFT_FN uint64_t canon_blk(uint32_t x) const {
+    BFT_FN uint64_t canon_blk(uint32_t x) {
         if (x == canon_h && x != 0) return canon_tip;
+        check_window(x);
         uint32_t w1 = wv.gload(rec_row(x) + 1);
         uint32_t T = wv.gload(rec_row(x) + 2);
         return blk_make(x, w1 & 0xffffu, (w1 >> 16) & 1u, T);
     }
-    BFT_FN void prev_hash_words(uint32_t x, uint32_t w[8]) const {   // hash of canonical block x
+    BFT_FN void prev_hash_words(uint32_t x, uint32_t w[8]) {         // hash of canonical block x
         if (x == 0) {
             for (int i = 0; i < 8; ++i)
                 w[i] = (uint32_t)P.genesis_hash[4 * i] | ((uint32_t)P.genesis_hash[4 * i + 1] << 8) |
                        ((uint32_t)P.genesis_hash[4 * i + 2] << 16) | ((uint32_t)P.genesis_hash[4 * i + 3] << 24);
             return;
         }
+        check_window(x);
         const uint32_t* p = (const uint32_t*)hash_row(x);
         for (int i = 0; i < 8; ++i) w[i] = wv.gload(p + i);
     }
@@ -245,6 +271,7 @@ struct Sim {
             last_seed = canon_tip_seed;
             return;
         }
+        check_window(last);
         last_T = (int32_t)wv.gload(rec_row(last) + 2);
         last_seed = wv.gload(rec_row(last) + 3);
     }
@@ -595,8 +622,21 @@ struct Sim {
         }
     }
 
-    // record a new canonical height (segment leader; global stores for the outputs)
-    BFT_FN void record_canon(uint32_t x, uint64_t b, uint32_t round, uint32_t seed, const uint32_t* hs) {
+    // histogram bins in the unused words 5..7 of the commit hand-off slots (LDS, per wave)
+    BFT_FN uint32_t* hist_slot(uint32_t b) const {
+        return (uint32_t*)(lds + LDS_CMT_OFF) + (b / 3u) * 8u + 5u + (b % 3u);
+    }
+    // record a new canonical height (segment leader; global stores for the outputs). `ctick` is the
+    // tick of the previous canonical record; returns the instance-rounds to add (0 beyond H).
+    BFT_FN uint32_t record_canon(uint32_t x, uint64_t b, uint32_t round, uint32_t seed, const uint32_t* hs,
+                                 uint32_t ctick) {
+        uint32_t add = 0;
+        if (x <= P.heights) {
+            uint32_t lat = (uint32_t)tick - ctick;
+            wv.lds_add(hist_slot(round < 64u ? round : 64u), 1u);
+            wv.lds_add(hist_slot(65u + (lat < 64u ? lat : 64u)), 1u);
+            add = round + 1u;
+        }
         uint32_t* row = rec_row(x);
         wv.gstore(row + 0, round);
         wv.gstore(row + 2, blk_T(b));
@@ -606,6 +646,7 @@ struct Sim {
             uint32_t* dst = (uint32_t*)hash_row(x);
             for (int i = 0; i < 8; ++i) wv.gstore(dst + i, hs[i]);
         }
+        return add;
     }
 
     // first Core commits of the phase → canonical table, in lane order (oracle receiver order)
@@ -622,7 +663,7 @@ struct Sim {
         M segbits = bal & seg_mask;
         uint32_t* segw = (uint32_t*)(lds + LDS_SEG_OFF) + (lane / S) * 8;
         const bool mine = segbits.any() && !seg_done;
-        const uint32_t lead = segbits.any() ? segbits.ctz() : 0u;
+        const uint32_t lead = segbits.any() ? segbits.ctz_nz() : 0u;
         // fast path: every committer of the segment commits the same height as the first one
         const uint32_t* cl = (const uint32_t*)(lds + LDS_CMT_OFF) + lead * 8;
         uint32_t x0 = mine ? cl[0] : 0u;
@@ -641,10 +682,11 @@ struct Sim {
             bool fr = badm.any();
             uint32_t ch = canon_h;
             uint64_t tip = canon_tip;
-            uint32_t tseed = canon_tip_seed;
+            uint32_t tseed = canon_tip_seed, ctick = canon_tick;
+            uint64_t va = views_acc;
             if (!x0_known && x0 < P.hcap && (!fr || badm.ctz() > lead)) {
-                record_canon(x0, b0, cl[3], cl[4], (const uint32_t*)(lds + LDS_CHASH_OFF + lead * 32));
-                ch = x0; tip = b0; tseed = cl[4];
+                va += record_canon(x0, b0, cl[3], cl[4], (const uint32_t*)(lds + LDS_CHASH_OFF + lead * 32), ctick);
+                ch = x0; tip = b0; tseed = cl[4]; ctick = (uint32_t)tick;
             }
             if (x0 >= P.hcap) fr = true;
             segw[0] = ch;
@@ -652,16 +694,20 @@ struct Sim {
             segw[2] = (uint32_t)tip;
             segw[3] = (uint32_t)(tip >> 32);
             segw[4] = tseed;
+            segw[5] = (uint32_t)va;
+            segw[6] = (uint32_t)(va >> 32);
+            segw[7] = ctick;
         }
         if (mine && !uniform && lane == lead) {
             // general case: replay the commits of this phase in lane order
             uint32_t ch = canon_h;
             uint64_t tip = canon_tip;
-            uint32_t tseed = canon_tip_seed;
+            uint32_t tseed = canon_tip_seed, ctick = canon_tick;
+            uint64_t va = views_acc;
             bool fr = false;
             M bits = segbits;
             while (bits.any()) {
-                uint32_t j = bits.ctz();
+                uint32_t j = bits.ctz_nz();
                 bits.clear_lowest();
                 const uint32_t* cj = (const uint32_t*)(lds + LDS_CMT_OFF) + j * 8;
                 uint32_t x = cj[0];
@@ -672,8 +718,8 @@ struct Sim {
                     if (!blk_eq(cb, b)) { fr = true; break; }
                 } else {
                     // x == ch + 1: heights are recorded contiguously
-                    record_canon(x, b, cj[3], cj[4], (const uint32_t*)(lds + LDS_CHASH_OFF + j * 32));
-                    ch = x; tip = b; tseed = cj[4];
+                    va += record_canon(x, b, cj[3], cj[4], (const uint32_t*)(lds + LDS_CHASH_OFF + j * 32), ctick);
+                    ch = x; tip = b; tseed = cj[4]; ctick = (uint32_t)tick;
                 }
             }
             segw[0] = ch;
@@ -681,12 +727,17 @@ struct Sim {
             segw[2] = (uint32_t)tip;
             segw[3] = (uint32_t)(tip >> 32);
             segw[4] = tseed;
+            segw[5] = (uint32_t)va;
+            segw[6] = (uint32_t)(va >> 32);
+            segw[7] = ctick;
         }
         sync();
         if (mine) {
             canon_h = segw[0];
             canon_tip = (uint64_t)segw[2] | ((uint64_t)segw[3] << 32);
             canon_tip_seed = segw[4];
+            views_acc = (uint64_t)segw[5] | ((uint64_t)segw[6] << 32);
+            canon_tick = segw[7];
             if (segw[1]) { frozen = true; seg_flags |= FLAG_SAFETY; }
         }
         commit_x = 0;
@@ -735,7 +786,25 @@ struct Sim {
         uint32_t pr_h, pr_r, cm_h, cm_r, blk_lo, blk_hi;
         uint64_t pr_cls, cm_cls;              // (height, proposer) class of the digests
         bool u_pr, u_cm, u_blk;               // one view / one digest class / one range
+        uint32_t pp_src, pp_h, pp_r, pp_eq;   // the Preprepare of a single-proposer phase
+        uint64_t pp_b;
     };
+    // how a phase is delivered (segment-uniform): the closed forms read the summary only;
+    // the general path reads the published LDS records in each receiver's rotated order
+    enum : uint32_t { PATH_GENERAL = 0, PATH_BLK = 1, PATH_PC = 2, PATH_PP = 3 };
+    BFT_FN uint32_t classify(const PhaseSummary& ps) const {
+        if (!P.fast) return PATH_GENERAL;
+        const bool rest = (ps.k_ocm | ps.k_rc | ps.k_sync).any();
+        if (rest) return PATH_GENERAL;
+        if (ps.k_pp.any()) {
+            // one Preprepare and nothing else: arrival order cannot matter
+            if (BFT_PP_PATH && (ps.k_pr | ps.k_cm | ps.k_blk).none() && ps.k_pp.popc() == 1) return PATH_PP;
+            return PATH_GENERAL;
+        }
+        if (ps.k_pr.none() && ps.k_cm.none()) return (ps.k_blk.any() && ps.u_blk) ? PATH_BLK : PATH_GENERAL;
+        if (ps.k_blk.none() && ps.u_pr && ps.u_cm) return PATH_PC;
+        return PATH_GENERAL;
+    }
 
     BFT_FN M seg_bits(const M& bal) const {
         if constexpr (S >= 64) return bal;
@@ -758,17 +827,28 @@ struct Sim {
         ps.k_rc = seg_bits(ballot((f & F_RC) != 0));
         ps.k_sync = seg_bits(ballot((f & F_SYNC) != 0));
         ps.k_blk = seg_bits(ballot((f & F_BLK) != 0));
-        const bool pr = (f & F_PR) != 0, cm = (f & F_CM) != 0, bk = (f & F_BLK) != 0;
+        const bool pr = (f & F_PR) != 0, cm = (f & F_CM) != 0, bk = (f & F_BLK) != 0, pq = (f & F_PP) != 0;
         const bool prw = (f & F_PR_W) != 0, cmw = (f & F_CM_W) != 0;
         ps.pr_h = ps.pr_r = ps.cm_h = ps.cm_r = ps.blk_lo = ps.blk_hi = 0;
         ps.pr_cls = ps.cm_cls = 0;
         ps.pr_w = ps.pr_v0 = ps.pr_v1 = ps.cm_w = ps.cm_v0 = ps.cm_v1 = M::zero();
         ps.u_pr = ps.u_cm = ps.u_blk = true;
+        ps.pp_src = ps.pp_h = ps.pp_r = ps.pp_eq = 0;
+        ps.pp_b = 0;
         // leader of each kind (the first sender of the segment) and uniformity against it
         bool any_pr = ballot(pr).any(), any_cm = ballot(cm).any(), any_bk = ballot(bk).any();
+        bool any_pp = ballot(pq).any();
         bool mm_pr = false, mm_cm = false, mm_blk = false;
+        if (BFT_PP_PATH && any_pp) {
+            uint32_t j = ps.k_pp.any() ? ps.k_pp.ctz_nz() : 0u;
+            ps.pp_src = j;
+            ps.pp_h = from_seg_lane(nx.pp_h, j);
+            ps.pp_r = from_seg_lane(nx.pp_r, j);
+            ps.pp_b = (uint64_t)from_seg_lane((uint32_t)nx.pp_b, j) | ((uint64_t)from_seg_lane((uint32_t)(nx.pp_b >> 32), j) << 32);
+            ps.pp_eq = from_seg_lane(f & F_PP_EQ, j);
+        }
         if (any_pr) {
-            uint32_t j = ps.k_pr.any() ? ps.k_pr.ctz() : 0u;
+            uint32_t j = ps.k_pr.any() ? ps.k_pr.ctz_nz() : 0u;
             uint64_t cls = nx.pr_d & BLK_HP_MASK;
             ps.pr_h = from_seg_lane(nx.pr_h, j);
             ps.pr_r = from_seg_lane(nx.pr_r, j);
@@ -779,7 +859,7 @@ struct Sim {
             ps.pr_v1 = seg_bits(ballot(pr && !prw && blk_var(nx.pr_d) == 1));
         }
         if (any_cm) {
-            uint32_t j = ps.k_cm.any() ? ps.k_cm.ctz() : 0u;
+            uint32_t j = ps.k_cm.any() ? ps.k_cm.ctz_nz() : 0u;
             uint64_t cls = nx.cm_d & BLK_HP_MASK;
             ps.cm_h = from_seg_lane(nx.cm_h, j);
             ps.cm_r = from_seg_lane(nx.cm_r, j);
@@ -790,7 +870,7 @@ struct Sim {
             ps.cm_v1 = seg_bits(ballot(cm && !cmw && blk_var(nx.cm_d) == 1));
         }
         if (any_bk) {
-            uint32_t j = ps.k_blk.any() ? ps.k_blk.ctz() : 0u;
+            uint32_t j = ps.k_blk.any() ? ps.k_blk.ctz_nz() : 0u;
             ps.blk_lo = from_seg_lane(nx.blk_lo, j);
             ps.blk_hi = from_seg_lane(nx.blk_hi, j);
             mm_blk = bk && (nx.blk_lo != ps.blk_lo || nx.blk_hi != ps.blk_hi);
@@ -806,7 +886,12 @@ struct Sim {
     BFT_FN M rot(const M& m, uint32_t off) const {
         if (off == 0) return m;
         uint32_t n = P.n;
-        return (m.shr(off) | m.shl(n - off)) & M::low(n);
+        if constexpr (NW == 1) {                     // 0 < off < n <= 64: both shifts in [1, 63]
+            uint64_t nm = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+            return M::from(((m.w[0] >> off) | (m.w[0] << (n - off))) & nm);
+        } else {
+            return (m.shr(off) | m.shl(n - off)) & M::low(n);
+        }
     }
     BFT_FN static M low(uint32_t k) { return M::low(k); }
     // smallest position p in [0,n) with popcount(base | a & low(p+1) | b & low(p)) > q, else n
@@ -865,7 +950,7 @@ struct Sim {
         const bool cexists = CM.any() && (C0 | CM).popc() > q;
         uint32_t lastT = 0, t1 = 64u * NW;
         if (trig) {
-            if (lm.any()) t1 = lm.ctz();
+            if (lm.any()) t1 = lm.ctz_nz();
             if (trigB) {
                 lastT = lastPR;                                 // every prepare from tB on
             } else {
@@ -903,26 +988,27 @@ struct Sim {
         st = fin;
     }
 
-    BFT_FN void deliver_phase(const PhaseSummary& ps, const M& mk, uint32_t off) {
-        bool other = (ps.k_pp | ps.k_ocm | ps.k_rc | ps.k_sync).any();
-        if (P.fast && !other) {
-            if (ps.k_pr.none() && ps.k_cm.none()) {
-                if (ps.k_blk.any() && ps.u_blk) {          // block gossip with one range
-                    if ((mk & ps.k_blk & ~M::bit(me)).any()) handle_blocks(ps.blk_lo, ps.blk_hi);
-                    BFT_STAMP(8);
-                    return;
-                }
-            } else if (ps.k_blk.none() && ps.u_pr && ps.u_cm) {
-                if (!core_dead) deliver_prepare_commit(ps, mk, off);
-                BFT_STAMP(9);
-                return;
-            }
+    BFT_FN void deliver_phase(const PhaseSummary& ps, uint32_t path, const M& mk, uint32_t off) {
+        if (path == PATH_BLK) {                       // block gossip with one range
+            if ((mk & ps.k_blk & ~M::bit(me)).any()) handle_blocks(ps.blk_lo, ps.blk_hi);
+            BFT_STAMP(8);
+            return;
+        }
+        if (path == PATH_PC) {
+            if (!core_dead) deliver_prepare_commit(ps, mk, off);
+            BFT_STAMP(9);
+            return;
+        }
+        if (BFT_PP_PATH && path == PATH_PP) {         // deliver_from() of the single sender
+            if (mk.get(ps.pp_src) && !core_dead) handle_preprepare(ps.pp_src, ps.pp_h, ps.pp_r, ps.pp_b, ps.pp_eq != 0);
+            BFT_STAMP(8);
+            return;
         }
         // general path: every delivered non-empty sender, in rotated order, one at a time
         M any = ps.k_pp | ps.k_pr | ps.k_cm | ps.k_ocm | ps.k_rc | ps.k_sync | ps.k_blk;
         M c = rot(mk & any, off);
         while (c.any()) {
-            uint32_t pos = c.ctz();
+            uint32_t pos = c.ctz_nz();
             c.clear_lowest();
             uint32_t s = pos + off;
             if (s >= P.n) s -= P.n;
@@ -938,9 +1024,15 @@ struct Sim {
         st_t = wv.clock();
 #endif
         if (P.byz_count > 0) init_byzantine();
+        {   // zero this lane's histogram words (after init_byzantine's scratch use of the area)
+            uint32_t* hw = (uint32_t*)(lds + LDS_CMT_OFF) + lane * 8u;
+            hw[5] = hw[6] = hw[7] = 0;
+            sync();
+        }
         for (tick = 0; tick < (int32_t)P.max_ticks; ++tick) {
             if (ballot(!seg_done).none()) break;
             bool act = running && !seg_done;
+            off_tick = offset_tick_part(off_inst, (uint32_t)tick);
             BFT_STAMP(7);
             if (act) t_step();
             BFT_STAMP(0);
@@ -961,17 +1053,21 @@ struct Sim {
                 PhaseSummary ps;
                 summarize(ps);
                 BFT_STAMP(1);
-                publish();
-                sync();
+                const uint32_t path = classify(ps);
+                // records go to LDS only if some segment of the wave takes the general path
+                const bool pub = !BFT_LAZY_PUBLISH || ballot(path == PATH_GENERAL).any();
+                if (pub) { publish(); sync(); }
+                else outbox_clear(nx);
                 BFT_STAMP(2);
                 if (act && seg_pending) {
                     miner_step();                             // event step
                     M mk = deliver_mask<NW>(P.seed, P.n, P.thr16, inst, (uint32_t)tick, p, me);
-                    uint32_t off = delivery_offset(P.seed, P.n, inst, (uint32_t)tick, p, me);
+                    uint32_t off = (path == PATH_GENERAL || path == PATH_PC)
+                                       ? offset_from_parts(P.seed, P.n, off_tick, p, me) : 0u;
                     BFT_STAMP(5);
-                    deliver_phase(ps, mk, off);
+                    deliver_phase(ps, path, mk, off);
                 }
-                sync();
+                if (pub) sync();                              // records read before the next publish
                 BFT_STAMP(3);
                 resolve_commits();
                 BFT_STAMP(4);
@@ -986,18 +1082,21 @@ struct Sim {
         if (lane == 0 && P.stamps)
             for (int k = 0; k < 12; ++k) P.stamps[(uint64_t)(S >= 64 ? inst_local : inst_local / (64u / S)) * 12 + k] = st_acc[k];
 #endif
-        // outputs (segment lane 0); instance-rounds = sum of (round + 1), loaded lane-parallel
+        // outputs (segment lane 0); instance-rounds = sum of (round + 1) over heights <= H
         uint32_t lf = seg_or(lane_flags);
-        uint32_t chv = canon_h < P.heights ? canon_h : P.heights;
-        uint32_t part = 0;
-        if (inst_local < P.n_instances)
-            for (uint32_t x = 1 + me; x <= chv; x += S) part += wv.gload(rec_row(x)) + 1u;
-        uint64_t vsum = seg_sum64(part);
+        sync();
+        if (P.hist) {                                  // this wave's histogram → the launch totals
+            const uint32_t* hw = (const uint32_t*)(lds + LDS_CMT_OFF) + lane * 8u;
+            for (uint32_t k = 0; k < 3; ++k) {
+                uint32_t b = 3u * lane + k;
+                if (b < HIST_BINS && hw[5 + k] != 0) wv.gadd64(P.hist + b, hw[5 + k]);
+            }
+        }
         if (me == 0 && inst_local < P.n_instances) {
             uint32_t flags = lf | seg_flags;
             if (!frozen && canon_h < P.heights) flags |= FLAG_TIMEOUT;
             uint32_t chh = canon_h < P.heights ? canon_h : P.heights;
-            uint64_t views = vsum;
+            uint64_t views = views_acc;
             P.committed_height[inst_local] = chh;
             P.flags[inst_local] = flags;
             P.ticks[inst_local] = done_tick;

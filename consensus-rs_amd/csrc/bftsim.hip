@@ -47,6 +47,8 @@ struct WaveHip {
     __device__ static void gstore(uint32_t* p, uint32_t v) {
         __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    __device__ static void lds_add(uint32_t* p, uint32_t v) { atomicAdd(p, v); }
+    __device__ static void gadd64(uint64_t* p, uint64_t v) { atomicAdd((unsigned long long*)p, (unsigned long long)v); }
 };
 
 // ------------------------------------------------------------- workgroup ops (S = 64*NW lanes)
@@ -125,10 +127,15 @@ struct GroupHip {
     __device__ static void gstore(uint32_t* p, uint32_t v) {
         __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    __device__ static void lds_add(uint32_t* p, uint32_t v) { atomicAdd(p, v); }
+    __device__ static void gadd64(uint64_t* p, uint64_t v) { atomicAdd((unsigned long long*)p, (unsigned long long)v); }
 };
 
 template <bool NEED_SEED, uint32_t S>
-__global__ __launch_bounds__(S > 64 ? S : 64) void bft_consensus_kernel(Params p) {
+#ifndef BFT_WAVES_PER_SIMD
+#define BFT_WAVES_PER_SIMD 3   // register budget of the one-wave kernels (LDS allows ~2.75 per SIMD)
+#endif
+__global__ __launch_bounds__(S > 64 ? S : 64, S > 64 ? 1 : BFT_WAVES_PER_SIMD) void bft_consensus_kernel(Params p) {
     extern __shared__ uint8_t lds[];
     if constexpr (S > 64) {
         Sim<GroupHip<(int)(S / 64)>, NEED_SEED, S> sim(p, lds, blockIdx.x);
@@ -184,41 +191,49 @@ __global__ __launch_bounds__(64) void bft_hash_lane_kernel(Params p) {
                   ((uint32_t)p.genesis_hash[4 * i + 2] << 16) | ((uint32_t)p.genesis_hash[4 * i + 3] << 24);
     uint8_t* buf = bufs + threadIdx.x * LANE_HASH_BUF;
     for (uint32_t x = 1; x <= ch; ++x) {
-        const uint32_t* row = p.rec + ((uint64_t)il * p.hcap + x) * 4;
+        const uint32_t* row = p.rec + ((uint64_t)il * p.rows + x) * 4;
         uint32_t w1 = row[1];
         uint32_t prop = w1 & 0xffffu, var = (w1 >> 16) & 1u, T = row[2];
         uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)T + 1ull);
         uint32_t out[8];
         lane_block_hash(buf, prev, p.addresses + 20u * prop, p.seed, inst, x, prop, var, time, out);
-        uint32_t* dst = (uint32_t*)(p.hash + ((uint64_t)il * p.hcap + x) * 32);
+        uint32_t* dst = (uint32_t*)(p.hash + ((uint64_t)il * p.rows + x) * 32);
         for (int i = 0; i < 8; ++i) { dst[i] = out[i]; prev[i] = out[i]; }
     }
 }
 
-// totals: [0] instances [1] committed [2] views [3] ticks [4..9] flag counts [10..74] round hist
-// block-level reduction in LDS, then one global atomic per counter per block
+// totals: [0] instances [1] committed [2] views [3] ticks [4..10] flag counts (the histograms are
+// accumulated by the consensus kernel); block-level reduction in LDS, then one global atomic per
+// counter per block
+constexpr int STAT_WORDS = 11;
 __global__ __launch_bounds__(256) void bft_stats_kernel(Params p, unsigned long long* st) {
-    __shared__ unsigned long long acc[80];
-    for (uint32_t k = threadIdx.x; k < 80; k += 256) acc[k] = 0;
+    __shared__ unsigned long long acc[STAT_WORDS];
+    for (uint32_t k = threadIdx.x; k < STAT_WORDS; k += 256) acc[k] = 0;
     __syncthreads();
     uint32_t il = blockIdx.x * 256u + threadIdx.x;
     if (il < p.n_instances) {
-        uint32_t ch = p.committed_height[il];
         atomicAdd(&acc[0], 1ull);
-        atomicAdd(&acc[1], (unsigned long long)ch);
+        atomicAdd(&acc[1], (unsigned long long)p.committed_height[il]);
         atomicAdd(&acc[2], (unsigned long long)p.views[il]);
         atomicAdd(&acc[3], (unsigned long long)p.ticks[il]);
         uint32_t f = p.flags[il];
-        for (int b = 0; b < 6; ++b)
+        for (int b = 0; b < 7; ++b)
             if (f & (1u << b)) atomicAdd(&acc[4 + b], 1ull);
-        for (uint32_t x = 1; x <= ch; ++x) {
-            uint32_t rd = p.rec[((uint64_t)il * p.hcap + x) * 4];
-            atomicAdd(&acc[10 + (rd < 64 ? rd : 64)], 1ull);
-        }
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < 75; k += 256)
+    for (uint32_t k = threadIdx.x; k < STAT_WORDS; k += 256)
         if (acc[k]) atomicAdd(&st[k], acc[k]);
+}
+
+// hash of each instance's block at its committed height (the genesis hash at height 0): it
+// commits to the whole chain, so it stands in for the per-height rows in windowed runs
+__global__ __launch_bounds__(256) void bft_tip_kernel(Params p, uint8_t* tips) {
+    uint32_t il = blockIdx.x * 256u + threadIdx.x;
+    if (il >= p.n_instances) return;
+    uint32_t ch = p.committed_height[il];
+    const uint8_t* src = ch == 0 ? p.genesis_hash
+                                 : p.hash + ((uint64_t)il * p.rows + (p.window_mask ? (ch & p.window_mask) : ch)) * 32;
+    for (int i = 0; i < 32; ++i) tips[(uint64_t)il * 32 + i] = src[i];
 }
 
 }  // namespace bft
@@ -247,6 +262,9 @@ struct bftsim {
     uint32_t* d_rec = nullptr;
     uint8_t* d_hash = nullptr;
     unsigned long long* d_stats = nullptr;
+    uint64_t* d_hist = nullptr;       // [HIST_BINS] of the last launch
+    uint8_t* d_tips = nullptr;        // [cap_inst * 32]
+    uint32_t window = 0;              // 0: full per-height rows; else ring of `window` rows
     uint64_t* d_trace = nullptr;
     uint64_t* h_trace = nullptr;
     uint32_t trace_ticks = 0;
@@ -268,9 +286,9 @@ static int fail(bftsim* h, int code, const std::string& msg) {
 
 static void free_bufs(bftsim* h) {
     (void)hipFree(h->d_ch); (void)hipFree(h->d_flags); (void)hipFree(h->d_ticks); (void)hipFree(h->d_views);
-    (void)hipFree(h->d_rec); (void)hipFree(h->d_hash); (void)hipFree(h->d_trace);
+    (void)hipFree(h->d_rec); (void)hipFree(h->d_hash); (void)hipFree(h->d_trace); (void)hipFree(h->d_tips);
     h->d_ch = h->d_flags = h->d_ticks = nullptr; h->d_views = nullptr;
-    h->d_rec = nullptr; h->d_hash = nullptr; h->d_trace = nullptr;
+    h->d_rec = nullptr; h->d_hash = nullptr; h->d_trace = nullptr; h->d_tips = nullptr;
     h->cap_inst = 0;
 }
 
@@ -339,7 +357,8 @@ int bftsim_create(const bftsim_config* cfg, int hip_device, bftsim_t** out) {
     HIPCHECK(h, hipMemcpy(h->d_addr, h->addresses.data(), 20 * cfg->n, hipMemcpyHostToDevice));
     HIPCHECK(h, hipMalloc(&h->d_ghash, 32));
     HIPCHECK(h, hipMemcpy(h->d_ghash, h->genesis_hash, 32, hipMemcpyHostToDevice));
-    HIPCHECK(h, hipMalloc(&h->d_stats, 80 * sizeof(unsigned long long)));
+    HIPCHECK(h, hipMalloc(&h->d_stats, 16 * sizeof(unsigned long long)));
+    HIPCHECK(h, hipMalloc(&h->d_hist, bft::HIST_BINS * sizeof(uint64_t)));
     for (int i = 0; i < 3; ++i) HIPCHECK(h, hipEventCreate(&h->ev[i]));
     return BFTSIM_OK;
 }
@@ -348,7 +367,7 @@ void bftsim_destroy(bftsim_t* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     free_bufs(h);
-    (void)hipFree(h->d_addr); (void)hipFree(h->d_ghash); (void)hipFree(h->d_stats);
+    (void)hipFree(h->d_addr); (void)hipFree(h->d_ghash); (void)hipFree(h->d_stats); (void)hipFree(h->d_hist);
     for (int i = 0; i < 3; ++i) if (h->ev[i]) (void)hipEventDestroy(h->ev[i]);
     delete h;
 }
@@ -364,7 +383,20 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
     HIPCHECK(h, hipMalloc(&h->d_views, n * 8));
     HIPCHECK(h, hipMalloc(&h->d_rec, n * h->hcap * 16));
     HIPCHECK(h, hipMalloc(&h->d_hash, n * h->hcap * 32));
+    HIPCHECK(h, hipMalloc(&h->d_tips, n * 32));
     h->cap_inst = n;
+    return BFTSIM_OK;
+}
+
+int bftsim_set_window(bftsim_t* h, uint32_t window) {
+    if (!h) return BFTSIM_EINVAL;
+    if (window != 0 && (window < 64 || (window & (window - 1)) != 0 || window > (1u << 20)))
+        return fail(h, BFTSIM_EINVAL, "window must be 0 or a power of two in [64, 2^20]");
+    if (window == h->window) return BFTSIM_OK;
+    h->window = window;
+    h->hcap = window ? window : h->cfg.heights + 64;
+    (void)hipSetDevice(h->device);
+    free_bufs(h);                                   // row tables are re-sized by the next prepare
     return BFTSIM_OK;
 }
 
@@ -387,6 +419,13 @@ static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
     p.hash = h->d_hash;
     p.trace = h->d_trace;
     p.trace_ticks = h->trace_ticks;
+    p.hist = h->d_hist;
+    if (h->window) {
+        p.window_mask = h->window - 1;
+        p.rows = h->window;
+        p.hcap = h->cfg.heights + 64;               // height limit; rows live in the ring
+        p.need_seed = 1;                            // hashes in-kernel: no post-pass over a ring
+    }
     return p;
 }
 
@@ -418,6 +457,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     }
 #endif
     HIPCHECK(h, hipMemsetAsync(h->d_rec, 0, n * h->hcap * 16, s));
+    HIPCHECK(h, hipMemsetAsync(h->d_hist, 0, bft::HIST_BINS * sizeof(uint64_t), s));
     uint32_t per_block = h->seg > 64 ? 1u : 64u / h->seg;      // instances per workgroup
     uint32_t grid = (uint32_t)((n + per_block - 1) / per_block);
     size_t lds = bft::lds_bytes(h->seg, p.need_seed != 0);
@@ -459,6 +499,7 @@ int bftsim_last_kernel_ms(bftsim_t* h, float* cms, float* hms) {
 
 int bftsim_fetch(bftsim_t* h, bftsim_result* out) {
     if (!h || !out) return BFTSIM_EINVAL;
+    if (h->window) return fail(h, BFTSIM_EINVAL, "windowed run: per-height rows are not kept (bftsim_fetch_summary)");
     HIPCHECK(h, hipSetDevice(h->device));
     HIPCHECK(h, hipStreamSynchronize(h->last_stream));
     uint64_t n = h->last_n;
@@ -503,23 +544,46 @@ int bftsim_run(bftsim_t* h, uint64_t first, uint64_t n, bftsim_result* out) {
     return bftsim_fetch(h, out);
 }
 
+int bftsim_fetch_summary(bftsim_t* h, uint32_t* committed_height, uint32_t* flags, uint32_t* ticks,
+                         uint64_t* views, uint8_t* tip_hash) {
+    if (!h || h->last_n == 0) return BFTSIM_EINVAL;
+    HIPCHECK(h, hipSetDevice(h->device));
+    uint64_t n = h->last_n;
+    if (tip_hash) {
+        bft::Params p = make_params(h, h->last_first, n);
+        hipLaunchKernelGGL(bft::bft_tip_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, h->last_stream, p,
+                           h->d_tips);
+        HIPCHECK(h, hipGetLastError());
+    }
+    HIPCHECK(h, hipStreamSynchronize(h->last_stream));
+    if (committed_height) HIPCHECK(h, hipMemcpy(committed_height, h->d_ch, n * 4, hipMemcpyDeviceToHost));
+    if (flags) HIPCHECK(h, hipMemcpy(flags, h->d_flags, n * 4, hipMemcpyDeviceToHost));
+    if (ticks) HIPCHECK(h, hipMemcpy(ticks, h->d_ticks, n * 4, hipMemcpyDeviceToHost));
+    if (views) HIPCHECK(h, hipMemcpy(views, h->d_views, n * 8, hipMemcpyDeviceToHost));
+    if (tip_hash) HIPCHECK(h, hipMemcpy(tip_hash, h->d_tips, n * 32, hipMemcpyDeviceToHost));
+    return BFTSIM_OK;
+}
+
 int bftsim_stats_get(bftsim_t* h, bftsim_stats* out) {
     if (!h || !out || h->last_n == 0) return BFTSIM_EINVAL;
     HIPCHECK(h, hipSetDevice(h->device));
     bft::Params p = make_params(h, h->last_first, h->last_n);
-    HIPCHECK(h, hipMemsetAsync(h->d_stats, 0, 80 * 8, h->last_stream));
+    HIPCHECK(h, hipMemsetAsync(h->d_stats, 0, 16 * 8, h->last_stream));
     uint32_t g = (uint32_t)((h->last_n + 255) / 256);
     hipLaunchKernelGGL(bft::bft_stats_kernel, dim3(g), dim3(256), 0, h->last_stream, p, h->d_stats);
     HIPCHECK(h, hipGetLastError());
-    unsigned long long st[80];
+    unsigned long long st[16];
+    uint64_t hist[bft::HIST_BINS];
     HIPCHECK(h, hipMemcpyAsync(st, h->d_stats, sizeof st, hipMemcpyDeviceToHost, h->last_stream));
+    HIPCHECK(h, hipMemcpyAsync(hist, h->d_hist, sizeof hist, hipMemcpyDeviceToHost, h->last_stream));
     HIPCHECK(h, hipStreamSynchronize(h->last_stream));
     out->instances = st[0];
     out->committed_heights = st[1];
     out->views = st[2];
     out->ticks = st[3];
-    for (int i = 0; i < 6; ++i) out->flagged[i] = st[4 + i];
-    for (int i = 0; i < 65; ++i) out->round_hist[i] = st[10 + i];
+    for (int i = 0; i < 7; ++i) out->flagged[i] = st[4 + i];
+    for (int i = 0; i < 65; ++i) out->round_hist[i] = hist[i];
+    for (int i = 0; i < 65; ++i) out->latency_hist[i] = hist[65 + i];
     return BFTSIM_OK;
 }
 

@@ -41,6 +41,7 @@ extern "C" {
 #define BFTSIM_FLAG_OUTBOX 8u        /* a second message of one kind in one phase was dropped */
 #define BFTSIM_FLAG_TIMEOUT 16u      /* max_ticks reached before `heights` */
 #define BFTSIM_FLAG_RCS_OVERFLOW 32u /* more round-change rounds than the GPU table holds */
+#define BFTSIM_FLAG_WINDOW 64u       /* windowed run: a lookup older than the row ring (result unpinned) */
 
 typedef struct bftsim_config {
     uint32_t n;                  /* validators per instance: 1..64 */
@@ -76,8 +77,10 @@ typedef struct bftsim_stats {    /* summed over the instances of the last launch
     uint64_t committed_heights;
     uint64_t views;              /* instance-rounds */
     uint64_t ticks;
-    uint64_t flagged[6];         /* instances with each flag bit set */
-    uint64_t round_hist[65];     /* heights committed in round 0..63, [64] = 64+ */
+    uint64_t flagged[7];         /* instances with each flag bit set */
+    uint64_t round_hist[65];     /* rounds-to-commit: heights committed in round 0..63, [64] = 64+ */
+    uint64_t latency_hist[65];   /* commit latency: ticks between the records of heights x-1 and x
+                                    (genesis = tick 0), [64] = 64+ */
 } bftsim_stats;
 
 typedef struct bftsim bftsim_t;
@@ -100,6 +103,16 @@ int bftsim_stats_get(bftsim_t *h, bftsim_stats *out);   /* device reduction + co
 int bftsim_last_kernel_ms(bftsim_t *h, float *consensus_ms, float *hash_ms);
 /* optional per-tick state digests of the next launch (debug; NULL disables) */
 int bftsim_set_trace(bftsim_t *h, uint64_t *host_out, uint32_t trace_ticks);
+/* windowed runs for long horizons (10,000 heights x 1M instances): keep only a ring
+ * of `window` canonical rows per instance (power of two >= 64; 0 = every height, the default).
+ * Block hashes are then computed in-kernel; per-height outputs are not kept (bftsim_fetch fails):
+ * read bftsim_fetch_summary and the histograms of bftsim_stats_get. A lookup older than the ring
+ * (a validator lagging > window heights) sets BFTSIM_FLAG_WINDOW. */
+int bftsim_set_window(bftsim_t *h, uint32_t window);
+/* per-instance outputs of the last launch (any pointer may be NULL); tip_hash[i*32..] = hash of
+ * the block at committed_height[i] (the genesis hash at 0), which commits to the whole chain */
+int bftsim_fetch_summary(bftsim_t *h, uint32_t *committed_height, uint32_t *flags, uint32_t *ticks,
+                         uint64_t *views, uint8_t *tip_hash);
 
 /* ValidatorSet / block helpers on the host (validator.rs, types/block.rs) */
 uint32_t bftsim_two_thirds_majority(uint32_t n);                    /* validator.rs:149-154 */

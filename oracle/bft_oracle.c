@@ -362,6 +362,7 @@ typedef struct {
     int64_t T;           /* time tick */
     uint8_t hash[32];
     uint32_t seed;
+    int64_t commit_tick; /* tick of the phase that recorded it (commit-latency histogram) */
 } canon_entry;
 
 typedef struct {
@@ -773,6 +774,7 @@ static void canon_record(world *w, uint32_t x, blk b, uint32_t round) {
     c->b = b;
     c->round = round;
     c->T = b.T;
+    c->commit_tick = w->tick;
     set_hash(w, x);    /* the next height's proposer seed needs it at once */
     if (x > w->canon_h) w->canon_h = x;
 }
@@ -899,8 +901,20 @@ static void set_hash(world *w, uint32_t x) {
     c->seed = orc_seed_from_hash(c->hash, w->n);
 }
 
+/* per-instance summary of a streamed run (orc_run_stream) */
+static void stream_summary(const orc_config *cfg, world *w, uint32_t done_tick, orc_stream *st, uint64_t idx,
+                           uint64_t hist[ORC_HIST_BINS]);
+
+static int run_instance_ex(const orc_config *cfg, uint32_t inst, const orc_result *res, uint64_t idx,
+                           uint64_t *trace, uint32_t max_rec, orc_stream *st, uint64_t *hist);
+
 static int run_instance(const orc_config *cfg, uint32_t inst, const orc_result *res, uint64_t idx,
                         uint64_t *trace, uint32_t max_rec) {
+    return run_instance_ex(cfg, inst, res, idx, trace, max_rec, NULL, NULL);
+}
+
+static int run_instance_ex(const orc_config *cfg, uint32_t inst, const orc_result *res, uint64_t idx,
+                           uint64_t *trace, uint32_t max_rec, orc_stream *st, uint64_t *hist) {
     runner *R = (runner *)calloc(1, sizeof(runner));
     world *w = &R->w;
     uint32_t n = cfg->n;
@@ -914,7 +928,7 @@ static int run_instance(const orc_config *cfg, uint32_t inst, const orc_result *
     w->canon = (canon_entry *)calloc(w->canon_cap + 1, sizeof(canon_entry));
     /* genesis (core/genesis.rs:24-59) */
     canon_entry *g = canon_at(w, 0);
-    g->set = 1; g->b.h = 0; g->b.valid = 1; g->T = -1; g->round = 0;
+    g->set = 1; g->b.h = 0; g->b.valid = 1; g->T = -1; g->round = 0; g->commit_tick = 0;
     orc_genesis_hash(cfg, g->hash);
     g->seed = orc_seed_from_hash(g->hash, n);
     uint64_t byz[4];
@@ -973,6 +987,7 @@ static int run_instance(const orc_config *cfg, uint32_t inst, const orc_result *
         }
         res->views[idx] = views;
     }
+    if (st) stream_summary(cfg, w, done_tick, st, idx, hist);
     free(w->v);
     free(w->canon);
     free(R);
@@ -1078,4 +1093,73 @@ uint64_t orc_verify_chains(const orc_config *cfg, uint64_t first, uint64_t n, co
     for (int i = 0; i < threads; ++i) pthread_join(th[i], NULL);
     free(th);
     return bad;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Streamed runs: per-instance totals, the tip hash (it commits to the whole chain) and the     */
+/* rounds-to-commit / commit-latency histograms of SURVEY.md §8d cfg5, without per-height rows. */
+/* ------------------------------------------------------------------------------------------ */
+static void stream_summary(const orc_config *cfg, world *w, uint32_t done_tick, orc_stream *st, uint64_t idx,
+                           uint64_t hist[ORC_HIST_BINS]) {
+    uint32_t H = cfg->heights;
+    uint32_t ch = w->canon_h < H ? w->canon_h : H;
+    uint32_t flags = w->flags;
+    if (!w->frozen && w->canon_h < H) flags |= ORC_FLAG_TIMEOUT;
+    uint64_t views = 0;
+    for (uint32_t x = 1; x <= ch; ++x) {
+        canon_entry *c = canon_at(w, x);
+        views += (uint64_t)c->round + 1;
+        hist[c->round < 64 ? c->round : 64] += 1;
+        int64_t lat = c->commit_tick - canon_at(w, x - 1)->commit_tick;
+        hist[65 + (lat < 64 ? lat : 64)] += 1;
+    }
+    st->committed_height[idx] = ch;
+    st->flags[idx] = flags;
+    st->ticks[idx] = done_tick;
+    st->views[idx] = views;
+    memcpy(st->tip_hash + idx * 32, canon_at(w, ch)->hash, 32);
+}
+
+typedef struct {
+    const orc_config *cfg;
+    uint64_t first, n;
+    orc_stream *st;
+    uint64_t *next;
+    pthread_mutex_t *mu;
+    uint64_t hist[ORC_HIST_BINS];
+} sjob;
+
+static void *stream_worker(void *arg) {
+    sjob *j = (sjob *)arg;
+    for (;;) {
+        pthread_mutex_lock(j->mu);
+        uint64_t i = *j->next;
+        *j->next += 1;
+        pthread_mutex_unlock(j->mu);
+        if (i >= j->n) break;
+        run_instance_ex(j->cfg, (uint32_t)(j->first + i), NULL, i, NULL, 0, j->st, j->hist);
+    }
+    return NULL;
+}
+
+int orc_run_stream(const orc_config *cfg, uint64_t first_instance, uint64_t n_instances, orc_stream *st,
+                   int threads) {
+    if (threads < 1) threads = 1;
+    memset(st->hist, 0, sizeof st->hist);
+    pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    sjob *jobs = (sjob *)calloc((size_t)threads, sizeof(sjob));
+    pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+    uint64_t next = 0;
+    for (int t = 0; t < threads; ++t) {
+        jobs[t].cfg = cfg; jobs[t].first = first_instance; jobs[t].n = n_instances;
+        jobs[t].st = st; jobs[t].next = &next; jobs[t].mu = &mu;
+        pthread_create(&th[t], NULL, stream_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; ++t) {
+        pthread_join(th[t], NULL);
+        for (int b = 0; b < ORC_HIST_BINS; ++b) st->hist[b] += jobs[t].hist[b];
+    }
+    free(jobs);
+    free(th);
+    return 0;
 }

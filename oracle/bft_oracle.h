@@ -85,6 +85,22 @@ int orc_run_threads(const orc_config *cfg, uint64_t first_instance, uint64_t n_i
 uint64_t orc_verify_chains(const orc_config *cfg, uint64_t first, uint64_t n, const orc_result *res,
                            int threads);
 
+/* streamed run (no per-height rows): per-instance totals, the hash of the block at
+ * committed_height (genesis hash if 0), and summed histograms: hist[0..64] rounds-to-commit of each
+ * committed height (64 = overflow), hist[65..129] commit latency in ticks (tick of the phase that
+ * recorded height x minus that of x-1; genesis = tick 0; 64 = overflow). */
+#define ORC_HIST_BINS 130
+typedef struct orc_stream {
+    uint32_t *committed_height;  /* [n] */
+    uint32_t *flags;             /* [n] */
+    uint32_t *ticks;             /* [n] */
+    uint64_t *views;             /* [n] */
+    uint8_t *tip_hash;           /* [n * 32] */
+    uint64_t hist[ORC_HIST_BINS];
+} orc_stream;
+int orc_run_stream(const orc_config *cfg, uint64_t first_instance, uint64_t n_instances, orc_stream *st,
+                   int threads);
+
 /* per-tick state digest of one instance (debug/parity localisation):
  * for each tick t < max_rec, out[t*n + v] = packed state of validator v at the end of tick t */
 int orc_trace(const orc_config *cfg, uint64_t instance, uint64_t *out, uint32_t max_rec);

@@ -77,6 +77,8 @@ struct EmuWave {
     }
     static uint32_t gload(const uint32_t* p) { return *p; }
     static void gstore(uint32_t* p, uint32_t v) { *p = v; }
+    static void lds_add(uint32_t* p, uint32_t v) { *p += v; }
+    static void gadd64(uint64_t* p, uint64_t v) { *p += v; }
 };
 
 // the workgroup flavour (S = 64*NW lanes): same collectives as GroupHip in bftsim.hip
@@ -98,6 +100,8 @@ struct EmuGroup {
     static uint64_t clock() { return 0; }
     static uint32_t gload(const uint32_t* p) { return *p; }
     static void gstore(uint32_t* p, uint32_t v) { *p = v; }
+    static void lds_add(uint32_t* p, uint32_t v) { *p += v; }
+    static void gadd64(uint64_t* p, uint64_t v) { *p += v; }
 };
 
 template <bool NS, uint32_t S>
@@ -209,8 +213,48 @@ int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds, int
 
 }  // namespace
 
+// windowed run (bftsim_set_window): per-instance outputs, tip hashes and the histograms
+extern "C" int emu_run_stream(const bftsim_config* cfg, uint64_t first, uint64_t n, uint32_t window,
+                              uint32_t* committed, uint32_t* flags_out, uint32_t* ticks_out, uint64_t* views_out,
+                              uint8_t* tips, uint64_t* hist) {
+    if (cfg->n < 1 || cfg->n > 256 || window < 64 || (window & (window - 1))) return -4;
+    uint8_t gh[32];
+    bft::host_genesis_hash(cfg, gh);
+    uint32_t gseed = bft::seed_from_hash(gh, cfg->n);
+    uint32_t seg = bft::segment_size(cfg->n);
+    bft::Params P = bft::params_from_config(*cfg, seg, cfg->heights + 64, gseed, first, n);
+    P.window_mask = window - 1;
+    P.rows = window;
+    P.need_seed = 1;
+    std::vector<uint32_t> rec((size_t)n * window * 4, 0);
+    std::vector<uint8_t> hs((size_t)n * window * 32, 0);
+    for (int b = 0; b < (int)bft::HIST_BINS; ++b) hist[b] = 0;
+    P.addresses = cfg->addresses;
+    P.genesis_hash = gh;
+    P.committed_height = committed;
+    P.flags = flags_out;
+    P.ticks = ticks_out;
+    P.views = views_out;
+    P.rec = rec.data();
+    P.hash = hs.data();
+    P.hist = hist;
+    uint32_t per_wave = seg > 64 ? 1 : 64 / seg;
+    uint32_t waves = (uint32_t)((n + per_wave - 1) / per_wave);
+    std::vector<uint8_t> lds(bft::lds_bytes(seg, true));
+    for (uint32_t w = 0; w < waves; ++w) {
+        memset(lds.data(), 0xcd, lds.size());
+        if (run_wave(P, w, lds, 0, seg > 64 ? (int)seg : 64)) return -1;
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+        uint32_t ch = committed[i];
+        const uint8_t* src = ch == 0 ? gh : &hs[(i * window + (ch & (window - 1))) * 32];
+        memcpy(tips + i * 32, src, 32);
+    }
+    return 0;
+}
+
 extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bftsim_result* out,
-                       uint64_t* trace, uint32_t trace_ticks) {
+                       uint64_t* trace, uint32_t trace_ticks, uint64_t* hist) {
     if (cfg->n < 1 || cfg->n > 256) return -4;
     uint8_t gh[32];
     bft::host_genesis_hash(cfg, gh);
@@ -233,6 +277,8 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
     P.hash = hs.data();
     P.trace = trace;
     P.trace_ticks = trace ? trace_ticks : 0;
+    P.hist = hist;
+    if (hist) for (int b = 0; b < (int)bft::HIST_BINS; ++b) hist[b] = 0;
     uint32_t per_wave = seg > 64 ? 1 : 64 / seg;
     uint32_t waves = (uint32_t)((n + per_wave - 1) / per_wave);
     std::vector<uint8_t> lds(bft::lds_bytes(seg, P.need_seed != 0));

@@ -33,7 +33,10 @@ def lib():
         build()
         _lib = ctypes.CDLL(LIB)
         _lib.emu_run.argtypes = [ctypes.POINTER(_abi.CConfig), ctypes.c_uint64, ctypes.c_uint64,
-                                 ctypes.POINTER(_abi.CResult), ctypes.c_void_p, ctypes.c_uint32]
+                                 ctypes.POINTER(_abi.CResult), ctypes.c_void_p, ctypes.c_uint32,
+                                 ctypes.c_void_p]
+        _lib.emu_run_stream.argtypes = [ctypes.POINTER(_abi.CConfig), ctypes.c_uint64, ctypes.c_uint64,
+                                        ctypes.c_uint32] + [ctypes.c_void_p] * 6
     return _lib
 
 
@@ -43,12 +46,32 @@ def run(cfg, first, n_inst, trace_ticks=0):
     tr = None
     if trace_ticks:
         tr = np.zeros(n_inst * trace_ticks * cfg.n, np.uint64)
+    hist = np.zeros(130, np.uint64)
     rc = lib().emu_run(ctypes.byref(c), first, n_inst, ctypes.byref(r),
-                       tr.ctypes.data if tr is not None else None, trace_ticks)
+                       tr.ctypes.data if tr is not None else None, trace_ticks, hist.ctypes.data)
     del keep
     if rc != 0:
         raise RuntimeError(f"emu_run failed: {rc}")
     arrs = _abi.shape_result(arrs, n_inst, cfg.heights)
     if tr is not None:
         arrs["trace"] = tr.reshape(n_inst, trace_ticks, cfg.n)
+    arrs["round_hist"], arrs["latency_hist"] = hist[:65], hist[65:]
     return arrs
+
+
+def run_stream(cfg, first, n_inst, window=128):
+    """The windowed kernel body (ring of `window` rows, in-kernel hashes): per-instance outputs,
+    tip hashes and the two histograms."""
+    c, keep = _abi.to_cconfig(cfg)
+    out = dict(committed_height=np.zeros(n_inst, np.uint32), flags=np.zeros(n_inst, np.uint32),
+               ticks=np.zeros(n_inst, np.uint32), views=np.zeros(n_inst, np.uint64),
+               tip_hash=np.zeros((n_inst, 32), np.uint8))
+    hist = np.zeros(130, np.uint64)
+    rc = lib().emu_run_stream(ctypes.byref(c), first, n_inst, window, out["committed_height"].ctypes.data,
+                              out["flags"].ctypes.data, out["ticks"].ctypes.data, out["views"].ctypes.data,
+                              out["tip_hash"].ctypes.data, hist.ctypes.data)
+    del keep
+    if rc != 0:
+        raise RuntimeError(f"emu_run_stream failed: {rc}")
+    out["round_hist"], out["latency_hist"] = hist[:65], hist[65:]
+    return out

@@ -128,6 +128,33 @@ def verify_chains(cfg: BftConfig, first: int, res: dict, threads: int = 8) -> in
     return int(bad)
 
 
+class OrcStream(ctypes.Structure):
+    _fields_ = [("committed_height", ctypes.c_void_p), ("flags", ctypes.c_void_p),
+                ("ticks", ctypes.c_void_p), ("views", ctypes.c_void_p), ("tip_hash", ctypes.c_void_p),
+                ("hist", ctypes.c_uint64 * 130)]
+
+
+def run_stream(cfg: BftConfig, first: int, n_inst: int, threads: int = 8):
+    """Streamed run: per-instance totals, tip hashes and the summed rounds-to-commit (hist[:65])
+    and commit-latency (hist[65:]) histograms."""
+    c, keep = to_orc(cfg)
+    arrs = dict(committed_height=np.zeros(n_inst, np.uint32), flags=np.zeros(n_inst, np.uint32),
+                ticks=np.zeros(n_inst, np.uint32), views=np.zeros(n_inst, np.uint64),
+                tip_hash=np.zeros((n_inst, 32), np.uint8))
+    st = OrcStream()
+    for k, a in arrs.items():
+        setattr(st, k, a.ctypes.data)
+    L = lib()
+    L.orc_run_stream.argtypes = [ctypes.POINTER(OrcConfig), ctypes.c_uint64, ctypes.c_uint64,
+                                 ctypes.POINTER(OrcStream), ctypes.c_int]
+    L.orc_run_stream(ctypes.byref(c), first, n_inst, ctypes.byref(st), threads)
+    del keep
+    h = np.array(st.hist[:], dtype=np.uint64)
+    arrs["round_hist"] = h[:65]
+    arrs["latency_hist"] = h[65:]
+    return arrs
+
+
 def trace(cfg: BftConfig, instance: int, max_rec: int = 512):
     c, keep = to_orc(cfg)
     out = np.zeros(max_rec * cfg.n, np.uint64)

@@ -28,7 +28,7 @@ def test_struct_layouts_match_header():
     # offsets the C side relies on (x86-64 SysV)
     assert ctypes.sizeof(_abi.CConfig) == 4 * 4 + 8 * 2 + 4 * 4 + 8 * 4 + 8 + 20 + 4 + 8
     assert ctypes.sizeof(_abi.CResult) == 9 * 8
-    assert ctypes.sizeof(_abi.CStats) == 8 * (4 + 6 + 65)
+    assert ctypes.sizeof(_abi.CStats) == 8 * (4 + 7 + 65 + 65)
 
 
 def test_create_rejects_bad_configs_without_gpu():

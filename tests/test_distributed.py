@@ -30,7 +30,7 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     first, n = weak_shard(rank, 8)
-    st = stats_from_result(O.run(cfg2(heights=15), first, n))
+    st = stats_from_result(O.run_stream(cfg2(heights=15), first, n, threads=2))
     tot = all_reduce_stats(st)
     if rank == 0:
         q.put(tot)
@@ -59,5 +59,8 @@ def test_gloo_world2_stats_equal_single_process():
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    single = stats_from_result(O.run(cfg2(heights=15), 0, 16))
+    single = stats_from_result(O.run_stream(cfg2(heights=15), 0, 16, threads=2))
     assert tot == single
+    assert sum(tot["latency_hist"]) == tot["committed_heights"] == sum(tot["round_hist"])
+    # the per-height rows give the same rounds-to-commit histogram
+    assert stats_from_result(O.run(cfg2(heights=15), 0, 16))["round_hist"] == single["round_hist"]

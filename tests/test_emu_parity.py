@@ -48,3 +48,27 @@ def test_fast_paths_off_is_identical(monkeypatch):
     slow = E.run(cfg, 0, 8)
     assert_same(fast, slow, "fast vs one-message-at-a-time")
     assert_same(O.run(cfg, 0, 8), slow, "oracle vs slow")
+
+
+STREAM_CASES = [
+    ("cfg5-300", lambda: cfg5(heights=300), 0, 16, 64),
+    ("cfg2-60", lambda: cfg2(heights=60), 100, 32, 64),
+    ("cfg3-12", lambda: cfg3(heights=12), 7, 2, 64),
+    ("cfg4-n100", lambda: cfg4(100, heights=8), 0, 1, 64),
+    ("n7-crash-drop-w128", lambda: BftConfig(n=7, heights=200, seed=41, drop_ppm=150_000,
+                                             proposer_crash_ppm=300_000), 0, 8, 128),
+]
+
+
+@pytest.mark.parametrize("name,mk,first,n,window", STREAM_CASES, ids=[c[0] for c in STREAM_CASES])
+def test_emulated_windowed_run_matches_streamed_oracle(name, mk, first, n, window):
+    import numpy as np
+    cfg = mk()
+    ref = O.run_stream(cfg, first, n, threads=4)
+    got = E.run_stream(cfg, first, n, window=window)
+    for k in ("committed_height", "flags", "ticks", "views", "tip_hash", "round_hist", "latency_hist"):
+        assert np.array_equal(ref[k], got[k]), (name, k)
+    # the full-row kernel accumulates the same histograms in-kernel
+    full = E.run(cfg, first, n)
+    assert np.array_equal(full["round_hist"], ref["round_hist"])
+    assert np.array_equal(full["latency_hist"], ref["latency_hist"])
