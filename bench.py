@@ -8,6 +8,11 @@ kernel, inputs resident on the GPU, results left in HBM. Ranks shard instances (
 [r*I, (r+1)*I)), no data-path collective; the per-run statistics are all-reduced over RCCL.
 
 Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the roofline model.
+
+`--workload cfg5` measures SURVEY §8d cfg5 instead (not the headline): N=7, 5 % drops, 10,000 heights,
+131,072 instances per GPU (1,048,576 on 8 GPUs), windowed rows (bftsim_set_window) with in-kernel
+hashes; the rounds-to-commit and commit-latency histograms are all-reduced over RCCL and printed.
+One step takes ~11 s on one MI355X: run it with --steps 1 --warmup 0.
 """
 from __future__ import annotations
 
@@ -22,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "consensus-rs_amd"))
 
 METRIC = "BFT instance-rounds/sec (whole node), N=64 f=21, 1/2/4/8 GPUs; bit-exact"
+METRIC_CFG5 = "cfg5 instance-rounds/sec (whole node), N=7, 5% drop, 10,000 heights; windowed, bit-exact"
 VALU_PEAK = 256 * 4 * 32 * 2.4e9        # lane-ops/s (MI355X_MICROARCH.md chip table)
 HBM_PEAK = 8.0e12                       # B/s spec
 
@@ -35,16 +41,21 @@ def consensus_ops_per_view(n: int) -> int:
 HEADER_HASH_OPS = 14_976                # 2 Keccak-f[1600] x 24 rounds x 156 64-bit ops x 2
 
 
-def cpu_baseline(cfg, sample: int, threads: int):
+def cpu_baseline(cfg, sample: int, threads: int, name: str = "cfg3"):
     """The C oracle (oracle/, a scalar restatement of the reference handlers) timed on this
     host's cores over a bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    r = O.run(cfg, 0, sample, threads=threads)
+    if name == "cfg5":
+        t = time.perf_counter()
+        r = O.run_stream(cfg, 0, sample, threads=threads)
+        secs = time.perf_counter() - t
+    else:
+        r = O.run(cfg, 0, sample, threads=threads)
+        secs = r["seconds"]
     views = int(r["views"].sum())
-    secs = r["seconds"]
     return dict(value=views / secs, unit="instance-rounds/s", cores=threads, kind="port",
-                sample=f"{sample} cfg3 instances ({views} instance-rounds) on {threads} threads, "
+                sample=f"{sample} {name} instances ({views} instance-rounds) on {threads} threads, "
                        f"{secs:.1f} s")
 
 
@@ -53,16 +64,26 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--instances", type=int, default=16_384, help="instances per GPU")
-    ap.add_argument("--heights", type=int, default=100)
-    ap.add_argument("--cpu-sample", type=int, default=768)
+    ap.add_argument("--workload", choices=("cfg3", "cfg5"), default="cfg3")
+    ap.add_argument("--instances", type=int, default=None, help="instances per GPU")
+    ap.add_argument("--heights", type=int, default=None)
+    ap.add_argument("--window", type=int, default=256, help="cfg5: canonical rows kept per instance")
+    ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
-    from bftsim.configs import cfg3
+    from bftsim.configs import cfg3, cfg5
+    from bftsim.distributed import all_reduce_stats
     from bftsim.runtime import Simulator
+    c5 = args.workload == "cfg5"
+    if args.instances is None:
+        args.instances = 131_072 if c5 else 16_384
+    if args.heights is None:
+        args.heights = 10_000 if c5 else 100
+    if args.cpu_sample is None:
+        args.cpu_sample = 512 if c5 else 768
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -73,9 +94,11 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    cfg = cfg3(heights=args.heights)
+    cfg = cfg5(heights=args.heights) if c5 else cfg3(heights=args.heights)
     sim = Simulator(cfg, device=local)
     I = args.instances
+    if c5:
+        sim.set_window(args.window)
     sim.prepare(I)
     first = rank * I
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -85,12 +108,13 @@ def main():
     torch.cuda.synchronize(dev)
 
     # work per step: instance-rounds of this shard (identical every step), summed over ranks
+    if args.warmup == 0:                  # the work of a step is read from one run's statistics
+        sim.launch(first, stream)
+        torch.cuda.synchronize(dev)
     st = sim.stats()
-    totals = torch.tensor([st["views"], st["committed_heights"], st["instances"],
-                           st["flagged"][0], st["flagged"][4]], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(totals)           # RCCL over xGMI
-    views_all, heights_all, inst_all, safety_all, timeout_all = [int(x) for x in totals.tolist()]
+    tot = all_reduce_stats(st, device=dev)   # one int64 all-reduce (RCCL over xGMI)
+    views_all, heights_all = tot["views"], tot["committed_heights"]
+    safety_all, timeout_all = tot["flagged"][0], tot["flagged"][4]
 
     if world > 1:
         dist.barrier()
@@ -121,14 +145,21 @@ def main():
         # dominant kernel by device time
         c_ops = consensus_ops_per_view(cfg.n) * views_rank
         h_ops = HEADER_HASH_OPS * st["committed_heights"]
+        if c5:                            # windowed runs hash inside the consensus kernel
+            c_ops, h_ops = c_ops + h_ops, 0
         if cms >= hms:
             dom, ops, ms = "bft_consensus_kernel", c_ops, cms
         else:
             dom, ops, ms = "bft_hash_kernel", h_ops, hms
         achieved = ops / (ms / 1e3) / 1e12
         peak = VALU_PEAK / 1e12
+        def trim(h):
+            h = list(h)
+            while h and h[-1] == 0:
+                h.pop()
+            return h
         out = {
-            "metric": METRIC,
+            "metric": METRIC_CFG5 if c5 else METRIC,
             "value": value,
             "unit": "instance-rounds/s",
             "n_gpus": world,
@@ -141,13 +172,17 @@ def main():
             "dtype": "u64",
             "data": "synthetic (seeded Philox schedule, SPEC.md)",
             "config": {
-                "workload": f"cfg3: {I} instances per GPU, N=64, f=21 equivocating, "
-                            f"{args.heights} heights",
+                "workload": (f"cfg5: {I} instances per GPU, N=7, 5% drop, {args.heights} heights, "
+                             f"window {args.window}") if c5 else
+                            (f"cfg3: {I} instances per GPU, N=64, f=21 equivocating, "
+                             f"{args.heights} heights"),
                 "instances_per_gpu": I, "n_validators": cfg.n, "byzantine": cfg.byz_count,
                 "heights": args.heights, "parallelism": f"instance-sharded x{world}",
                 "instance_rounds_per_step": views_all,
                 "committed_heights_per_step": heights_all,
                 "safety_violations": safety_all, "timeouts": timeout_all,
+                "rounds_to_commit_hist": trim(tot["round_hist"]),
+                "commit_latency_ticks_hist": trim(tot["latency_hist"]),
             },
             "roofline": {
                 "bound": "valu", "kernel": dom, "achieved": achieved, "peak": peak,
@@ -160,7 +195,7 @@ def main():
         if not args.no_cpu:
             try:
                 threads = min(16, os.cpu_count() or 1)
-                out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample, threads)
+                out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample, threads, args.workload)
             except Exception as e:  # the baseline is reported, never the target
                 out["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(out), flush=True)

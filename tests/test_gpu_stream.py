@@ -69,7 +69,13 @@ def test_cfg5_full_horizon_sampled():
     assert (got["committed_height"] == cfg.heights).all()
     assert (got["flags"] == 0).all()
     assert int(got["round_hist"].sum()) == n * cfg.heights == int(got["latency_hist"].sum())
-    assert int(got["views"].sum()) == sum(int(k + 1) * int(c) for k, c in enumerate(got["round_hist"][:64]))
+    # views = sum of (round + 1); bin 64 of the rounds histogram is an overflow bucket (round >= 64)
+    part = sum(int(k + 1) * int(c) for k, c in enumerate(got["round_hist"][:64]))
+    over = int(got["round_hist"][64])
+    if over == 0:
+        assert int(got["views"].sum()) == part
+    else:
+        assert int(got["views"].sum()) >= part + 65 * over
     idx = np.linspace(0, n - 1, 256).astype(np.int64)
     for i in idx[::32]:
         ref = O.run_stream(cfg, int(i), 32, threads=16)
