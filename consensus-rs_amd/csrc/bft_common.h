@@ -402,80 +402,130 @@ BFT_FN void tx_hash_words(uint64_t seed, uint32_t inst, uint32_t h, uint32_t pro
 }
 
 constexpr uint32_t LANE_HASH_BUF = 408;    // 3 rate blocks; the header is at most 274 bytes
+constexpr uint32_t HDR_WORDS = LANE_HASH_BUF / 8;
 
-// one header field byte of a 32-byte hash as a MessagePack uint (0xcc prefix for >= 128)
-BFT_FN uint32_t put_u8(uint8_t* buf, uint32_t k, uint32_t b) {
-    if (b >= 128u) buf[k++] = 0xcc;
-    buf[k++] = (uint8_t)b;
-    return k;
-}
-BFT_FN uint32_t put_uint(uint8_t* buf, uint32_t k, uint64_t v) {
-    if (v < 128) { buf[k++] = (uint8_t)v; return k; }
-    if (v < 256) { buf[k++] = 0xcc; buf[k++] = (uint8_t)v; return k; }
-    if (v < 65536) { buf[k++] = 0xcd; buf[k++] = (uint8_t)(v >> 8); buf[k++] = (uint8_t)v; return k; }
-    if (v < 4294967296ull) {
-        buf[k++] = 0xce;
-        for (int i = 0; i < 4; ++i) buf[k++] = (uint8_t)(v >> (24 - 8 * i));
-        return k;
+// The MessagePack header (SPEC.md §7) is produced as a stream of little-endian 64-bit words, not
+// byte by byte: a field contributes one `put` of up to 8 bytes into a 64-bit accumulator, and every
+// completed word is stored once (LDS on the device). The byte layout is exactly the one of
+// host_header_bytes() (bft_host.h), which the tests compare against the msgpack package.
+struct HdrWriter {
+    uint64_t* wb;        // HDR_WORDS words, 8-aligned
+    uint64_t acc;
+    uint32_t fill;       // bytes in acc, 0..7
+    uint32_t wi;         // next word index
+    BFT_FN explicit HdrWriter(uint64_t* w) : wb(w), acc(0), fill(0), wi(0) {}
+    BFT_FN void put(uint64_t v, uint32_t n) {            // 1 <= n <= 8, v < 2^(8n)
+        const uint32_t sh = 8u * fill;
+        const uint64_t lo = acc | (v << sh);
+        const uint32_t nf = fill + n;
+        if (nf >= 8u) {
+            wb[wi++] = lo;
+            acc = sh ? (v >> (64u - sh)) : 0ull;
+            fill = nf - 8u;
+        } else {
+            acc = lo;
+            fill = nf;
+        }
     }
-    buf[k++] = 0xcf;
-    for (int i = 0; i < 8; ++i) buf[k++] = (uint8_t)(v >> (56 - 8 * i));
-    return k;
+    // four bytes of a 32-byte hash as MessagePack uints (0xcc prefix for bytes >= 128)
+    BFT_FN void put_hash_word(uint32_t w) {
+        uint64_t v = 0;
+        uint32_t n = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t b = (w >> (8 * i)) & 0xffu;
+            const uint32_t big = b >> 7;
+            const uint64_t e = big ? (uint64_t)(0xccu | (b << 8)) : (uint64_t)b;
+            v |= e << (8u * n);
+            n += 1u + big;
+        }
+        put(v, n);
+    }
+    // compact MessagePack uint (rmp's write_uint)
+    BFT_FN void put_uint(uint64_t v) {
+        if (v < 128u) { put(v, 1); return; }
+        if (v < 256u) { put(0xccu | (v << 8), 2); return; }
+        if (v < 65536u) { put(0xcdu | ((v >> 8) << 8) | ((v & 0xffu) << 16), 3); return; }
+        if (v < 4294967296ull) {
+            const uint64_t be = ((v >> 24) & 0xffu) | (((v >> 16) & 0xffu) << 8) | (((v >> 8) & 0xffu) << 16) |
+                                ((v & 0xffu) << 24);
+            put(0xceu | (be << 8), 5);
+            return;
+        }
+        uint64_t be = 0;
+        for (int i = 0; i < 8; ++i) be |= ((v >> (8 * i)) & 0xffu) << (8 * (7 - i));
+        put(0xcfu, 1);
+        put(be, 8);
+    }
+    // "0x" + 40 lowercase hex digits of a 20-byte address, as a 42-byte str8 (d9 2a ...)
+    BFT_FN void put_address(const uint8_t* addr20) {
+        put(0x78302ad9ull, 4);
+        for (int k = 0; k < 5; ++k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+            const uint64_t x = ((const uint32_t*)addr20)[k];    // device table: 20*v is 4-aligned
+#else
+            const uint64_t x = (uint64_t)addr20[4 * k] | ((uint64_t)addr20[4 * k + 1] << 8) |
+                               ((uint64_t)addr20[4 * k + 2] << 16) | ((uint64_t)addr20[4 * k + 3] << 24);
+#endif
+            // bytes b0..b3 into 16-bit slots, then (hi nibble, lo nibble) per slot
+            uint64_t s = (x & 0xffull) | ((x & 0xff00ull) << 8) | ((x & 0xff0000ull) << 16) | ((x & 0xff000000ull) << 24);
+            uint64_t nb = ((s >> 4) & 0x000f000f000f000full) | ((s & 0x000f000f000f000full) << 8);
+            uint64_t alpha = ((nb + 0x0606060606060606ull) >> 4) & 0x0101010101010101ull;
+            put(nb + 0x3030303030303030ull + alpha * 39ull, 8);
+        }
+    }
+    // pad10*1 with the Keccak domain byte 0x01; returns the number of 136-byte blocks
+    BFT_FN uint32_t finish() {
+        const uint32_t k = 8u * wi + fill;
+        const uint32_t nb = k / 136u + 1u;
+        wb[wi++] = acc | (0x01ull << (8u * fill));
+        const uint32_t end = 17u * nb;
+        while (wi < end) wb[wi++] = 0;
+        wb[end - 1u] ^= 0x80ull << 56;
+        return nb;
+    }
+};
+
+// Header of block (x, prop, var) with parent hash `prev` (8 LE words) at `time`, into wb; returns
+// the number of rate blocks (2 or 3). Field order = Header declaration order (types/block.rs:16-36).
+BFT_FN uint32_t header_words(uint64_t* wb, const uint32_t prev[8], const uint8_t* addr20, uint64_t seed,
+                             uint32_t inst, uint32_t h, uint32_t prop, uint32_t var, uint64_t time) {
+    HdrWriter w(wb);
+    w.put(0x2000dc9dull, 4);                           // array(13); prev_hash: array16(32)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w.put_hash_word(prev[i]);
+    w.put_address(addr20);                             // proposer
+    w.put(0x2000dcull, 3);                             // root = EMPTY_HASH
+    for (int i = 0; i < 4; ++i) w.put(0, 8);
+    w.put(0x2000dcull, 3);                             // tx_hash (seeded, SPEC.md §5)
+    uint32_t tx[8];
+    tx_hash_words(seed, inst, h, prop, var, tx);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w.put_hash_word(tx[i]);
+    w.put(0x2000dcull, 3);                             // receipt_hash = EMPTY_HASH
+    for (int i = 0; i < 4; ++i) w.put(0, 8);
+    w.put(0, 2);                                       // bloom, difficulty
+    w.put_uint(h);                                     // height
+    w.put(0, 2);                                       // gas_limit, gas_used
+    w.put_uint(time);
+    w.put(0x2065736e696f439bull, 8);                   // extra = "Coinse base" (minner/mod.rs:113)
+    w.put(0xc065736162ull, 5);                         //   ... + votes: None
+    return w.finish();
 }
 
-// Keccak-256 of a candidate header (SPEC.md §7) by ONE lane: the whole MessagePack encoding is
-// written to `buf` (LANE_HASH_BUF bytes, 8-aligned; LDS on the device), then absorbed block by
-// block from a single call site, so the permutation is instantiated once (compact code).
-// prev/out: the hash as 8 little-endian words.
+// Keccak-256 of a candidate header (SPEC.md §7) by ONE lane. `buf`: LANE_HASH_BUF bytes, 8-aligned
+// (LDS on the device). prev/out: the hash as 8 little-endian words.
 BFT_FN void lane_block_hash(uint8_t* buf, const uint32_t prev[8], const uint8_t* addr20, uint64_t seed,
                             uint32_t inst, uint32_t h, uint32_t prop, uint32_t var, uint64_t time,
                             uint32_t out[8]) {
-    uint32_t k = 0;
-    buf[k++] = 0x9d;                                   // 13 serialized fields
-    buf[k++] = 0xdc; buf[k++] = 0x00; buf[k++] = 0x20; // prev_hash
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) k = put_u8(buf, k, (prev[i] >> (8 * b)) & 0xffu);
-    buf[k++] = 0xd9; buf[k++] = 42; buf[k++] = '0'; buf[k++] = 'x';   // proposer
-#pragma unroll 1
-    for (int i = 0; i < 20; ++i) {
-        uint32_t ab = addr20[i];
-        buf[k++] = (uint8_t)hexdigit(ab >> 4);
-        buf[k++] = (uint8_t)hexdigit(ab & 15u);
-    }
-    buf[k++] = 0xdc; buf[k++] = 0x00; buf[k++] = 0x20; // root
-#pragma unroll 1
-    for (int i = 0; i < 32; ++i) buf[k++] = 0;
-    uint32_t tx[8];
-    tx_hash_words(seed, inst, h, prop, var, tx);
-    buf[k++] = 0xdc; buf[k++] = 0x00; buf[k++] = 0x20; // tx_hash
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) k = put_u8(buf, k, (tx[i] >> (8 * b)) & 0xffu);
-    buf[k++] = 0xdc; buf[k++] = 0x00; buf[k++] = 0x20; // receipt_hash
-#pragma unroll 1
-    for (int i = 0; i < 32; ++i) buf[k++] = 0;
-    buf[k++] = 0; buf[k++] = 0;                        // bloom, difficulty
-    k = put_uint(buf, k, h);
-    buf[k++] = 0; buf[k++] = 0;                        // gas_limit, gas_used
-    k = put_uint(buf, k, time);
-    buf[k++] = 0x9b;                                   // extra = "Coinse base" (minner/mod.rs:113)
-    buf[k++] = 'C'; buf[k++] = 'o'; buf[k++] = 'i'; buf[k++] = 'n'; buf[k++] = 's'; buf[k++] = 'e';
-    buf[k++] = ' '; buf[k++] = 'b'; buf[k++] = 'a'; buf[k++] = 's'; buf[k++] = 'e';
-    buf[k++] = 0xc0;                                   // votes: None
-    const uint32_t nb = k / 136u + 1u;                 // pad10*1 with domain byte 0x01
-#pragma unroll 1
-    for (uint32_t i = k; i < 136u * nb; ++i) buf[i] = 0;
-    buf[k] ^= 0x01;
-    buf[136u * nb - 1u] ^= 0x80;
+    uint64_t* wb = (uint64_t*)buf;
+    const uint32_t nb = header_words(wb, prev, addr20, seed, inst, h, prop, var, time);
     uint64_t a[25];
 #pragma unroll
     for (int i = 0; i < 25; ++i) a[i] = 0;
 #pragma unroll 1
     for (uint32_t blk = 0; blk < nb; ++blk) {
-        const uint64_t* w = (const uint64_t*)(buf + 136u * blk);
+        const uint64_t* w = wb + 17u * blk;
 #pragma unroll
         for (int i = 0; i < 17; ++i) a[i] ^= w[i];
         keccak_f1600(a);

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/gpu_parity.log 2>&1 && \
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_parity.log 2>&1 && \
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?
 tail -3 gpurun_out/gpu_parity.log
