@@ -60,8 +60,10 @@ BFT_FN void outbox_clear(Outbox& o) {
 //   [0, L*REC_WORDS*4)                published outbox records (one per lane)
 //   [.., + K*(1+2*NW)*L*4)            RoundChangeSet, SoA: K round words [k][lane], then the
 //                                     sender bitmaps as 2*NW 32-bit words [k][j][lane]
-//   [.., + L*8*4)                     per-lane commit hand-off {x, blk lo, blk hi, round, seed}
-//                                     (also the Fisher-Yates scratch at init)
+//   (aliases the records)             per-lane commit hand-off {x, blk lo, blk hi, round, seed}
+//                                     (also the Fisher-Yates scratch at init): written only after
+//                                     every receiver has read the phase's records
+//   [.., + 528)                       per-wave histogram bins (HIST_BINS words)
 //   [.., + 512)                       per-segment shared words (8 per segment for S <= 64; 16 words
 //                                     + the group-collective slots at +256 for S > 64)
 //   need_seed only:
@@ -75,8 +77,11 @@ struct Layout {
     static constexpr int K = S > 64 ? 4 : 8;          // RoundChangeSet rounds kept per validator
     static constexpr uint32_t REC_OFF = 0;
     static constexpr uint32_t RC_OFF = REC_OFF + L * REC_WORDS * 4;
-    static constexpr uint32_t CMT_OFF = RC_OFF + (uint32_t)K * (1u + 2u * NW) * L * 4;
-    static constexpr uint32_t SEG_OFF = CMT_OFF + L * 8 * 4;
+    static constexpr uint32_t CMT_OFF = REC_OFF;
+    static constexpr uint32_t HIST_OFF = RC_OFF + (uint32_t)K * (1u + 2u * NW) * L * 4;
+    static constexpr uint32_t SEG_OFF = HIST_OFF + 528;
+    static_assert(L * 8 <= L * REC_WORDS, "commit hand-off must fit in the record area");
+    static_assert(HIST_BINS * 4 <= 528, "histogram area");
     static constexpr uint32_t GRP_OFF = SEG_OFF + 256;
     static constexpr uint32_t CHASH_OFF = SEG_OFF + 512;
     static constexpr uint32_t SCR_OFF = CHASH_OFF + L * 32;
@@ -95,6 +100,7 @@ struct Sim {
     static constexpr int NW = LY::NW;
     static constexpr int RCS_K = LY::K;
     static constexpr uint32_t LDS_REC_OFF = LY::REC_OFF, LDS_RC_OFF = LY::RC_OFF, LDS_CMT_OFF = LY::CMT_OFF,
+                              LDS_HIST_OFF = LY::HIST_OFF,
                               LDS_SEG_OFF = LY::SEG_OFF, LDS_CHASH_OFF = LY::CHASH_OFF, LDS_SCR_OFF = LY::SCR_OFF;
     using M = Bits<NW>;
     const Params& P;
@@ -622,10 +628,8 @@ struct Sim {
         }
     }
 
-    // histogram bins in the unused words 5..7 of the commit hand-off slots (LDS, per wave)
-    BFT_FN uint32_t* hist_slot(uint32_t b) const {
-        return (uint32_t*)(lds + LDS_CMT_OFF) + (b / 3u) * 8u + 5u + (b % 3u);
-    }
+    // histogram bins (LDS, per wave / workgroup)
+    BFT_FN uint32_t* hist_slot(uint32_t b) const { return (uint32_t*)(lds + LDS_HIST_OFF) + b; }
     // record a new canonical height (segment leader; global stores for the outputs). `ctick` is the
     // tick of the previous canonical record; returns the instance-rounds to add (0 beyond H).
     BFT_FN uint32_t record_canon(uint32_t x, uint64_t b, uint32_t round, uint32_t seed, const uint32_t* hs,
@@ -1024,11 +1028,8 @@ struct Sim {
         st_t = wv.clock();
 #endif
         if (P.byz_count > 0) init_byzantine();
-        {   // zero this lane's histogram words (after init_byzantine's scratch use of the area)
-            uint32_t* hw = (uint32_t*)(lds + LDS_CMT_OFF) + lane * 8u;
-            hw[5] = hw[6] = hw[7] = 0;
-            sync();
-        }
+        for (uint32_t b = lane; b < HIST_BINS; b += LY::L) *hist_slot(b) = 0;
+        sync();
         for (tick = 0; tick < (int32_t)P.max_ticks; ++tick) {
             if (ballot(!seg_done).none()) break;
             bool act = running && !seg_done;
@@ -1054,6 +1055,10 @@ struct Sim {
                 summarize(ps);
                 BFT_STAMP(1);
                 const uint32_t path = classify(ps);
+#ifdef BFT_STAMPS
+                st_acc[6] += 1;                               // phases (a count, not cycles)
+                st_acc[11] += path == PATH_GENERAL ? 1 : 0;   // general-path phases
+#endif
                 // records go to LDS only if some segment of the wave takes the general path
                 const bool pub = !BFT_LAZY_PUBLISH || ballot(path == PATH_GENERAL).any();
                 if (pub) { publish(); sync(); }
@@ -1086,10 +1091,9 @@ struct Sim {
         uint32_t lf = seg_or(lane_flags);
         sync();
         if (P.hist) {                                  // this wave's histogram → the launch totals
-            const uint32_t* hw = (const uint32_t*)(lds + LDS_CMT_OFF) + lane * 8u;
-            for (uint32_t k = 0; k < 3; ++k) {
-                uint32_t b = 3u * lane + k;
-                if (b < HIST_BINS && hw[5 + k] != 0) wv.gadd64(P.hist + b, hw[5 + k]);
+            for (uint32_t b = lane; b < HIST_BINS; b += LY::L) {
+                const uint32_t v = *hist_slot(b);
+                if (v != 0) wv.gadd64(P.hist + b, v);
             }
         }
         if (me == 0 && inst_local < P.n_instances) {

@@ -14,8 +14,9 @@ for _ in range(2):
     sim.sync()
 out = (ctypes.c_uint64 * 12)()
 runtime.lib().bftsim_debug_stamps(out)
-names = ["t_step", "summarize", "publish+sync", "deliver?", "resolve", "mask+offset", "-", "loop/other", "fast_blk", "fast_pc", "general", "-"]
-tot = sum(out)
+names = ["t_step", "summarize", "publish+sync", "deliver?", "resolve", "mask+offset", "#phases", "loop/other", "fast_blk", "fast_pc", "general", "#general"]
+tot = sum(out[k] for k in range(12) if k not in (6, 11))
+print("phases per wave-height", out[6] / (16384 * 100.0), "general", out[11] / (16384 * 100.0))
 for k in range(12):
     print(f"{names[k]:14s} {out[k]:16d} {100.0*out[k]/max(tot,1):6.2f}%")
 print("kernel ms", sim.kernel_ms())
