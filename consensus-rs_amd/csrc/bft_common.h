@@ -55,6 +55,7 @@ struct Params {
     uint64_t* hist;                   // [130] summed rounds-to-commit (65) + commit-latency (65) bins
     uint32_t window_mask;             // 0: rec/hash rows for every height; else ring of window_mask+1 rows
     uint32_t rows;                    // rec/hash rows per instance (hcap, or the ring size)
+    uint32_t* rcs;                    // RoundChangeSet tables: per wave / workgroup rcs_words(seg) words
 };
 
 // flags (same bits as the oracle)

@@ -58,12 +58,13 @@ BFT_FN void outbox_clear(Outbox& o) {
 
 // LDS layout of one wave (S <= 64, L = 64 lanes) or one workgroup (S > 64, L = S lanes):
 //   [0, L*REC_WORDS*4)                published outbox records (one per lane)
-//   [.., + K*(1+2*NW)*L*4)            RoundChangeSet, SoA: K round words [k][lane], then the
-//                                     sender bitmaps as 2*NW 32-bit words [k][j][lane]
 //   (aliases the records)             per-lane commit hand-off {x, blk lo, blk hi, round, seed}
 //                                     (also the Fisher-Yates scratch at init): written only after
 //                                     every receiver has read the phase's records
 //   [.., + 528)                       per-wave histogram bins (HIST_BINS words)
+// The RoundChangeSet tables are lane-private and touched only by round changes: they live in global
+// memory (P.rcs, coalesced SoA per wave: K round words [k][lane], then the sender bitmaps as 2*NW
+// 32-bit words [k][j][lane]) so the LDS of a wave stays small enough for 4 waves per SIMD.
 //   [.., + 512)                       per-segment shared words (8 per segment for S <= 64; 16 words
 //                                     + the group-collective slots at +256 for S > 64)
 //   need_seed only:
@@ -78,7 +79,8 @@ struct Layout {
     static constexpr uint32_t REC_OFF = 0;
     static constexpr uint32_t RC_OFF = REC_OFF + L * REC_WORDS * 4;
     static constexpr uint32_t CMT_OFF = REC_OFF;
-    static constexpr uint32_t HIST_OFF = RC_OFF + (uint32_t)K * (1u + 2u * NW) * L * 4;
+    static constexpr uint32_t HIST_OFF = RC_OFF;
+    static constexpr uint32_t RCS_WORDS = (uint32_t)K * (1u + 2u * NW) * L;    // global, per wave
     static constexpr uint32_t SEG_OFF = HIST_OFF + 528;
     static_assert(L * 8 <= L * REC_WORDS, "commit hand-off must fit in the record area");
     static_assert(HIST_BINS * 4 <= 528, "histogram area");
@@ -89,6 +91,9 @@ struct Layout {
     static constexpr uint32_t BYTES_SEED = S > 64 ? SCR_OFF : SCR_OFF + 64 * LANE_HASH_BUF;
     static constexpr uint32_t bytes(bool need_seed) { return need_seed ? BYTES_SEED : BYTES_POW2; }
 };
+BFT_FN uint32_t rcs_words(uint32_t seg) {
+    return seg == 256 ? Layout<256>::RCS_WORDS : seg == 128 ? Layout<128>::RCS_WORDS : Layout<64>::RCS_WORDS;
+}
 BFT_FN uint32_t lds_bytes(uint32_t seg, bool need_seed) {
     return seg == 256 ? Layout<256>::bytes(need_seed) : seg == 128 ? Layout<128>::bytes(need_seed)
                                                                  : Layout<64>::bytes(need_seed);
@@ -141,6 +146,7 @@ struct Sim {
     uint32_t off_inst, off_tick;     // hoisted parts of delivery_offset (SPEC.md §3)
     uint64_t commit_blk;
     uint32_t lane_flags;
+    uint32_t* rcs_base;      // this wave's RoundChangeSet table (global)
 #ifdef BFT_STAMPS
     uint64_t st_acc[12];
     uint64_t st_t;
@@ -186,6 +192,7 @@ struct Sim {
         commit_x = 0; commit_round = 0; commit_seed = 0; commit_blk = 0;
         lane_flags = 0;
         off_inst = offset_inst_part(p.seed, inst);
+        rcs_base = p.rcs + (uint64_t)wave_global * LY::RCS_WORDS;
         off_tick = 0;
     }
 
@@ -391,10 +398,10 @@ struct Sim {
         if (r < round) catchup_round();
         out_round_change(h, round);
     }
-    // RoundChangeSet table in LDS, SoA [k][lane] (conflict-free per-lane access)
-    BFT_FN uint32_t* rc_round_p(uint32_t k) const { return (uint32_t*)(lds + LDS_RC_OFF) + k * LY::L + lane; }
+    // RoundChangeSet table (global, lane-private), SoA [k][lane]: coalesced per wave
+    BFT_FN uint32_t* rc_round_p(uint32_t k) const { return rcs_base + k * LY::L + lane; }
     BFT_FN uint32_t* rc_word_p(uint32_t k, uint32_t j) const {
-        return (uint32_t*)(lds + LDS_RC_OFF) + (RCS_K + k * 2u * NW + j) * LY::L + lane;
+        return rcs_base + (RCS_K + k * 2u * NW + j) * LY::L + lane;
     }
     BFT_FN M rc_set_at(uint32_t k) const {
         M m;

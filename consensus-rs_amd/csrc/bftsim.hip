@@ -360,6 +360,7 @@ struct bftsim {
     unsigned long long* d_stats = nullptr;
     uint64_t* d_hist = nullptr;       // [HIST_BINS] of the last launch
     uint8_t* d_tips = nullptr;        // [cap_inst * 32]
+    uint32_t* d_rcs = nullptr;        // RoundChangeSet tables, rcs_words(seg) per wave / workgroup
     uint32_t window = 0;              // 0: full per-height rows; else ring of `window` rows
     uint64_t* d_trace = nullptr;
     uint64_t* h_trace = nullptr;
@@ -383,6 +384,8 @@ static int fail(bftsim* h, int code, const std::string& msg) {
 static void free_bufs(bftsim* h) {
     (void)hipFree(h->d_ch); (void)hipFree(h->d_flags); (void)hipFree(h->d_ticks); (void)hipFree(h->d_views);
     (void)hipFree(h->d_rec); (void)hipFree(h->d_hash); (void)hipFree(h->d_trace); (void)hipFree(h->d_tips);
+    (void)hipFree(h->d_rcs);
+    h->d_rcs = nullptr;
     h->d_ch = h->d_flags = h->d_ticks = nullptr; h->d_views = nullptr;
     h->d_rec = nullptr; h->d_hash = nullptr; h->d_trace = nullptr; h->d_tips = nullptr;
     h->cap_inst = 0;
@@ -480,6 +483,11 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
     HIPCHECK(h, hipMalloc(&h->d_rec, n * h->hcap * 16));
     HIPCHECK(h, hipMalloc(&h->d_hash, n * h->hcap * 32));
     HIPCHECK(h, hipMalloc(&h->d_tips, n * 32));
+    {
+        uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg;
+        uint64_t blocks = (n + per_block - 1) / per_block;
+        HIPCHECK(h, hipMalloc(&h->d_rcs, blocks * bft::rcs_words(h->seg) * 4));
+    }
     h->cap_inst = n;
     return BFTSIM_OK;
 }
@@ -516,6 +524,7 @@ static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
     p.trace = h->d_trace;
     p.trace_ticks = h->trace_ticks;
     p.hist = h->d_hist;
+    p.rcs = h->d_rcs;
     if (h->window) {
         p.window_mask = h->window - 1;
         p.rows = h->window;

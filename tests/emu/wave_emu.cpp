@@ -241,6 +241,8 @@ extern "C" int emu_run_stream(const bftsim_config* cfg, uint64_t first, uint64_t
     uint32_t per_wave = seg > 64 ? 1 : 64 / seg;
     uint32_t waves = (uint32_t)((n + per_wave - 1) / per_wave);
     std::vector<uint8_t> lds(bft::lds_bytes(seg, true));
+    std::vector<uint32_t> rcs((size_t)waves * bft::rcs_words(seg), 0xcdcdcdcdu);
+    P.rcs = rcs.data();
     for (uint32_t w = 0; w < waves; ++w) {
         memset(lds.data(), 0xcd, lds.size());
         if (run_wave(P, w, lds, 0, seg > 64 ? (int)seg : 64)) return -1;
@@ -282,6 +284,8 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
     uint32_t per_wave = seg > 64 ? 1 : 64 / seg;
     uint32_t waves = (uint32_t)((n + per_wave - 1) / per_wave);
     std::vector<uint8_t> lds(bft::lds_bytes(seg, P.need_seed != 0));
+    std::vector<uint32_t> rcs((size_t)waves * bft::rcs_words(seg), 0xcdcdcdcdu);
+    P.rcs = rcs.data();
     for (uint32_t w = 0; w < waves; ++w) {
         memset(lds.data(), 0xcd, lds.size());
         if (run_wave(P, w, lds, 0, seg > 64 ? (int)seg : 64)) return -1;
