@@ -39,6 +39,9 @@ def lib():
         L.bftsim_stats_get.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.CStats)]
         L.bftsim_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
                                             ctypes.POINTER(ctypes.c_float)]
+        L.bftsim_kernel_ms_sum.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]
+        L.bftsim_set_pipeline.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.bftsim_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
         L.bftsim_set_window.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         L.bftsim_fetch_summary.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5
@@ -136,6 +139,13 @@ class Simulator:
     def launch(self, first: int, stream: int = 0):
         _check(self.h, lib().bftsim_launch(self.h, first, ctypes.c_void_p(stream)), "bftsim_launch")
 
+    def fetch(self):
+        """Per-height results of the last launch (all prepared instances), as run() returns them."""
+        n = self.n_prepared
+        r, arrs = _abi.alloc_result(n, self.cfg.heights)
+        _check(self.h, lib().bftsim_fetch(self.h, ctypes.byref(r)), "bftsim_fetch")
+        return _abi.shape_result(arrs, n, self.cfg.heights)
+
     def sync(self):
         _check(self.h, lib().bftsim_sync(self.h), "bftsim_sync")
 
@@ -143,6 +153,17 @@ class Simulator:
         a, b = ctypes.c_float(), ctypes.c_float()
         _check(self.h, lib().bftsim_last_kernel_ms(self.h, ctypes.byref(a), ctypes.byref(b)), "kernel_ms")
         return a.value, b.value
+
+    def kernel_ms_sum(self):
+        """(consensus ms, hash ms, launches) summed over the launches since the previous call."""
+        a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint32()
+        _check(self.h, lib().bftsim_kernel_ms_sum(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)),
+               "kernel_ms_sum")
+        return a.value, b.value, n.value
+
+    def set_pipeline(self, on: bool):
+        """Batch throughput mode: hash pass of launch k overlaps the consensus of launch k+1."""
+        _check(self.h, lib().bftsim_set_pipeline(self.h, 1 if on else 0), "bftsim_set_pipeline")
 
     def stats(self):
         s = _abi.CStats()

@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/bftsim.h"
@@ -366,8 +367,22 @@ struct bftsim {
     uint64_t* h_trace = nullptr;
     uint32_t trace_ticks = 0;
     uint64_t last_n = 0, last_first = 0;
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     hipStream_t last_stream = nullptr;
+    // pipelined launches (bftsim_set_pipeline): two row-table sets used alternately, the hash pass of
+    // launch k on its own stream `hs`, overlapping the consensus kernel of launch k+1
+    int pipeline = 0;
+    hipStream_t hs = nullptr;
+    uint32_t* alt_ch = nullptr; uint32_t* alt_flags = nullptr; uint32_t* alt_ticks = nullptr;
+    uint64_t* alt_views = nullptr; uint32_t* alt_rec = nullptr; uint8_t* alt_hash = nullptr;
+    hipEvent_t set_done[2] = {nullptr, nullptr};    // hash pass of the last launch that used set 0 / 1
+    bool set_busy[2] = {false, false};
+    uint32_t cur_set = 0;
+    // per-launch kernel timing: a ring of event quadruples, read by bftsim_kernel_ms_sum
+    static constexpr uint32_t RING = 64;
+    struct LaunchEv { hipEvent_t c0, c1, h0, h1; bool has_hash, pending; } ring[RING] = {};
+    uint32_t ring_head = 0;
+    double acc_c = 0, acc_h = 0;
+    uint32_t acc_n = 0;
     int hash_mode = 0;   // 0: one lane pair per instance, 1: one wave (BFTSIM_HASH=coop), 2: one lane (=lane)
 };
 
@@ -386,6 +401,10 @@ static void free_bufs(bftsim* h) {
     (void)hipFree(h->d_rec); (void)hipFree(h->d_hash); (void)hipFree(h->d_trace); (void)hipFree(h->d_tips);
     (void)hipFree(h->d_rcs);
     h->d_rcs = nullptr;
+    (void)hipFree(h->alt_ch); (void)hipFree(h->alt_flags); (void)hipFree(h->alt_ticks); (void)hipFree(h->alt_views);
+    (void)hipFree(h->alt_rec); (void)hipFree(h->alt_hash);
+    h->alt_ch = h->alt_flags = h->alt_ticks = nullptr; h->alt_views = nullptr; h->alt_rec = nullptr; h->alt_hash = nullptr;
+    h->set_busy[0] = h->set_busy[1] = false;
     h->d_ch = h->d_flags = h->d_ticks = nullptr; h->d_views = nullptr;
     h->d_rec = nullptr; h->d_hash = nullptr; h->d_trace = nullptr; h->d_tips = nullptr;
     h->cap_inst = 0;
@@ -458,7 +477,11 @@ int bftsim_create(const bftsim_config* cfg, int hip_device, bftsim_t** out) {
     HIPCHECK(h, hipMemcpy(h->d_ghash, h->genesis_hash, 32, hipMemcpyHostToDevice));
     HIPCHECK(h, hipMalloc(&h->d_stats, 16 * sizeof(unsigned long long)));
     HIPCHECK(h, hipMalloc(&h->d_hist, bft::HIST_BINS * sizeof(uint64_t)));
-    for (int i = 0; i < 3; ++i) HIPCHECK(h, hipEventCreate(&h->ev[i]));
+    for (uint32_t i = 0; i < bftsim::RING; ++i) {
+        HIPCHECK(h, hipEventCreate(&h->ring[i].c0)); HIPCHECK(h, hipEventCreate(&h->ring[i].c1));
+        HIPCHECK(h, hipEventCreate(&h->ring[i].h0)); HIPCHECK(h, hipEventCreate(&h->ring[i].h1));
+    }
+    for (int i = 0; i < 2; ++i) HIPCHECK(h, hipEventCreateWithFlags(&h->set_done[i], hipEventDisableTiming));
     return BFTSIM_OK;
 }
 
@@ -467,7 +490,14 @@ void bftsim_destroy(bftsim_t* h) {
     (void)hipSetDevice(h->device);
     free_bufs(h);
     (void)hipFree(h->d_addr); (void)hipFree(h->d_ghash); (void)hipFree(h->d_stats); (void)hipFree(h->d_hist);
-    for (int i = 0; i < 3; ++i) if (h->ev[i]) (void)hipEventDestroy(h->ev[i]);
+    for (uint32_t i = 0; i < bftsim::RING; ++i) {
+        if (h->ring[i].c0) (void)hipEventDestroy(h->ring[i].c0);
+        if (h->ring[i].c1) (void)hipEventDestroy(h->ring[i].c1);
+        if (h->ring[i].h0) (void)hipEventDestroy(h->ring[i].h0);
+        if (h->ring[i].h1) (void)hipEventDestroy(h->ring[i].h1);
+    }
+    for (int i = 0; i < 2; ++i) if (h->set_done[i]) (void)hipEventDestroy(h->set_done[i]);
+    if (h->hs) (void)hipStreamDestroy(h->hs);
     delete h;
 }
 
@@ -487,6 +517,14 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg;
         uint64_t blocks = (n + per_block - 1) / per_block;
         HIPCHECK(h, hipMalloc(&h->d_rcs, blocks * bft::rcs_words(h->seg) * 4));
+    }
+    if (h->pipeline) {
+        HIPCHECK(h, hipMalloc(&h->alt_ch, n * 4));
+        HIPCHECK(h, hipMalloc(&h->alt_flags, n * 4));
+        HIPCHECK(h, hipMalloc(&h->alt_ticks, n * 4));
+        HIPCHECK(h, hipMalloc(&h->alt_views, n * 8));
+        HIPCHECK(h, hipMalloc(&h->alt_rec, n * h->hcap * 16));
+        HIPCHECK(h, hipMalloc(&h->alt_hash, n * h->hcap * 32));
     }
     h->cap_inst = n;
     return BFTSIM_OK;
@@ -561,44 +599,112 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         g_stamp_waves = waves;
     }
 #endif
+    const bool pipe = h->pipeline && !p.need_seed && h->alt_rec;
+    if (pipe) {
+        // alternate row-table sets: the hash pass of launch k-1 may still be reading the other one
+        std::swap(h->d_ch, h->alt_ch); std::swap(h->d_flags, h->alt_flags); std::swap(h->d_ticks, h->alt_ticks);
+        std::swap(h->d_views, h->alt_views); std::swap(h->d_rec, h->alt_rec); std::swap(h->d_hash, h->alt_hash);
+        h->cur_set ^= 1u;
+        if (h->set_busy[h->cur_set]) HIPCHECK(h, hipStreamWaitEvent(s, h->set_done[h->cur_set], 0));
+        p.committed_height = h->d_ch; p.flags = h->d_flags; p.ticks = h->d_ticks; p.views = h->d_views;
+        p.rec = h->d_rec; p.hash = h->d_hash;
+        if (!h->hs) HIPCHECK(h, hipStreamCreateWithFlags(&h->hs, hipStreamNonBlocking));
+    }
+    bftsim::LaunchEv& ev = h->ring[h->ring_head % bftsim::RING];
+    if (ev.pending) {                                    // 64 launches unread: fold the oldest in
+        HIPCHECK(h, hipEventSynchronize(ev.has_hash ? ev.h1 : ev.c1));
+        float a = 0, b = 0;
+        HIPCHECK(h, hipEventElapsedTime(&a, ev.c0, ev.c1));
+        if (ev.has_hash) HIPCHECK(h, hipEventElapsedTime(&b, ev.h0, ev.h1));
+        h->acc_c += a; h->acc_h += b; h->acc_n += 1;
+        ev.pending = false;
+    }
+    h->ring_head += 1;
     HIPCHECK(h, hipMemsetAsync(h->d_rec, 0, n * h->hcap * 16, s));
     HIPCHECK(h, hipMemsetAsync(h->d_hist, 0, bft::HIST_BINS * sizeof(uint64_t), s));
     uint32_t per_block = h->seg > 64 ? 1u : 64u / h->seg;      // instances per workgroup
     uint32_t grid = (uint32_t)((n + per_block - 1) / per_block);
     size_t lds = bft::lds_bytes(h->seg, p.need_seed != 0);
-    HIPCHECK(h, hipEventRecord(h->ev[0], s));
+    HIPCHECK(h, hipEventRecord(ev.c0, s));
     if (p.need_seed) HIPCHECK(h, bft::launch_consensus<true>(h->seg, dim3(grid), lds, s, p));
     else HIPCHECK(h, bft::launch_consensus<false>(h->seg, dim3(grid), lds, s, p));
-    HIPCHECK(h, hipEventRecord(h->ev[1], s));
+    HIPCHECK(h, hipEventRecord(ev.c1, s));
+    ev.has_hash = !p.need_seed;
+    ev.pending = true;
     if (!p.need_seed) {
+        hipStream_t t = pipe ? h->hs : s;
+        if (pipe) HIPCHECK(h, hipStreamWaitEvent(t, ev.c1, 0));
+        HIPCHECK(h, hipEventRecord(ev.h0, t));
         if (h->hash_mode == 1)
-            hipLaunchKernelGGL(bft::bft_hash_coop_kernel, dim3((uint32_t)n), dim3(64), 0, s, p);
+            hipLaunchKernelGGL(bft::bft_hash_coop_kernel, dim3((uint32_t)n), dim3(64), 0, t, p);
         else if (h->hash_mode == 2)
-            hipLaunchKernelGGL(bft::bft_hash_lane_kernel, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, s, p);
+            hipLaunchKernelGGL(bft::bft_hash_lane_kernel, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, t, p);
         else
-            hipLaunchKernelGGL(bft::bft_hash_pair_kernel, dim3((uint32_t)((n + 31) / 32)), dim3(64), 0, s, p);
+            hipLaunchKernelGGL(bft::bft_hash_pair_kernel, dim3((uint32_t)((n + 31) / 32)), dim3(64), 0, t, p);
         HIPCHECK(h, hipGetLastError());
+        HIPCHECK(h, hipEventRecord(ev.h1, t));
+        if (pipe) {
+            HIPCHECK(h, hipEventRecord(h->set_done[h->cur_set], t));
+            h->set_busy[h->cur_set] = true;
+        }
     }
-    HIPCHECK(h, hipEventRecord(h->ev[2], s));
     h->last_n = n;
     h->last_first = first;
     h->last_stream = s;
     return BFTSIM_OK;
 }
 
-int bftsim_sync(bftsim_t* h) {
-    if (!h) return BFTSIM_EINVAL;
+static int sync_all(bftsim* h) {
     HIPCHECK(h, hipSetDevice(h->device));
     HIPCHECK(h, hipStreamSynchronize(h->last_stream));
+    if (h->hs) HIPCHECK(h, hipStreamSynchronize(h->hs));
     return BFTSIM_OK;
 }
 
-int bftsim_last_kernel_ms(bftsim_t* h, float* cms, float* hms) {
+int bftsim_set_pipeline(bftsim_t* h, int on) {
     if (!h) return BFTSIM_EINVAL;
-    HIPCHECK(h, hipEventSynchronize(h->ev[2]));
+    if ((on != 0) == (h->pipeline != 0)) return BFTSIM_OK;
+    int rc = h->last_stream || h->hs ? sync_all(h) : BFTSIM_OK;
+    if (rc) return rc;
+    h->pipeline = on != 0;
+    (void)hipSetDevice(h->device);
+    free_bufs(h);                                   // re-sized (one or two sets) by the next prepare
+    return BFTSIM_OK;
+}
+
+int bftsim_kernel_ms_sum(bftsim_t* h, double* consensus_ms, double* hash_ms, uint32_t* launches) {
+    if (!h) return BFTSIM_EINVAL;
+    for (uint32_t i = 0; i < bftsim::RING; ++i) {
+        bftsim::LaunchEv& ev = h->ring[i];
+        if (!ev.pending) continue;
+        HIPCHECK(h, hipEventSynchronize(ev.has_hash ? ev.h1 : ev.c1));
+        float a = 0, b = 0;
+        HIPCHECK(h, hipEventElapsedTime(&a, ev.c0, ev.c1));
+        if (ev.has_hash) HIPCHECK(h, hipEventElapsedTime(&b, ev.h0, ev.h1));
+        h->acc_c += a; h->acc_h += b; h->acc_n += 1;
+        ev.pending = false;
+    }
+    if (consensus_ms) *consensus_ms = h->acc_c;
+    if (hash_ms) *hash_ms = h->acc_h;
+    if (launches) *launches = h->acc_n;
+    h->acc_c = h->acc_h = 0;
+    h->acc_n = 0;
+    return BFTSIM_OK;
+}
+
+int bftsim_sync(bftsim_t* h) {
+    if (!h) return BFTSIM_EINVAL;
+    if (!h->last_stream && !h->hs) return BFTSIM_OK;
+    return sync_all(h);
+}
+
+int bftsim_last_kernel_ms(bftsim_t* h, float* cms, float* hms) {
+    if (!h || h->ring_head == 0) return BFTSIM_EINVAL;
+    bftsim::LaunchEv& ev = h->ring[(h->ring_head - 1) % bftsim::RING];
+    HIPCHECK(h, hipEventSynchronize(ev.has_hash ? ev.h1 : ev.c1));
     float a = 0, b = 0;
-    HIPCHECK(h, hipEventElapsedTime(&a, h->ev[0], h->ev[1]));
-    HIPCHECK(h, hipEventElapsedTime(&b, h->ev[1], h->ev[2]));
+    HIPCHECK(h, hipEventElapsedTime(&a, ev.c0, ev.c1));
+    if (ev.has_hash) HIPCHECK(h, hipEventElapsedTime(&b, ev.h0, ev.h1));
     if (cms) *cms = a;
     if (hms) *hms = b;
     return BFTSIM_OK;
@@ -607,8 +713,8 @@ int bftsim_last_kernel_ms(bftsim_t* h, float* cms, float* hms) {
 int bftsim_fetch(bftsim_t* h, bftsim_result* out) {
     if (!h || !out) return BFTSIM_EINVAL;
     if (h->window) return fail(h, BFTSIM_EINVAL, "windowed run: per-height rows are not kept (bftsim_fetch_summary)");
-    HIPCHECK(h, hipSetDevice(h->device));
-    HIPCHECK(h, hipStreamSynchronize(h->last_stream));
+    if (h->last_n == 0) return fail(h, BFTSIM_EINVAL, "nothing launched");
+    if (int rc = sync_all(h)) return rc;
     uint64_t n = h->last_n;
     uint32_t H = h->cfg.heights, hc = h->hcap;
     HIPCHECK(h, hipMemcpy(out->committed_height, h->d_ch, n * 4, hipMemcpyDeviceToHost));
@@ -654,7 +760,7 @@ int bftsim_run(bftsim_t* h, uint64_t first, uint64_t n, bftsim_result* out) {
 int bftsim_fetch_summary(bftsim_t* h, uint32_t* committed_height, uint32_t* flags, uint32_t* ticks,
                          uint64_t* views, uint8_t* tip_hash) {
     if (!h || h->last_n == 0) return BFTSIM_EINVAL;
-    HIPCHECK(h, hipSetDevice(h->device));
+    if (int rc = sync_all(h)) return rc;                // the hash pass may run on its own stream
     uint64_t n = h->last_n;
     if (tip_hash) {
         bft::Params p = make_params(h, h->last_first, n);

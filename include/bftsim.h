@@ -44,7 +44,7 @@ extern "C" {
 #define BFTSIM_FLAG_WINDOW 64u       /* windowed run: a lookup older than the row ring (result unpinned) */
 
 typedef struct bftsim_config {
-    uint32_t n;                  /* validators per instance: 1..64 */
+    uint32_t n;                  /* validators per instance: 1..256 */
     uint32_t heights;            /* stop once the canonical chain reaches this height */
     uint32_t max_ticks;          /* cap on ticks (a tick = block_period = RC timeout) */
     uint32_t block_period;       /* seconds (examples/c1.toml:6) */
@@ -101,6 +101,15 @@ int bftsim_fetch(bftsim_t *h, bftsim_result *out);
 int bftsim_stats_get(bftsim_t *h, bftsim_stats *out);   /* device reduction + copy */
 /* per-kernel device time of the last launch, from HIP events on the launch stream (ms) */
 int bftsim_last_kernel_ms(bftsim_t *h, float *consensus_ms, float *hash_ms);
+/* summed per-kernel device times (ms) of every launch since the previous call, without blocking
+ * between launches (waits only for the launches being summed) */
+int bftsim_kernel_ms_sum(bftsim_t *h, double *consensus_ms, double *hash_ms, uint32_t *launches);
+/* pipelined launches (power-of-two N, the batch throughput mode of the benchmark): two sets of
+ * per-height row tables used alternately, and the block-hash pass of launch k on a second stream,
+ * where it overlaps the consensus kernel of launch k+1. Results of a launch are complete once
+ * bftsim_sync returns; bftsim_fetch/_stats_get/_fetch_summary read the last launch. Takes effect at
+ * the next bftsim_prepare (buffers are re-allocated). */
+int bftsim_set_pipeline(bftsim_t *h, int on);
 /* optional per-tick state digests of the next launch (debug; NULL disables) */
 int bftsim_set_trace(bftsim_t *h, uint64_t *host_out, uint32_t trace_ticks);
 /* windowed runs for long horizons (10,000 heights x 1M instances): keep only a ring

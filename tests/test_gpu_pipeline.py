@@ -1,0 +1,57 @@
+"""GPU: the pipelined launch mode of the benchmark (bftsim_set_pipeline) — alternating row-table
+sets, the block-hash pass of launch k on a second stream overlapping the consensus of launch k+1 —
+gives the oracle's results for every launch, and the per-launch HIP-event timings are all read."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from bftsim.configs import cfg3, BftConfig
+from parity_util import assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+def _sim(cfg):
+    from bftsim.runtime import Simulator
+    return Simulator(cfg)
+
+
+def test_pipelined_launches_match_oracle():
+    cfg = cfg3(heights=30)
+    n = 64
+    sim = _sim(cfg)
+    try:
+        sim.set_pipeline(True)
+        sim.prepare(n)
+        sim.kernel_ms_sum()
+        for k in range(5):                       # odd count: the last launch used the second set
+            sim.launch(k * n)
+        sim.sync()
+        got = sim.fetch()
+        c, h, nl = sim.kernel_ms_sum()
+        summ = sim.fetch_summary(n)
+        st = sim.stats()
+    finally:
+        sim.close()
+    ref = O.run(cfg, 4 * n, n)
+    assert_same(ref, got, "pipelined launch 4")
+    assert nl == 5 and c > 0 and h > 0
+    tips = got["block_hash"][np.arange(n), got["committed_height"] - 1]
+    assert np.array_equal(summ["tip_hash"], tips)
+    assert st["views"] == int(ref["views"].sum())
+
+
+def test_pipeline_toggle_and_sizes():
+    cfg = BftConfig(n=16, heights=20, seed=21, drop_ppm=100_000)
+    sim = _sim(cfg)
+    try:
+        for on in (True, False, True):
+            sim.set_pipeline(on)
+            sim.prepare(32)
+            sim.launch(0)
+            sim.launch(32)
+            sim.sync()
+            got = sim.fetch()
+            assert_same(O.run(cfg, 32, 32), got, f"pipeline={on}")
+    finally:
+        sim.close()
