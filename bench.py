@@ -39,6 +39,22 @@ def consensus_ops_per_view(n: int) -> int:
 
 
 HEADER_HASH_OPS = 14_976                # 2 Keccak-f[1600] x 24 rounds x 156 64-bit ops x 2
+# SURVEY §8d algorithmic HBM bytes per instance-round with in-kernel delivery masks: 8 B view descriptor
+# + 40 B result per committed height (hash 32 + round/proposer/time 8)
+ALGO_BYTES_PER_VIEW = 48
+
+
+def pmc_traffic():
+    """HBM bytes per dispatch per kernel from the newest committed PMC summary
+    (profiles/<round>/pmc_summary.json, written by scripts/pmc_summary.py from rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this same bench command)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return {k: v.get("hbm_bytes_per_dispatch") for k, v in d.get("kernels", {}).items()}, \
+        os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(cfg, sample: int, threads: int, name: str = "cfg3"):
@@ -85,7 +101,7 @@ def main():
     if args.heights is None:
         args.heights = 10_000 if c5 else 100
     if args.cpu_sample is None:
-        args.cpu_sample = 512 if c5 else 768
+        args.cpu_sample = 512 if c5 else 16_384
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -155,6 +171,8 @@ def main():
             dom, ops, ms = "bft_hash_kernel", h_ops, hms
         achieved = ops / (ms / 1e3) / 1e12
         peak = VALU_PEAK / 1e12
+        traffic, traffic_src = pmc_traffic()
+        algo_bytes = ALGO_BYTES_PER_VIEW * views_rank
         def trim(h):
             h = list(h)
             while h and h[-1] == 0:
@@ -189,7 +207,11 @@ def main():
             },
             "roofline": {
                 "bound": "valu", "kernel": dom, "achieved": achieved, "peak": peak,
-                "unit": "Tops/s", "frac": achieved / peak, "traffic": None,
+                "unit": "Tops/s", "frac": achieved / peak,
+                "traffic": (traffic or {}).get(dom),
+                "traffic_source": traffic_src,
+                "hbm": {"algorithmic_bytes": algo_bytes, "achieved_GBps": algo_bytes / (ms / 1e3) / 1e9,
+                        "peak_GBps": HBM_PEAK / 1e9, "frac": algo_bytes / (ms / 1e3) / HBM_PEAK},
                 "kernel_ms": {"bft_consensus_kernel": cms, "bft_hash_kernel": hms},
                 "ops_model": "consensus 4*N*(3*ceil(N/64)+8) lane-ops per instance-round; "
                              "hash 14976 lane-ops per header (SURVEY.md 8d)",

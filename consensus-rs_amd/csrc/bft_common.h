@@ -56,6 +56,8 @@ struct Params {
     uint32_t window_mask;             // 0: rec/hash rows for every height; else ring of window_mask+1 rows
     uint32_t rows;                    // rec/hash rows per instance (hcap, or the ring size)
     uint32_t* rcs;                    // RoundChangeSet tables: per wave / workgroup rcs_words(seg) words
+    uint32_t q;                       // floor(2N/3) (two_thirds_majority, validator.rs:149-154)
+    uint32_t nmask;                   // N-1 when N is a power of two (x mod N = x & nmask), else 0
 };
 
 // flags (same bits as the oracle)

@@ -86,6 +86,8 @@ inline Params params_from_config(const bftsim_config& c, uint32_t seg, uint32_t 
     p.n_instances = (uint32_t)n;
     p.genesis_seed = genesis_seed;
     p.fast = 1;
+    p.q = (2u * c.n) / 3u;
+    p.nmask = (c.n & (c.n - 1)) == 0 ? c.n - 1 : 0;
     return p;
 }
 

@@ -365,6 +365,7 @@ struct Sim {
 
     // ---------------------------------------------------------------- Core
     BFT_FN bool is_proposer(uint32_t who) const { return proposer == who; }
+    BFT_FN uint32_t mod_n(uint32_t x) const { return P.nmask ? (x & P.nmask) : x % P.n; }   // proposer index
 
     // Core::check_message (core.rs:366-399): 0 ok, 1 unknown, 2 future block, 3 old, 4 future msg
     BFT_FN int check_message(int code, uint32_t vh) const {
@@ -452,7 +453,7 @@ struct Sim {
         n_rcs = 0;
         lock = pp = pend = BLK_NONE;
         prep = comm = M::zero();
-        proposer = (last_seed + 0u) % P.n;
+        proposer = mod_n(last_seed);
         wait = false;
         st = ST_ACCEPT_REQUEST;
         new_round_change_timer();
@@ -465,7 +466,7 @@ struct Sim {
         if (!blk_valid(lock)) pp = BLK_NONE;
         prep = comm = M::zero();
         r = round;
-        proposer = (last_seed + round) % P.n;
+        proposer = mod_n(last_seed + round);
         wait = false;
         st = ST_ACCEPT_REQUEST;
         if (is_proposer(me)) {
@@ -506,7 +507,7 @@ struct Sim {
                 uint32_t bh = blk_h(b);
                 if (bh > last) return;                                        // InvalidProposal
                 if (!blk_eq(canon_blk(bh), b)) return;                        // InvalidProposal
-                uint32_t old_prop = (canon_seed(bh - 1) + vr) % P.n;
+                uint32_t old_prop = mod_n(canon_seed(bh - 1) + vr);
                 if (old_prop == src) out_old_commit(vh, vr, b, byz);
             } else if (res != 2) {
                 return;
@@ -530,7 +531,7 @@ struct Sim {
         if (vh != h || vr != r) return;
         prep.set(src);
         if (blk_valid(lock) && digest_match(d, wild, lock)) { lock_hash(); st = ST_PREPARED; send_commit(); }
-        if ((prep | comm).popc() > (2u * P.n) / 3u) { lock_hash(); st = ST_PREPARED; send_commit(); }
+        if ((prep | comm).popc() > P.q) { lock_hash(); st = ST_PREPARED; send_commit(); }
     }
 
     BFT_FN void handle_commit(uint32_t src, uint32_t vh, uint32_t vr, uint64_t d, bool wild) {    // commit.rs:63-111
@@ -538,7 +539,7 @@ struct Sim {
         if (res != 0) { if (res == 2) note_future_block(vh); return; }
         if (!digest_match(d, wild, pp) || vh != h || vr != r) return;
         comm.set(src);
-        if (comm.popc() > (2u * P.n) / 3u && st < ST_COMMITTED) { lock_hash(); core_commit(); }
+        if (comm.popc() > P.q && st < ST_COMMITTED) { lock_hash(); core_commit(); }
     }
 
     BFT_FN void handle_round_change(uint32_t src, uint32_t vh, uint32_t mr) {   // round_change.rs:65-98
@@ -546,7 +547,7 @@ struct Sim {
         if (res != 0) { if (res == 2) note_future_block(vh); return; }
         if (r > mr && mr > 0) { send_round_change(mr); return; }
         int n = rcs_add(mr, src);
-        if ((uint32_t)n >= (2u * P.n) / 3u + 1u && wait && r < mr) {
+        if ((uint32_t)n >= P.q + 1u && wait && r < mr) {
             send_round_change(mr);
             start_new_round(mr);
         }
@@ -648,14 +649,12 @@ struct Sim {
             wv.lds_add(hist_slot(65u + (lat < 64u ? lat : 64u)), 1u);
             add = round + 1u;
         }
-        uint32_t* row = rec_row(x);
-        wv.gstore(row + 0, round);
-        wv.gstore(row + 2, blk_T(b));
-        wv.gstore(row + 3, seed);
-        wv.gstore(row + 1, blk_prop(b) | (blk_var(b) << 16) | (1u << 24));
+        // one 16-byte store per row (and two per hash row): whole 32-byte sectors, no partial writes
+        wv.gstore4(rec_row(x), round, blk_prop(b) | (blk_var(b) << 16) | (1u << 24), blk_T(b), seed);
         if (NEED_SEED) {
             uint32_t* dst = (uint32_t*)hash_row(x);
-            for (int i = 0; i < 8; ++i) wv.gstore(dst + i, hs[i]);
+            wv.gstore4(dst, hs[0], hs[1], hs[2], hs[3]);
+            wv.gstore4(dst + 4, hs[4], hs[5], hs[6], hs[7]);
         }
         return add;
     }
@@ -945,7 +944,7 @@ struct Sim {
             else if (ps.cm_h == h && ps.cm_r == r) CMacc = cmd & class_match(ps.cm_cls, ps.cm_v0, ps.cm_v1, ps.cm_w, pp);
         }
         if (PRacc.none() && CMacc.none()) return;
-        const uint32_t q = (2u * P.n) / 3u;
+        const uint32_t q = P.q;
         uint32_t n = P.n;
         M PR = rot(PRacc, off), CM = rot(CMacc, off);
         M U0 = rot(prep | comm, off), C0 = rot(comm, off);

@@ -48,6 +48,10 @@ struct WaveHip {
     __device__ static void gstore(uint32_t* p, uint32_t v) {
         __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    // 16-byte aligned row store (global_store_dwordx4; L1 is write-through, readers use L2 loads)
+    __device__ static void gstore4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+        *(uint4*)p = make_uint4(a, b, c, d);
+    }
     __device__ static void lds_add(uint32_t* p, uint32_t v) { atomicAdd(p, v); }
     __device__ static void gadd64(uint64_t* p, uint64_t v) { atomicAdd((unsigned long long*)p, (unsigned long long)v); }
 };
@@ -127,6 +131,10 @@ struct GroupHip {
     }
     __device__ static void gstore(uint32_t* p, uint32_t v) {
         __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // 16-byte aligned row store (global_store_dwordx4; L1 is write-through, readers use L2 loads)
+    __device__ static void gstore4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+        *(uint4*)p = make_uint4(a, b, c, d);
     }
     __device__ static void lds_add(uint32_t* p, uint32_t v) { atomicAdd(p, v); }
     __device__ static void gadd64(uint64_t* p, uint64_t v) { atomicAdd((unsigned long long*)p, (unsigned long long)v); }

@@ -77,6 +77,7 @@ struct EmuWave {
     }
     static uint32_t gload(const uint32_t* p) { return *p; }
     static void gstore(uint32_t* p, uint32_t v) { *p = v; }
+    static void gstore4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) { p[0] = a; p[1] = b; p[2] = c; p[3] = d; }
     static void lds_add(uint32_t* p, uint32_t v) { *p += v; }
     static void gadd64(uint64_t* p, uint64_t v) { *p += v; }
 };
@@ -100,6 +101,7 @@ struct EmuGroup {
     static uint64_t clock() { return 0; }
     static uint32_t gload(const uint32_t* p) { return *p; }
     static void gstore(uint32_t* p, uint32_t v) { *p = v; }
+    static void gstore4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) { p[0] = a; p[1] = b; p[2] = c; p[3] = d; }
     static void lds_add(uint32_t* p, uint32_t v) { *p += v; }
     static void gadd64(uint64_t* p, uint64_t v) { *p += v; }
 };
