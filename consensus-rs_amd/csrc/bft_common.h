@@ -58,6 +58,12 @@ struct Params {
     uint32_t* rcs;                    // RoundChangeSet tables: per wave / workgroup rcs_words(seg) words
     uint32_t q;                       // floor(2N/3) (two_thirds_majority, validator.rs:149-154)
     uint32_t nmask;                   // N-1 when N is a power of two (x mod N = x & nmask), else 0
+    // FAST launches (bft_wave.h): instances that need the general path are saved and resumed
+    uint32_t* resume_flags;           // [n_inst] 1 = saved by the FAST kernel
+    uint32_t* save;                   // [n_inst * 64][SAVE_WORDS] per-lane state
+    uint64_t save_stride;             // unused (kept for the layout)
+    uint32_t resume_mode;             // CPU emulator only: run the MODE_RESUME body
+    uint32_t pad2;
 };
 
 // flags (same bits as the oracle)
@@ -88,6 +94,13 @@ BFT_FN uint32_t blk_var(uint64_t b) { return (uint32_t)((b >> 33) & 1u); }
 BFT_FN uint32_t blk_T(uint64_t b) { return (uint32_t)(b >> 35); }
 BFT_FN bool blk_eq(uint64_t a, uint64_t b) {
     return blk_valid(a) && blk_valid(b) && ((a ^ b) & BLK_ID_MASK) == 0;
+}
+// 32-bit form of the id without the time tick: height (22 bits) | proposer (8) | variant | valid.
+// Equal for two valid blocks iff blk_eq (heights < 2^22 by the hcap limit, proposers < 256); 0 for
+// BLK_NONE.
+BFT_FN uint32_t blk_d32(uint64_t b) {
+    if (!blk_valid(b)) return 0;
+    return (uint32_t)(b & 0x3fffffu) | (blk_prop(b) << 22) | (blk_var(b) << 30) | 0x80000000u;
 }
 // digest comparison; a Byzantine vote's wildcard digest matches both variants (SPEC.md §6)
 BFT_FN bool digest_match(uint64_t d, bool wild, uint64_t t) {

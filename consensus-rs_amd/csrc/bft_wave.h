@@ -61,6 +61,9 @@ BFT_FN void outbox_clear(Outbox& o) {
 //   (aliases the records)             per-lane commit hand-off {x, blk lo, blk hi, round, seed}
 //                                     (also the Fisher-Yates scratch at init): written only after
 //                                     every receiver has read the phase's records
+//   [.., + 12*L*4)                    gossip outbound cache (backend.rs:141-148), SoA [word][lane]:
+//                                     per kind (Preprepare, Prepare, Commit, old Commit) the last
+//                                     subject sent {height, round, 32-bit block id}
 //   [.., + 528)                       per-wave histogram bins (HIST_BINS words)
 // The RoundChangeSet tables are lane-private and touched only by round changes: they live in global
 // memory (P.rcs, coalesced SoA per wave: K round words [k][lane], then the sender bitmaps as 2*NW
@@ -79,7 +82,8 @@ struct Layout {
     static constexpr uint32_t REC_OFF = 0;
     static constexpr uint32_t RC_OFF = REC_OFF + L * REC_WORDS * 4;
     static constexpr uint32_t CMT_OFF = REC_OFF;
-    static constexpr uint32_t HIST_OFF = RC_OFF;
+    static constexpr uint32_t CACHE_OFF = RC_OFF;
+    static constexpr uint32_t HIST_OFF = CACHE_OFF + 12u * L * 4u;
     static constexpr uint32_t RCS_WORDS = (uint32_t)K * (1u + 2u * NW) * L;    // global, per wave
     static constexpr uint32_t SEG_OFF = HIST_OFF + 528;
     static_assert(L * 8 <= L * REC_WORDS, "commit hand-off must fit in the record area");
@@ -99,13 +103,26 @@ BFT_FN uint32_t lds_bytes(uint32_t seg, bool need_seed) {
                                                                  : Layout<64>::bytes(need_seed);
 }
 
-template <class W, bool NEED_SEED, uint32_t S>
+// Kernel modes (S == 64 only for the last two):
+//   MODE_FULL    every path;
+//   MODE_FAST    the general one-message-at-a-time path is compiled out (a shorter hot loop and fewer
+//                live registers). A phase that needs it hands the instance over: its state is saved at
+//                the start of that phase (SAVE_WORDS per lane, P.save) and P.resume_flags is set;
+//   MODE_RESUME  the full kernel over the handed-over instances only, from their saved phase.
+constexpr int MODE_FULL = 0, MODE_FAST = 1, MODE_RESUME = 2;
+constexpr uint32_t SAVE_WORDS = 80;
+constexpr uint32_t SAVE_COLD = 72;   // words 72..78: outbox kinds that always take the general path
+
+template <class W, bool NEED_SEED, uint32_t S, int MODE = MODE_FULL>
 struct Sim {
+    static constexpr bool FAST = MODE == MODE_FAST;
+    static constexpr bool RESUME = MODE == MODE_RESUME;
+    static_assert(MODE == MODE_FULL || S == 64, "hand-over modes are for one instance per wave");
     using LY = Layout<S>;
     static constexpr int NW = LY::NW;
     static constexpr int RCS_K = LY::K;
     static constexpr uint32_t LDS_REC_OFF = LY::REC_OFF, LDS_RC_OFF = LY::RC_OFF, LDS_CMT_OFF = LY::CMT_OFF,
-                              LDS_HIST_OFF = LY::HIST_OFF,
+                              LDS_HIST_OFF = LY::HIST_OFF, LDS_CACHE_OFF = LY::CACHE_OFF,
                               LDS_SEG_OFF = LY::SEG_OFF, LDS_CHASH_OFF = LY::CHASH_OFF, LDS_SCR_OFF = LY::SCR_OFF;
     using M = Bits<NW>;
     const Params& P;
@@ -136,9 +153,6 @@ struct Sim {
     int32_t tick, timer_tick, rc_last_tick, wake_tick;
     uint32_t mint_height, miner_queue, sync_pending;
     uint64_t cand;
-    // gossip outbound cache (last subject per kind)
-    uint32_t s_pp_h, s_pp_r, s_pr_h, s_pr_r, s_cm_h, s_cm_r, s_ocm_h, s_ocm_r;
-    uint64_t s_pp_b, s_pr_d, s_cm_d, s_ocm_d;   // 0 = nothing sent yet
     // outbox of the next phase
     Outbox nx;
     // Core commit of this phase (for canonical resolution)
@@ -186,8 +200,7 @@ struct Sim {
         tick = 0; timer_tick = -1; rc_last_tick = 0; wake_tick = -1;
         mint_height = 0; miner_queue = 0; sync_pending = 0;
         cand = BLK_NONE;
-        s_pp_h = s_pp_r = s_pr_h = s_pr_r = s_cm_h = s_cm_r = s_ocm_h = s_ocm_r = 0;
-        s_pp_b = s_pr_d = s_cm_d = s_ocm_d = 0;
+        for (uint32_t k = 0; k < 12; ++k) *cache_p(k) = 0;
         outbox_clear(nx);
         commit_x = 0; commit_round = 0; commit_seed = 0; commit_blk = 0;
         lane_flags = 0;
@@ -234,37 +247,62 @@ struct Sim {
     }
 
     // ---------------------------------------------------------------- outbox (backend.rs:140-160)
+    // The outbound cache of ImplBackend::gossip (backend.rs:141-148): a message identical to the last
+    // one of its kind is not sent (nor self-delivered). Kept in LDS, {height, round, blk_d32} per kind.
+    BFT_FN uint32_t* cache_p(uint32_t w) const { return (uint32_t*)(lds + LDS_CACHE_OFF) + w * LY::L + lane; }
+    BFT_FN bool cache_hit(uint32_t kind, uint32_t vh, uint32_t vr, uint64_t d) {
+        const uint32_t d32 = blk_d32(d);
+        uint32_t* c = cache_p(3u * kind);
+        const uint32_t sd = c[2u * LY::L];
+        if (sd != 0 && c[0] == vh && c[LY::L] == vr && sd == d32) return true;
+        c[0] = vh; c[LY::L] = vr; c[2u * LY::L] = d32;
+        return false;
+    }
     BFT_FN void out_preprepare(uint32_t vh, uint32_t vr, uint64_t b, bool equiv) {
-        if (s_pp_b != 0 && s_pp_h == vh && s_pp_r == vr && blk_eq(s_pp_b, b)) return;
-        s_pp_h = vh; s_pp_r = vr; s_pp_b = b;
+        if (cache_hit(0, vh, vr, b)) return;
         if (nx.f & F_PP) { lane_flags |= FLAG_OUTBOX; return; }
         nx.f |= F_PP | (equiv ? F_PP_EQ : 0u); nx.pp_h = vh; nx.pp_r = vr; nx.pp_b = b;
     }
     BFT_FN void out_prepare(uint32_t vh, uint32_t vr, uint64_t d, bool wild) {
-        if (s_pr_d != 0 && s_pr_h == vh && s_pr_r == vr && blk_eq(s_pr_d, d)) return;
-        s_pr_h = vh; s_pr_r = vr; s_pr_d = d;
+        if (cache_hit(1, vh, vr, d)) return;
         if (nx.f & F_PR) { lane_flags |= FLAG_OUTBOX; return; }
         nx.f |= F_PR | (wild ? F_PR_W : 0u); nx.pr_h = vh; nx.pr_r = vr; nx.pr_d = d;
     }
     BFT_FN void out_commit(uint32_t vh, uint32_t vr, uint64_t d, bool wild) {
-        if (s_cm_d != 0 && s_cm_h == vh && s_cm_r == vr && blk_eq(s_cm_d, d)) return;
-        s_cm_h = vh; s_cm_r = vr; s_cm_d = d;
+        if (cache_hit(2, vh, vr, d)) return;
         if (nx.f & F_CM) { lane_flags |= FLAG_OUTBOX; return; }
         nx.f |= F_CM | (wild ? F_CM_W : 0u); nx.cm_h = vh; nx.cm_r = vr; nx.cm_d = d;
     }
+    // Old-block Commit, RoundChange and Sync always take the general path, which the FAST kernel
+    // does not have: there their fields go straight to the hand-over area (they are never read
+    // before the hand-over), keeping them out of the registers of the hot loop.
+    BFT_FN uint32_t* cold_p(uint32_t k) const {
+        return P.save + ((uint64_t)inst_local * LY::L + lane) * SAVE_WORDS + SAVE_COLD + k;
+    }
     BFT_FN void out_old_commit(uint32_t vh, uint32_t vr, uint64_t d, bool wild) {
-        if (s_ocm_d != 0 && s_ocm_h == vh && s_ocm_r == vr && blk_eq(s_ocm_d, d)) return;
-        s_ocm_h = vh; s_ocm_r = vr; s_ocm_d = d;
+        if (cache_hit(3, vh, vr, d)) return;
         if (nx.f & F_OCM) { lane_flags |= FLAG_OUTBOX; return; }
-        nx.f |= F_OCM | (wild ? F_OCM_W : 0u); nx.ocm_h = vh; nx.ocm_r = vr; nx.ocm_d = d;
+        nx.f |= F_OCM | (wild ? F_OCM_W : 0u);
+        if constexpr (FAST) {
+            *cold_p(0) = vh; *cold_p(1) = vr; *cold_p(2) = (uint32_t)d; *cold_p(3) = (uint32_t)(d >> 32);
+        } else {
+            nx.ocm_h = vh; nx.ocm_r = vr; nx.ocm_d = d;
+        }
     }
     BFT_FN void out_round_change(uint32_t vh, uint32_t vr) {
         if (nx.f & F_RC) { lane_flags |= FLAG_OUTBOX; return; }
-        nx.f |= F_RC; nx.rc_h = vh; nx.rc_r = vr;
+        nx.f |= F_RC;
+        if constexpr (FAST) { *cold_p(4) = vh; *cold_p(5) = vr; }
+        else { nx.rc_h = vh; nx.rc_r = vr; }
     }
     BFT_FN void out_sync(uint32_t height) {
-        if (nx.f & F_SYNC) { if (height < nx.sync_h) nx.sync_h = height; return; }
-        nx.f |= F_SYNC; nx.sync_h = height;
+        if constexpr (FAST) {
+            if (nx.f & F_SYNC) { if (height < *cold_p(6)) *cold_p(6) = height; return; }
+            nx.f |= F_SYNC; *cold_p(6) = height;
+        } else {
+            if (nx.f & F_SYNC) { if (height < nx.sync_h) nx.sync_h = height; return; }
+            nx.f |= F_SYNC; nx.sync_h = height;
+        }
     }
     BFT_FN void out_blocks(uint32_t lo, uint32_t hi) {
         if (lo > hi) return;
@@ -571,6 +609,7 @@ struct Sim {
     }
 
     BFT_FN void deliver_from(uint32_t s) {     // all messages of sender s (SPEC.md §2 order)
+        if constexpr (FAST) return;
         const uint32_t* m = rec_lds(seg_base + s);
         uint32_t f = m[0];
         if (f == 0) return;
@@ -808,7 +847,7 @@ struct Sim {
         if (rest) return PATH_GENERAL;
         if (ps.k_pp.any()) {
             // one Preprepare and nothing else: arrival order cannot matter
-            if (BFT_PP_PATH && (ps.k_pr | ps.k_cm | ps.k_blk).none() && ps.k_pp.popc() == 1) return PATH_PP;
+            if ((BFT_PP_PATH || FAST) && (ps.k_pr | ps.k_cm | ps.k_blk).none() && ps.k_pp.popc() == 1) return PATH_PP;
             return PATH_GENERAL;
         }
         if (ps.k_pr.none() && ps.k_cm.none()) return (ps.k_blk.any() && ps.u_blk) ? PATH_BLK : PATH_GENERAL;
@@ -849,7 +888,7 @@ struct Sim {
         bool any_pr = ballot(pr).any(), any_cm = ballot(cm).any(), any_bk = ballot(bk).any();
         bool any_pp = ballot(pq).any();
         bool mm_pr = false, mm_cm = false, mm_blk = false;
-        if (BFT_PP_PATH && any_pp) {
+        if ((BFT_PP_PATH || FAST) && any_pp) {
             uint32_t j = ps.k_pp.any() ? ps.k_pp.ctz_nz() : 0u;
             ps.pp_src = j;
             ps.pp_h = from_seg_lane(nx.pp_h, j);
@@ -1009,12 +1048,13 @@ struct Sim {
             BFT_STAMP(9);
             return;
         }
-        if (BFT_PP_PATH && path == PATH_PP) {         // deliver_from() of the single sender
+        if ((BFT_PP_PATH || FAST) && path == PATH_PP) {   // deliver_from() of the single sender
             if (mk.get(ps.pp_src) && !core_dead) handle_preprepare(ps.pp_src, ps.pp_h, ps.pp_r, ps.pp_b, ps.pp_eq != 0);
             BFT_STAMP(8);
             return;
         }
         // general path: every delivered non-empty sender, in rotated order, one at a time
+        if constexpr (FAST) return;                   // never reached: FAST bails before (run)
         M any = ps.k_pp | ps.k_pr | ps.k_cm | ps.k_ocm | ps.k_rc | ps.k_sync | ps.k_blk;
         M c = rot(mk & any, off);
         while (c.any()) {
@@ -1027,23 +1067,87 @@ struct Sim {
         BFT_STAMP(10);
     }
 
+    // ---------------------------------------------------------------- bail / resume (FAST)
+    // persistent per-lane and segment state, word by word (lane g's SAVE_WORDS words contiguous:
+    // one base pointer with immediate offsets — a strided SoA made the compiler hoist 80 addresses)
+#define BFT_STATE_32(X) X(h) X(r) X(st) X(n_rcs) X(proposer) X(last) X(last_seed) X(last_T) X(timer_tick) \
+    X(rc_last_tick) X(wake_tick) X(mint_height) X(miner_queue) X(sync_pending) X(lane_flags) X(canon_h)       \
+    X(done_tick) X(seg_flags) X(canon_tip_seed) X(canon_tick) X(nx.f) X(nx.pp_h) X(nx.pp_r) X(nx.pr_h)       \
+    X(nx.pr_r) X(nx.cm_h) X(nx.cm_r) X(nx.blk_lo) X(nx.blk_hi)
+#define BFT_STATE_64(X) X(lock) X(pp) X(pend) X(cand) X(canon_tip) X(views_acc) X(nx.pp_b) X(nx.pr_d)       \
+    X(nx.cm_d)
+    BFT_FN void save_state(uint32_t p) {
+        uint32_t* sv = P.save + ((uint64_t)inst_local * LY::L + lane) * SAVE_WORDS;
+#define save_p(k) (sv + (k))
+        uint32_t k = 0;
+#define BFT_SV32(f) *save_p(k++) = (uint32_t)(f);
+#define BFT_SV64(f) *save_p(k++) = (uint32_t)(f); *save_p(k++) = (uint32_t)((uint64_t)(f) >> 32);
+        BFT_STATE_32(BFT_SV32)
+        BFT_STATE_64(BFT_SV64)
+        for (int j = 0; j < NW; ++j) { BFT_SV64(prep.w[j]) BFT_SV64(comm.w[j]) }
+        for (uint32_t c = 0; c < 12; ++c) *save_p(k++) = *cache_p(c);
+        *save_p(k++) = (byz ? 1u : 0u) | (core_dead ? 2u : 0u) | (wait ? 4u : 0u) | (frozen ? 8u : 0u) |
+                       (seg_done ? 16u : 0u);
+        *save_p(k++) = (uint32_t)tick;
+        *save_p(k++) = p;
+        (void)k;                                       // k <= SAVE_COLD; the cold words are already stored
+#undef BFT_SV32
+#undef BFT_SV64
+    }
+    BFT_FN void load_state(uint32_t& p) {
+        const uint32_t* sv = P.save + ((uint64_t)inst_local * LY::L + lane) * SAVE_WORDS;
+        uint32_t k = 0;
+#define BFT_LD32(f) f = (decltype(f))*save_p(k++);
+#define BFT_LD64(f) { uint64_t lo_ = *save_p(k++); uint64_t hi_ = *save_p(k++); f = lo_ | (hi_ << 32); }
+        BFT_STATE_32(BFT_LD32)
+        BFT_STATE_64(BFT_LD64)
+        for (int j = 0; j < NW; ++j) { BFT_LD64(prep.w[j]) BFT_LD64(comm.w[j]) }
+        for (uint32_t c = 0; c < 12; ++c) *cache_p(c) = *save_p(k++);
+        const uint32_t b = *save_p(k++);
+        byz = (b & 1u) != 0; core_dead = (b & 2u) != 0; wait = (b & 4u) != 0; frozen = (b & 8u) != 0;
+        seg_done = (b & 16u) != 0;
+        tick = (int32_t)*save_p(k++);
+        p = *save_p(k++);
+        nx.ocm_h = sv[SAVE_COLD + 0]; nx.ocm_r = sv[SAVE_COLD + 1];
+        nx.ocm_d = (uint64_t)sv[SAVE_COLD + 2] | ((uint64_t)sv[SAVE_COLD + 3] << 32);
+        nx.rc_h = sv[SAVE_COLD + 4]; nx.rc_r = sv[SAVE_COLD + 5]; nx.sync_h = sv[SAVE_COLD + 6];
+#undef BFT_LD32
+#undef BFT_LD64
+#undef save_p
+    }
+
     // ---------------------------------------------------------------- the run
     BFT_FN void run() {
 #ifdef BFT_STAMPS
         for (int k = 0; k < 12; ++k) st_acc[k] = 0;
         st_t = wv.clock();
 #endif
-        if (P.byz_count > 0) init_byzantine();
+        // resume mode (S == 64): only instances a FAST launch handed over, from their saved phase
+        bool resuming = false;
+        uint32_t p0 = 0;
+        int32_t tick0 = 0;
+        if constexpr (RESUME) {
+            {
+                if (seg_done || P.resume_flags[inst_local] == 0) return;    // wave-uniform
+                load_state(p0);
+                tick0 = tick;
+                resuming = true;
+            }
+        }
+        if (!resuming && P.byz_count > 0) init_byzantine();
         for (uint32_t b = lane; b < HIST_BINS; b += LY::L) *hist_slot(b) = 0;
         sync();
-        for (tick = 0; tick < (int32_t)P.max_ticks; ++tick) {
+        bool bailed = false;
+        for (tick = tick0; tick < (int32_t)P.max_ticks; ++tick) {
             if (ballot(!seg_done).none()) break;
-            bool act = running && !seg_done;
+            bool act = running && !seg_done && !frozen;
             off_tick = offset_tick_part(off_inst, (uint32_t)tick);
             BFT_STAMP(7);
-            if (act) t_step();
+            if (act && !resuming) t_step();
             BFT_STAMP(0);
-            for (uint32_t p = 0;; ++p) {
+            const uint32_t pstart = resuming ? p0 : 0u;
+            resuming = false;
+            for (uint32_t p = pstart;; ++p) {
                 bool pend_l = act && !frozen && pending_local();
                 M bal = ballot(pend_l);
                 if (bal.none()) break;
@@ -1061,6 +1165,17 @@ struct Sim {
                 summarize(ps);
                 BFT_STAMP(1);
                 const uint32_t path = classify(ps);
+                if constexpr (FAST) {
+                    if (path == PATH_GENERAL) {               // hand the instance to the full kernel
+                        save_state(p);
+                        if (lane == 0) P.resume_flags[inst_local] = 1u;
+                        // wind down without an early exit (a `break` here costs ~25 VGPRs): nothing
+                        // is delivered, no phase or tick follows, no outputs are written
+                        bailed = true;
+                        seg_done = true;
+                        act = false;
+                    }
+                }
 #ifdef BFT_STAMPS
                 st_acc[6] += 1;                               // phases (a count, not cycles)
                 st_acc[11] += path == PATH_GENERAL ? 1 : 0;   // general-path phases
@@ -1102,7 +1217,7 @@ struct Sim {
                 if (v != 0) wv.gadd64(P.hist + b, v);
             }
         }
-        if (me == 0 && inst_local < P.n_instances) {
+        if (me == 0 && inst_local < P.n_instances && !bailed) {
             uint32_t flags = lf | seg_flags;
             if (!frozen && canon_h < P.heights) flags |= FLAG_TIMEOUT;
             uint32_t chh = canon_h < P.heights ? canon_h : P.heights;

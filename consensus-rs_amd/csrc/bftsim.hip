@@ -155,6 +155,22 @@ __global__ __launch_bounds__(S > 64 ? S : 64, S > 64 ? 1 : BFT_WAVES_PER_SIMD) v
     }
 }
 
+// FAST kernel (N = 64, power of two): no general path; instances needing it are saved for resume
+#ifndef BFT_FAST_WAVES_PER_SIMD
+#define BFT_FAST_WAVES_PER_SIMD 4
+#endif
+__global__ __launch_bounds__(64, BFT_FAST_WAVES_PER_SIMD) void bft_consensus_fast_kernel(Params p) {
+    extern __shared__ uint8_t lds[];
+    Sim<WaveHip, false, 64, MODE_FAST> sim(p, lds, blockIdx.x);
+    sim.run();
+}
+// the full kernel over the instances the FAST kernel handed over, from their saved phase
+__global__ __launch_bounds__(64, BFT_WAVES_PER_SIMD) void bft_consensus_resume_kernel(Params p) {
+    extern __shared__ uint8_t lds[];
+    Sim<WaveHip, false, 64, MODE_RESUME> sim(p, lds, blockIdx.x);
+    sim.run();
+}
+
 template <bool NEED_SEED>
 static hipError_t launch_consensus(uint32_t seg, dim3 grid, size_t lds, hipStream_t s, const Params& p) {
     switch (seg) {
@@ -370,6 +386,9 @@ struct bftsim {
     uint64_t* d_hist = nullptr;       // [HIST_BINS] of the last launch
     uint8_t* d_tips = nullptr;        // [cap_inst * 32]
     uint32_t* d_rcs = nullptr;        // RoundChangeSet tables, rcs_words(seg) per wave / workgroup
+    uint32_t* d_resume = nullptr;     // FAST launches: [cap_inst] hand-over flags
+    uint32_t* d_save = nullptr;       // FAST launches: [SAVE_WORDS][cap_inst * 64] saved lane state
+    int fast = 1;                     // FAST kernel + resume for N = 64 (BFTSIM_FAST=0 disables)
     uint32_t window = 0;              // 0: full per-height rows; else ring of `window` rows
     uint64_t* d_trace = nullptr;
     uint64_t* h_trace = nullptr;
@@ -409,6 +428,8 @@ static void free_bufs(bftsim* h) {
     (void)hipFree(h->d_rec); (void)hipFree(h->d_hash); (void)hipFree(h->d_trace); (void)hipFree(h->d_tips);
     (void)hipFree(h->d_rcs);
     h->d_rcs = nullptr;
+    (void)hipFree(h->d_resume); (void)hipFree(h->d_save);
+    h->d_resume = nullptr; h->d_save = nullptr;
     (void)hipFree(h->alt_ch); (void)hipFree(h->alt_flags); (void)hipFree(h->alt_ticks); (void)hipFree(h->alt_views);
     (void)hipFree(h->alt_rec); (void)hipFree(h->alt_hash);
     h->alt_ch = h->alt_flags = h->alt_ticks = nullptr; h->alt_views = nullptr; h->alt_rec = nullptr; h->alt_hash = nullptr;
@@ -475,6 +496,8 @@ int bftsim_create(const bftsim_config* cfg, int hip_device, bftsim_t** out) {
     {
         const char* hm = getenv("BFTSIM_HASH");
         h->hash_mode = (hm && strcmp(hm, "coop") == 0) ? 1 : (hm && strcmp(hm, "lane") == 0) ? 2 : 0;
+        const char* fm = getenv("BFTSIM_FAST");
+        h->fast = (fm && strcmp(fm, "0") == 0) ? 0 : 1;
     }
     *out = h;
     hipError_t e = hipSetDevice(hip_device);
@@ -525,6 +548,10 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg;
         uint64_t blocks = (n + per_block - 1) / per_block;
         HIPCHECK(h, hipMalloc(&h->d_rcs, blocks * bft::rcs_words(h->seg) * 4));
+    }
+    if (h->seg == 64 && h->cfg.n == 64) {          // FAST kernel hand-over buffers
+        HIPCHECK(h, hipMalloc(&h->d_resume, n * 4));
+        HIPCHECK(h, hipMalloc(&h->d_save, (uint64_t)bft::SAVE_WORDS * n * 64 * 4));
     }
     if (h->pipeline) {
         HIPCHECK(h, hipMalloc(&h->alt_ch, n * 4));
@@ -633,9 +660,23 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     uint32_t per_block = h->seg > 64 ? 1u : 64u / h->seg;      // instances per workgroup
     uint32_t grid = (uint32_t)((n + per_block - 1) / per_block);
     size_t lds = bft::lds_bytes(h->seg, p.need_seed != 0);
+    const bool fast = h->fast && h->d_save && !p.need_seed && !h->h_trace && h->seg == 64;
     HIPCHECK(h, hipEventRecord(ev.c0, s));
-    if (p.need_seed) HIPCHECK(h, bft::launch_consensus<true>(h->seg, dim3(grid), lds, s, p));
-    else HIPCHECK(h, bft::launch_consensus<false>(h->seg, dim3(grid), lds, s, p));
+    if (fast) {
+        // FAST kernel over every instance, then the full kernel over the ones it handed over
+        p.resume_flags = h->d_resume;
+        p.save = h->d_save;
+        p.save_stride = n * 64;
+        HIPCHECK(h, hipMemsetAsync(h->d_resume, 0, n * 4, s));
+        hipLaunchKernelGGL(bft::bft_consensus_fast_kernel, dim3(grid), dim3(64), lds, s, p);
+        HIPCHECK(h, hipGetLastError());
+        hipLaunchKernelGGL(bft::bft_consensus_resume_kernel, dim3(grid), dim3(64), lds, s, p);
+        HIPCHECK(h, hipGetLastError());
+    } else if (p.need_seed) {
+        HIPCHECK(h, bft::launch_consensus<true>(h->seg, dim3(grid), lds, s, p));
+    } else {
+        HIPCHECK(h, bft::launch_consensus<false>(h->seg, dim3(grid), lds, s, p));
+    }
     HIPCHECK(h, hipEventRecord(ev.c1, s));
     ev.has_hash = !p.need_seed;
     ev.pending = true;

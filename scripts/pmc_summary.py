@@ -13,7 +13,9 @@ import os
 import sys
 from collections import defaultdict
 
-SHORT = {"bft_consensus_kernel": "bft_consensus_kernel", "bft_hash_pair_kernel": "bft_hash_kernel",
+SHORT = {"bft_consensus_fast_kernel": "bft_consensus_fast_kernel",
+         "bft_consensus_resume_kernel": "bft_consensus_resume_kernel",
+         "bft_consensus_kernel": "bft_consensus_kernel", "bft_hash_pair_kernel": "bft_hash_kernel",
          "bft_hash_lane_kernel": "bft_hash_kernel", "bft_hash_coop_kernel": "bft_hash_kernel",
          "bft_stats_kernel": "bft_stats_kernel", "bft_tip_kernel": "bft_tip_kernel"}
 
@@ -76,6 +78,16 @@ def main():
         for c, v in sq.get(k, {}).items():
             e[c] = sum(v) / len(v)
         res["kernels"][k] = e
+    # N = 64 launches run the FAST kernel then the resume kernel (one dispatch each per launch):
+    # bench.py's HIP events bracket both, so the consensus entry is their per-launch sum
+    ks = res["kernels"]
+    parts = [ks.get("bft_consensus_fast_kernel"), ks.get("bft_consensus_resume_kernel")]
+    if all(parts) and "bft_consensus_kernel" not in ks:
+        e = {"composed_of": ["bft_consensus_fast_kernel", "bft_consensus_resume_kernel"]}
+        for f in ("avg_ms", "fetch_bytes_raw", "fetch_bytes", "write_bytes", "hbm_bytes_per_dispatch"):
+            if all(f in x for x in parts):
+                e[f] = parts[0][f] + parts[1][f]
+        ks["bft_consensus_kernel"] = e
     json.dump(res, open(dst, "w"), indent=1, sort_keys=True)
     print(json.dumps(res, indent=1, sort_keys=True))
 

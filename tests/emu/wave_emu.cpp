@@ -35,6 +35,7 @@ struct Sched {
     uint8_t* lds;
     uint32_t wave;
     int body;   // 0 consensus, 1 hash post-pass
+    bool fast;  // FAST kernel (S == 64, power-of-two N)
 };
 thread_local Sched* g = nullptr;
 
@@ -108,6 +109,18 @@ struct EmuGroup {
 
 template <bool NS, uint32_t S>
 void run_sim() {
+    if constexpr (S == 64 && !NS) {
+        if (g->fast) {                     // bft_consensus_fast_kernel
+            bft::Sim<EmuWave, false, 64, bft::MODE_FAST> sim(*g->P, g->lds, g->wave);
+            sim.run();
+            return;
+        }
+        if (g->P->resume_mode) {           // bft_consensus_resume_kernel
+            bft::Sim<EmuWave, false, 64, bft::MODE_RESUME> sim(*g->P, g->lds, g->wave);
+            sim.run();
+            return;
+        }
+    }
     if constexpr (S > 64) {
         bft::Sim<EmuGroup<(int)(S / 64)>, NS, S> sim(*g->P, g->lds, g->wave);
         sim.run();
@@ -145,9 +158,11 @@ void lane_entry(int lane) {
     g->op[lane] = 0;
 }
 
-int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds, int body = 0, int nl = 64) {
+int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds, int body = 0, int nl = 64,
+             bool fast = false) {
     static thread_local Sched s;
     g = &s;
+    s.fast = fast;
     s.nl = nl;
     s.body = body;
     s.P = &P;
@@ -288,9 +303,31 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
     std::vector<uint8_t> lds(bft::lds_bytes(seg, P.need_seed != 0));
     std::vector<uint32_t> rcs((size_t)waves * bft::rcs_words(seg), 0xcdcdcdcdu);
     P.rcs = rcs.data();
+    // as libbftsim: N = 64 runs the FAST kernel, then the full kernel resumes the instances it handed
+    // over (BFT_EMU_FAST=0: the full kernel alone)
+    const char* ef = getenv("BFT_EMU_FAST");
+    const bool fast = seg == 64 && cfg->n == 64 && !P.need_seed && !trace && !(ef && strcmp(ef, "0") == 0);
+    std::vector<uint32_t> resume, save;
+    if (fast) {
+        resume.assign(n, 0);
+        save.assign((size_t)n * 64 * bft::SAVE_WORDS, 0xcdcdcdcdu);
+        P.resume_flags = resume.data();
+        P.save = save.data();
+        for (uint32_t w = 0; w < waves; ++w) {
+            memset(lds.data(), 0xcd, lds.size());
+            if (run_wave(P, w, lds, 0, 64, true)) return -1;
+        }
+        P.resume_mode = 1;
+    }
     for (uint32_t w = 0; w < waves; ++w) {
         memset(lds.data(), 0xcd, lds.size());
         if (run_wave(P, w, lds, 0, seg > 64 ? (int)seg : 64)) return -1;
+    }
+    P.resume_mode = 0;
+    if (fast && getenv("BFT_EMU_FAST_REPORT")) {
+        uint64_t nb = 0;
+        for (uint64_t i = 0; i < n; ++i) nb += resume[i];
+        fprintf(stderr, "emu: FAST handed over %llu of %llu instances\n", (unsigned long long)nb, (unsigned long long)n);
     }
     // power-of-two N: the hash post-pass, as bft_hash_coop_kernel (one wave per instance,
     // BFTSIM_HASH=coop) or bft_hash_lane_kernel (one lane per instance, default)

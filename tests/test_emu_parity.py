@@ -18,6 +18,11 @@ CASES = [
     ("n4-cap2-drop30", lambda: BftConfig(n=4, heights=25, seed=12, drop_ppm=300_000, phase_cap=2), 0, 16),
     ("n16-crash-drop", lambda: BftConfig(n=16, heights=15, seed=21, drop_ppm=150_000,
                                          proposer_crash_ppm=300_000), 0, 4),
+    # N = 64: the FAST kernel hands instances needing the general path over to the full kernel
+    ("n64-fast-handover-drop", lambda: BftConfig(n=64, heights=10, seed=15, byz_count=21, drop_ppm=50_000), 0, 2),
+    ("n64-fast-handover-crash", lambda: BftConfig(n=64, heights=10, seed=22, drop_ppm=100_000,
+                                                  proposer_crash_ppm=300_000), 0, 2),
+    ("cfg4-n64", lambda: cfg4(64, heights=12), 0, 3),
     # workgroup segments (N > 64: 2 or 4 waves per instance, multi-word sender bitmaps)
     ("cfg4-n65", lambda: cfg4(65, heights=10), 5, 2),
     ("cfg4-n100", lambda: cfg4(100, heights=8), 0, 1),
@@ -72,3 +77,12 @@ def test_emulated_windowed_run_matches_streamed_oracle(name, mk, first, n, windo
     full = E.run(cfg, first, n)
     assert np.array_equal(full["round_hist"], ref["round_hist"])
     assert np.array_equal(full["latency_hist"], ref["latency_hist"])
+
+
+@pytest.mark.parametrize("name,mk", [("cfg3", lambda: cfg3(heights=8)),
+                                     ("cfg4-n64", lambda: cfg4(64, heights=8))])
+def test_full_kernel_alone_n64(name, mk, monkeypatch):
+    """BFTSIM_FAST=0 on the GPU: the full kernel runs N = 64 by itself."""
+    monkeypatch.setenv("BFT_EMU_FAST", "0")
+    cfg = mk()
+    assert_same(O.run(cfg, 0, 2), E.run(cfg, 0, 2), name + " full kernel")

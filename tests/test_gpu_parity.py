@@ -52,3 +52,13 @@ def test_gpu_matches_oracle(name, mk, first, n):
     ref = O.run(cfg, first, n)
     got = gpu_run(cfg, first, n)
     assert_same(ref, got, name)
+
+
+@pytest.mark.parametrize("name,mk,n", [("cfg3", lambda: cfg3(heights=30), 16),
+                                       ("n64-byz21-drop5", lambda: BftConfig(n=64, heights=20, seed=15, byz_count=21,
+                                                                             drop_ppm=50_000), 8)])
+def test_gpu_full_kernel_alone_n64(name, mk, n, monkeypatch):
+    """BFTSIM_FAST=0: N = 64 through the full kernel alone (no FAST kernel, no hand-over)."""
+    monkeypatch.setenv("BFTSIM_FAST", "0")
+    cfg = mk()
+    assert_same(O.run(cfg, 0, n), gpu_run(cfg, 0, n), name + " full kernel")
