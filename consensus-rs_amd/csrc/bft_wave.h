@@ -74,24 +74,30 @@ BFT_FN void outbox_clear(Outbox& o) {
 //   [.., + L*32)                      per-lane commit hash
 //   [.., + 64*LANE_HASH_BUF)          per-lane header buffer of lane_block_hash (S <= 64; the
 //                                     workgroup kernels use a private buffer)
-template <uint32_t S>
+// FAST kernel layout (F, S == 64): records are never published (a phase that would need them hands the
+// instance over first), so the record area shrinks to the commit hand-off (5 words per lane) and the
+// segment words to the one segment's 8: 4.9 KB per wave, 8 waves per SIMD (the full layout's 9.7 KB
+// allowed 4).
+template <uint32_t S, bool F = false>
 struct Layout {
+    static_assert(!F || S == 64, "the FAST layout is for one instance per wave");
     static constexpr uint32_t L = S > 64 ? S : 64;
     static constexpr int NW = S > 64 ? (int)(S / 64) : 1;
     static constexpr int K = S > 64 ? 4 : 8;          // RoundChangeSet rounds kept per validator
+    static constexpr uint32_t CMT_STRIDE = F ? 5 : 8;  // words per lane of the commit hand-off
     static constexpr uint32_t REC_OFF = 0;
-    static constexpr uint32_t RC_OFF = REC_OFF + L * REC_WORDS * 4;
+    static constexpr uint32_t RC_OFF = REC_OFF + L * (F ? CMT_STRIDE : (uint32_t)REC_WORDS) * 4;
     static constexpr uint32_t CMT_OFF = REC_OFF;
     static constexpr uint32_t CACHE_OFF = RC_OFF;
     static constexpr uint32_t HIST_OFF = CACHE_OFF + 12u * L * 4u;
     static constexpr uint32_t RCS_WORDS = (uint32_t)K * (1u + 2u * NW) * L;    // global, per wave
     static constexpr uint32_t SEG_OFF = HIST_OFF + 528;
-    static_assert(L * 8 <= L * REC_WORDS, "commit hand-off must fit in the record area");
+    static_assert(L * CMT_STRIDE <= L * REC_WORDS, "commit hand-off must fit in the record area");
     static_assert(HIST_BINS * 4 <= 528, "histogram area");
     static constexpr uint32_t GRP_OFF = SEG_OFF + 256;
     static constexpr uint32_t CHASH_OFF = SEG_OFF + 512;
     static constexpr uint32_t SCR_OFF = CHASH_OFF + L * 32;
-    static constexpr uint32_t BYTES_POW2 = CHASH_OFF;
+    static constexpr uint32_t BYTES_POW2 = F ? SEG_OFF + 32 : CHASH_OFF;
     static constexpr uint32_t BYTES_SEED = S > 64 ? SCR_OFF : SCR_OFF + 64 * LANE_HASH_BUF;
     static constexpr uint32_t bytes(bool need_seed) { return need_seed ? BYTES_SEED : BYTES_POW2; }
 };
@@ -102,6 +108,7 @@ BFT_FN uint32_t lds_bytes(uint32_t seg, bool need_seed) {
     return seg == 256 ? Layout<256>::bytes(need_seed) : seg == 128 ? Layout<128>::bytes(need_seed)
                                                                  : Layout<64>::bytes(need_seed);
 }
+BFT_FN uint32_t lds_bytes_fast() { return Layout<64, true>::BYTES_POW2; }
 
 // Kernel modes (S == 64 only for the last two):
 //   MODE_FULL    every path;
@@ -118,7 +125,7 @@ struct Sim {
     static constexpr bool FAST = MODE == MODE_FAST;
     static constexpr bool RESUME = MODE == MODE_RESUME;
     static_assert(MODE == MODE_FULL || S == 64, "hand-over modes are for one instance per wave");
-    using LY = Layout<S>;
+    using LY = Layout<S, MODE == MODE_FAST>;
     static constexpr int NW = LY::NW;
     static constexpr int RCS_K = LY::K;
     static constexpr uint32_t LDS_REC_OFF = LY::REC_OFF, LDS_RC_OFF = LY::RC_OFF, LDS_CMT_OFF = LY::CMT_OFF,
@@ -703,7 +710,7 @@ struct Sim {
         bool c = commit_x != 0;
         M bal = ballot(c);
         if (bal.none()) return;
-        uint32_t* cm = (uint32_t*)(lds + LDS_CMT_OFF) + lane * 8;
+        uint32_t* cm = (uint32_t*)(lds + LDS_CMT_OFF) + lane * LY::CMT_STRIDE;
         if (c) {
             cm[0] = commit_x; cm[1] = (uint32_t)commit_blk; cm[2] = (uint32_t)(commit_blk >> 32);
             cm[3] = commit_round; cm[4] = commit_seed;
@@ -714,7 +721,7 @@ struct Sim {
         const bool mine = segbits.any() && !seg_done;
         const uint32_t lead = segbits.any() ? segbits.ctz_nz() : 0u;
         // fast path: every committer of the segment commits the same height as the first one
-        const uint32_t* cl = (const uint32_t*)(lds + LDS_CMT_OFF) + lead * 8;
+        const uint32_t* cl = (const uint32_t*)(lds + LDS_CMT_OFF) + lead * LY::CMT_STRIDE;
         uint32_t x0 = mine ? cl[0] : 0u;
         uint64_t b0 = mine ? ((uint64_t)cl[1] | ((uint64_t)cl[2] << 32)) : 0ull;
         bool other_h = c && mine && commit_x != x0;
@@ -758,7 +765,7 @@ struct Sim {
             while (bits.any()) {
                 uint32_t j = bits.ctz_nz();
                 bits.clear_lowest();
-                const uint32_t* cj = (const uint32_t*)(lds + LDS_CMT_OFF) + j * 8;
+                const uint32_t* cj = (const uint32_t*)(lds + LDS_CMT_OFF) + j * LY::CMT_STRIDE;
                 uint32_t x = cj[0];
                 uint64_t b = (uint64_t)cj[1] | ((uint64_t)cj[2] << 32);
                 if (x >= P.hcap) { fr = true; break; }
@@ -1181,7 +1188,8 @@ struct Sim {
                 st_acc[11] += path == PATH_GENERAL ? 1 : 0;   // general-path phases
 #endif
                 // records go to LDS only if some segment of the wave takes the general path
-                const bool pub = !BFT_LAZY_PUBLISH || ballot(path == PATH_GENERAL).any();
+                // (never in FAST: its layout has no record area, and a general phase has handed over)
+                const bool pub = !FAST && (!BFT_LAZY_PUBLISH || ballot(path == PATH_GENERAL).any());
                 if (pub) { publish(); sync(); }
                 else outbox_clear(nx);
                 BFT_STAMP(2);

@@ -157,7 +157,7 @@ __global__ __launch_bounds__(S > 64 ? S : 64, S > 64 ? 1 : BFT_WAVES_PER_SIMD) v
 
 // FAST kernel (N = 64, power of two): no general path; instances needing it are saved for resume
 #ifndef BFT_FAST_WAVES_PER_SIMD
-#define BFT_FAST_WAVES_PER_SIMD 4
+#define BFT_FAST_WAVES_PER_SIMD 5   // 96 VGPRs + 92 B/lane of spills; measured best of 4..8 (LDS allows 8)
 #endif
 __global__ __launch_bounds__(64, BFT_FAST_WAVES_PER_SIMD) void bft_consensus_fast_kernel(Params p) {
     extern __shared__ uint8_t lds[];
@@ -668,7 +668,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         p.save = h->d_save;
         p.save_stride = n * 64;
         HIPCHECK(h, hipMemsetAsync(h->d_resume, 0, n * 4, s));
-        hipLaunchKernelGGL(bft::bft_consensus_fast_kernel, dim3(grid), dim3(64), lds, s, p);
+        hipLaunchKernelGGL(bft::bft_consensus_fast_kernel, dim3(grid), dim3(64), bft::lds_bytes_fast(), s, p);
         HIPCHECK(h, hipGetLastError());
         hipLaunchKernelGGL(bft::bft_consensus_resume_kernel, dim3(grid), dim3(64), lds, s, p);
         HIPCHECK(h, hipGetLastError());

@@ -313,9 +313,10 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
         save.assign((size_t)n * 64 * bft::SAVE_WORDS, 0xcdcdcdcdu);
         P.resume_flags = resume.data();
         P.save = save.data();
+        std::vector<uint8_t> lds_fast(bft::lds_bytes_fast());     // the FAST kernel's exact LDS size
         for (uint32_t w = 0; w < waves; ++w) {
-            memset(lds.data(), 0xcd, lds.size());
-            if (run_wave(P, w, lds, 0, 64, true)) return -1;
+            memset(lds_fast.data(), 0xcd, lds_fast.size());
+            if (run_wave(P, w, lds_fast, 0, 64, true)) return -1;
         }
         P.resume_mode = 1;
     }
