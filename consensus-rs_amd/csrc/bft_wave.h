@@ -361,7 +361,7 @@ struct Sim {
             for (int i = 0; i < 8; ++i) hs[i] = out[i];
             for (int i = 0; i < 2; ++i)
                 for (int q = 0; q < 4; ++q) hb[4 * i + q] = (uint8_t)(out[i] >> (8 * q));
-            sd = seed_from_hash(hb, P.n);
+            sd = seed_from_hash(hb, nval());
         }
         commit_seed = sd;
         last = x;
@@ -410,7 +410,10 @@ struct Sim {
 
     // ---------------------------------------------------------------- Core
     BFT_FN bool is_proposer(uint32_t who) const { return proposer == who; }
-    BFT_FN uint32_t mod_n(uint32_t x) const { return P.nmask ? (x & P.nmask) : x % P.n; }   // proposer index
+    BFT_FN uint32_t mod_n(uint32_t x) const {
+        if constexpr (FAST) return x & 63u;
+        return P.nmask ? (x & P.nmask) : x % P.n;
+    }   // proposer index
 
     // Core::check_message (core.rs:366-399): 0 ok, 1 unknown, 2 future block, 3 old, 4 future msg
     BFT_FN int check_message(int code, uint32_t vh) const {
@@ -576,7 +579,7 @@ struct Sim {
         if (vh != h || vr != r) return;
         prep.set(src);
         if (blk_valid(lock) && digest_match(d, wild, lock)) { lock_hash(); st = ST_PREPARED; send_commit(); }
-        if ((prep | comm).popc() > P.q) { lock_hash(); st = ST_PREPARED; send_commit(); }
+        if ((prep | comm).popc() > qval()) { lock_hash(); st = ST_PREPARED; send_commit(); }
     }
 
     BFT_FN void handle_commit(uint32_t src, uint32_t vh, uint32_t vr, uint64_t d, bool wild) {    // commit.rs:63-111
@@ -584,7 +587,7 @@ struct Sim {
         if (res != 0) { if (res == 2) note_future_block(vh); return; }
         if (!digest_match(d, wild, pp) || vh != h || vr != r) return;
         comm.set(src);
-        if (comm.popc() > P.q && st < ST_COMMITTED) { lock_hash(); core_commit(); }
+        if (comm.popc() > qval() && st < ST_COMMITTED) { lock_hash(); core_commit(); }
     }
 
     BFT_FN void handle_round_change(uint32_t src, uint32_t vh, uint32_t mr) {   // round_change.rs:65-98
@@ -592,7 +595,7 @@ struct Sim {
         if (res != 0) { if (res == 2) note_future_block(vh); return; }
         if (r > mr && mr > 0) { send_round_change(mr); return; }
         int n = rcs_add(mr, src);
-        if ((uint32_t)n >= P.q + 1u && wait && r < mr) {
+        if ((uint32_t)n >= qval() + 1u && wait && r < mr) {
             send_round_change(mr);
             start_new_round(mr);
         }
@@ -655,6 +658,14 @@ struct Sim {
     // segment collectives: ballots as sender bitmaps; reductions (butterfly inside a wave
     // segment, LDS-combined per-wave partials for a workgroup segment)
     BFT_FN M ballot(bool p) { return M::from(wv.ballot(p)); }
+    // segment-uniform value: into a scalar register when the segment is the whole wave
+    BFT_FN uint32_t uni(uint32_t v) {
+        if constexpr (S == 64) return wv.uni(v);
+        else return v;
+    }
+    // N and floor(2N/3): compile-time constants in the FAST kernel (launched only for N = 64)
+    BFT_FN uint32_t nval() const { if constexpr (FAST) return 64u; else return P.n; }
+    BFT_FN uint32_t qval() const { if constexpr (FAST) return 42u; else return P.q; }
     BFT_FN void sync() { wv.sync(); }
     BFT_FN uint32_t seg_max(uint32_t v) {
         if constexpr (S > 64) { return wv.grp_max(v); }
@@ -789,12 +800,12 @@ struct Sim {
         }
         sync();
         if (mine) {
-            canon_h = segw[0];
-            canon_tip = (uint64_t)segw[2] | ((uint64_t)segw[3] << 32);
-            canon_tip_seed = segw[4];
-            views_acc = (uint64_t)segw[5] | ((uint64_t)segw[6] << 32);
-            canon_tick = segw[7];
-            if (segw[1]) { frozen = true; seg_flags |= FLAG_SAFETY; }
+            canon_h = uni(segw[0]);
+            canon_tip = (uint64_t)uni(segw[2]) | ((uint64_t)uni(segw[3]) << 32);
+            canon_tip_seed = uni(segw[4]);
+            views_acc = (uint64_t)uni(segw[5]) | ((uint64_t)uni(segw[6]) << 32);
+            canon_tick = uni(segw[7]);
+            if (uni(segw[1])) { frozen = true; seg_flags |= FLAG_SAFETY; }
         }
         commit_x = 0;
         sync();
@@ -814,7 +825,7 @@ struct Sim {
         uint32_t* segw = (uint32_t*)(lds + LDS_SEG_OFF) + (lane / S) * 8;
         const uint32_t mw = NW == 1 ? 2u : 8u;                            // mask words in segw
         if (me == 0 && !seg_done) {
-            uint32_t n = P.n;
+            uint32_t n = nval();
             for (uint32_t i = 0; i < n; ++i) perm[i] = (uint8_t)i;
             M mask = M::zero();
             uint32_t f = P.byz_count < n ? P.byz_count : n;
@@ -941,7 +952,7 @@ struct Sim {
     // rotate a sender mask into this receiver's delivery order (position 0 = first delivered)
     BFT_FN M rot(const M& m, uint32_t off) const {
         if (off == 0) return m;
-        uint32_t n = P.n;
+        uint32_t n = nval();
         if constexpr (NW == 1) {                     // 0 < off < n <= 64: both shifts in [1, 63]
             uint64_t nm = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
             return M::from(((m.w[0] >> off) | (m.w[0] << (n - off))) & nm);
@@ -952,7 +963,7 @@ struct Sim {
     BFT_FN static M low(uint32_t k) { return M::low(k); }
     // smallest position p in [0,n) with popcount(base | a & low(p+1) | b & low(p)) > q, else n
     BFT_FN uint32_t first_over(const M& base, const M& a, const M& b, uint32_t q) const {
-        uint32_t n = P.n;
+        uint32_t n = nval();
         if ((base | a | (b & low(n - 1))).popc() <= q) return n;
         uint32_t lo = 0, hi = n - 1;                 // answer in [lo, hi]
         while (lo < hi) {
@@ -990,8 +1001,8 @@ struct Sim {
             else if (ps.cm_h == h && ps.cm_r == r) CMacc = cmd & class_match(ps.cm_cls, ps.cm_v0, ps.cm_v1, ps.cm_w, pp);
         }
         if (PRacc.none() && CMacc.none()) return;
-        const uint32_t q = P.q;
-        uint32_t n = P.n;
+        const uint32_t q = qval();
+        uint32_t n = nval();
         M PR = rot(PRacc, off), CM = rot(CMacc, off);
         M U0 = rot(prep | comm, off), C0 = rot(comm, off);
         const uint32_t lastPR = PR.hibit();
@@ -1068,7 +1079,7 @@ struct Sim {
             uint32_t pos = c.ctz_nz();
             c.clear_lowest();
             uint32_t s = pos + off;
-            if (s >= P.n) s -= P.n;
+            if (s >= nval()) s -= nval();
             deliver_from(s);
         }
         BFT_STAMP(10);
@@ -1195,9 +1206,9 @@ struct Sim {
                 BFT_STAMP(2);
                 if (act && seg_pending) {
                     miner_step();                             // event step
-                    M mk = deliver_mask<NW>(P.seed, P.n, P.thr16, inst, (uint32_t)tick, p, me);
+                    M mk = deliver_mask<NW>(P.seed, nval(), P.thr16, inst, (uint32_t)tick, p, me);
                     uint32_t off = (path == PATH_GENERAL || path == PATH_PC)
-                                       ? offset_from_parts(P.seed, P.n, off_tick, p, me) : 0u;
+                                       ? offset_from_parts(P.seed, nval(), off_tick, p, me) : 0u;
                     BFT_STAMP(5);
                     deliver_phase(ps, path, mk, off);
                 }
@@ -1208,7 +1219,7 @@ struct Sim {
                 if (frozen) act = false;
             }
             if (P.trace && is_val && !seg_done && (uint32_t)tick < P.trace_ticks)
-                P.trace[((uint64_t)inst_local * P.trace_ticks + (uint32_t)tick) * P.n + me] = state_digest();
+                P.trace[((uint64_t)inst_local * P.trace_ticks + (uint32_t)tick) * nval() + me] = state_digest();
             if (!seg_done && (frozen || canon_h >= P.heights)) { seg_done = true; done_tick = (uint32_t)tick + 1; }
         }
 #ifdef BFT_STAMPS

@@ -34,6 +34,8 @@ struct WaveHip {
     __device__ static uint32_t readlane(uint32_t v, uint32_t l) {      // l wave-uniform
         return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_amdgcn_readfirstlane((int)l));
     }
+    // a wave-uniform value held in a VGPR → SGPR (frees the VGPR for the lane state)
+    __device__ static uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
     __device__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
     __device__ static void sync() {
         // Intra-wave LDS hand-off: the LDS executes one wave's DS instructions in program order,

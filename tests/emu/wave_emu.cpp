@@ -70,6 +70,12 @@ struct EmuWave {
         return (uint32_t)g->res[l];
     }
     static uint32_t readlane(uint32_t v, uint32_t src) { return shfl(v, src); }
+    // readfirstlane on the GPU: here it checks that the value really is wave-uniform
+    static uint32_t uni(uint32_t v) {
+        uint32_t f = shfl(v, 0);
+        if (f != v) { fprintf(stderr, "emu: uni() of a non-uniform value (lane %d)\n", g->cur); abort(); }
+        return v;
+    }
     static uint64_t clock() { return 0; }
     static void sync() {
         int l = g->cur;
