@@ -13,7 +13,7 @@
 // mod p = 2^256 - 2^32 - 977 kept fully reduced; products by 32x32->64 multiply-adds
 // (v_mad_u64_u32) and the special-form reduction 2^256 = 2^32 + 977 (mod p). Points in Jacobian
 // coordinates (a = 0 formulas); k*G through a fixed-base table of 32 windows x 255 affine points
-// (8-bit windows, 510 KB, L2-resident), k*R through a 4-bit window. Written once as host+device code
+// (8-bit windows, 510 KB, L2-resident), k*R through signed 4-bit digits. Written once as host+device code
 // (BFT_FN): the same source runs on the GPU and, host-compiled, in the CPU tests.
 #pragma once
 #include "bft_common.h"
@@ -21,34 +21,38 @@
 namespace bft {
 namespace secp {
 
+// Everything on the arithmetic path is forced inline: an out-of-line call passes its by-reference
+// points through scratch memory and spills the callee-saved VGPRs (measured: 2.5 KB scratch per lane).
+#define SECP_FN __attribute__((always_inline)) BFT_FN
+
 struct U256 {
     uint32_t v[8];
 };
 
 // ------------------------------------------------------------------------------ constants
-BFT_FN U256 c_p() { return U256{{0xFFFFFC2Fu, 0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}}; }
-BFT_FN U256 c_n() { return U256{{0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u, 0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}}; }
-BFT_FN U256 c_nhalf() { return U256{{0x681B20A0u, 0xDFE92F46u, 0x57A4501Du, 0x5D576E73u, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu}}; }
+SECP_FN U256 c_p() { return U256{{0xFFFFFC2Fu, 0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}}; }
+SECP_FN U256 c_n() { return U256{{0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u, 0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}}; }
+SECP_FN U256 c_nhalf() { return U256{{0x681B20A0u, 0xDFE92F46u, 0x57A4501Du, 0x5D576E73u, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu}}; }
 // 2^256 - n (129 bits)
 constexpr uint32_t NC0 = 0x2FC9BEBFu, NC1 = 0x402DA173u, NC2 = 0x50B75FC4u, NC3 = 0x45512319u;
-BFT_FN U256 c_gx() { return U256{{0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu, 0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu}}; }
-BFT_FN U256 c_gy() { return U256{{0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u, 0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u}}; }
+SECP_FN U256 c_gx() { return U256{{0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu, 0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu}}; }
+SECP_FN U256 c_gy() { return U256{{0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u, 0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u}}; }
 
 // ------------------------------------------------------------------------------ 256-bit helpers
-BFT_FN U256 u_zero() { return U256{{0, 0, 0, 0, 0, 0, 0, 0}}; }
-BFT_FN U256 u_small(uint32_t x) { return U256{{x, 0, 0, 0, 0, 0, 0, 0}}; }
-BFT_FN bool u_is_zero(const U256& a) {
+SECP_FN U256 u_zero() { return U256{{0, 0, 0, 0, 0, 0, 0, 0}}; }
+SECP_FN U256 u_small(uint32_t x) { return U256{{x, 0, 0, 0, 0, 0, 0, 0}}; }
+SECP_FN bool u_is_zero(const U256& a) {
     uint32_t x = 0;
     for (int i = 0; i < 8; ++i) x |= a.v[i];
     return x == 0;
 }
-BFT_FN bool u_eq(const U256& a, const U256& b) {
+SECP_FN bool u_eq(const U256& a, const U256& b) {
     uint32_t x = 0;
     for (int i = 0; i < 8; ++i) x |= a.v[i] ^ b.v[i];
     return x == 0;
 }
 // a >= b
-BFT_FN bool u_ge(const U256& a, const U256& b) {
+SECP_FN bool u_ge(const U256& a, const U256& b) {
     uint64_t br = 0;
     for (int i = 0; i < 8; ++i) {
         uint64_t d = (uint64_t)a.v[i] - b.v[i] - br;
@@ -57,7 +61,7 @@ BFT_FN bool u_ge(const U256& a, const U256& b) {
     return br == 0;
 }
 // r = a + b, returns the carry
-BFT_FN uint32_t u_add(U256& r, const U256& a, const U256& b) {
+SECP_FN uint32_t u_add(U256& r, const U256& a, const U256& b) {
     uint64_t c = 0;
     for (int i = 0; i < 8; ++i) {
         c += (uint64_t)a.v[i] + b.v[i];
@@ -67,7 +71,7 @@ BFT_FN uint32_t u_add(U256& r, const U256& a, const U256& b) {
     return (uint32_t)c;
 }
 // r = a - b, returns the borrow
-BFT_FN uint32_t u_sub(U256& r, const U256& a, const U256& b) {
+SECP_FN uint32_t u_sub(U256& r, const U256& a, const U256& b) {
     uint64_t br = 0;
     for (int i = 0; i < 8; ++i) {
         uint64_t d = (uint64_t)a.v[i] - b.v[i] - br;
@@ -76,17 +80,17 @@ BFT_FN uint32_t u_sub(U256& r, const U256& a, const U256& b) {
     }
     return (uint32_t)br;
 }
-BFT_FN U256 u_sel(bool c, const U256& a, const U256& b) {
+SECP_FN U256 u_sel(bool c, const U256& a, const U256& b) {
     U256 r;
     for (int i = 0; i < 8; ++i) r.v[i] = c ? a.v[i] : b.v[i];
     return r;
 }
-BFT_FN uint32_t u_bit(const U256& a, uint32_t i) { return (a.v[i >> 5] >> (i & 31u)) & 1u; }
-BFT_FN uint32_t u_nibble(const U256& a, uint32_t i) { return (a.v[i >> 3] >> (4u * (i & 7u))) & 15u; }
-BFT_FN uint32_t u_byte(const U256& a, uint32_t i) { return (a.v[i >> 2] >> (8u * (i & 3u))) & 255u; }
+SECP_FN uint32_t u_bit(const U256& a, uint32_t i) { return (a.v[i >> 5] >> (i & 31u)) & 1u; }
+SECP_FN uint32_t u_nibble(const U256& a, uint32_t i) { return (a.v[i >> 3] >> (4u * (i & 7u))) & 15u; }
+SECP_FN uint32_t u_byte(const U256& a, uint32_t i) { return (a.v[i >> 2] >> (8u * (i & 3u))) & 255u; }
 
 // big-endian 32 bytes <-> limbs
-BFT_FN U256 u_from_be(const uint8_t* b) {
+SECP_FN U256 u_from_be(const uint8_t* b) {
     U256 r;
     for (int i = 0; i < 8; ++i) {
         const uint8_t* q = b + 28 - 4 * i;
@@ -94,7 +98,7 @@ BFT_FN U256 u_from_be(const uint8_t* b) {
     }
     return r;
 }
-BFT_FN void u_to_be(const U256& a, uint8_t* b) {
+SECP_FN void u_to_be(const U256& a, uint8_t* b) {
     for (int i = 0; i < 8; ++i) {
         uint8_t* q = b + 28 - 4 * i;
         q[0] = (uint8_t)(a.v[i] >> 24); q[1] = (uint8_t)(a.v[i] >> 16); q[2] = (uint8_t)(a.v[i] >> 8); q[3] = (uint8_t)a.v[i];
@@ -102,7 +106,7 @@ BFT_FN void u_to_be(const U256& a, uint8_t* b) {
 }
 
 // 512-bit product t[16] = a * b (row-wise 32x32->64 multiply-adds)
-BFT_FN void u_mul_wide(uint32_t t[16], const U256& a, const U256& b) {
+SECP_FN void u_mul_wide(uint32_t t[16], const U256& a, const U256& b) {
     for (int i = 0; i < 16; ++i) t[i] = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -117,7 +121,7 @@ BFT_FN void u_mul_wide(uint32_t t[16], const U256& a, const U256& b) {
     }
 }
 // squaring: cross products once, doubled, plus the diagonal
-BFT_FN void u_sqr_wide(uint32_t t[16], const U256& a) {
+SECP_FN void u_sqr_wide(uint32_t t[16], const U256& a) {
     for (int i = 0; i < 16; ++i) t[i] = 0;
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
@@ -152,7 +156,7 @@ BFT_FN void u_sqr_wide(uint32_t t[16], const U256& a) {
 
 // ------------------------------------------------------------------------------ field mod p
 // t[16] mod p, using 2^256 = 0x1000003D1 (mod p)
-BFT_FN U256 fe_reduce_wide(const uint32_t t[16]) {
+SECP_FN U256 fe_reduce_wide(const uint32_t t[16]) {
     U256 r;
     uint64_t c = 0;
 #pragma unroll
@@ -187,35 +191,35 @@ BFT_FN U256 fe_reduce_wide(const uint32_t t[16]) {
     uint32_t br = u_sub(s, r, c_p());
     return br ? r : s;
 }
-BFT_FN U256 fe_mul(const U256& a, const U256& b) {
+SECP_FN U256 fe_mul(const U256& a, const U256& b) {
     uint32_t t[16];
     u_mul_wide(t, a, b);
     return fe_reduce_wide(t);
 }
-BFT_FN U256 fe_sqr(const U256& a) {
+SECP_FN U256 fe_sqr(const U256& a) {
     uint32_t t[16];
     u_sqr_wide(t, a);
     return fe_reduce_wide(t);
 }
-BFT_FN U256 fe_add(const U256& a, const U256& b) {
+SECP_FN U256 fe_add(const U256& a, const U256& b) {
     U256 r, s;
     uint32_t c = u_add(r, a, b);
     uint32_t br = u_sub(s, r, c_p());
     return (c || !br) ? s : r;
 }
-BFT_FN U256 fe_sub(const U256& a, const U256& b) {
+SECP_FN U256 fe_sub(const U256& a, const U256& b) {
     U256 r, s;
     uint32_t br = u_sub(r, a, b);
     u_add(s, r, c_p());
     return br ? s : r;
 }
-BFT_FN U256 fe_neg(const U256& a) { return fe_sub(u_zero(), a); }
-BFT_FN U256 fe_sqr_n(U256 a, int n) {
+SECP_FN U256 fe_neg(const U256& a) { return fe_sub(u_zero(), a); }
+SECP_FN U256 fe_sqr_n(U256 a, int n) {
     for (int i = 0; i < n; ++i) a = fe_sqr(a);
     return a;
 }
 // a^(2^223 - 1) and the shared head of the inverse / square-root addition chains (libsecp256k1's)
-BFT_FN void fe_chain_head(const U256& a, U256& x2, U256& x22, U256& x223) {
+SECP_FN void fe_chain_head(const U256& a, U256& x2, U256& x22, U256& x223) {
     x2 = fe_mul(fe_sqr(a), a);
     U256 x3 = fe_mul(fe_sqr(x2), a);
     U256 x6 = fe_mul(fe_sqr_n(x3, 3), x3);
@@ -229,7 +233,7 @@ BFT_FN void fe_chain_head(const U256& a, U256& x2, U256& x22, U256& x223) {
     x223 = fe_mul(fe_sqr_n(x220, 3), x3);
 }
 // a^(p-2)
-BFT_FN U256 fe_inv(const U256& a) {
+SECP_FN U256 fe_inv(const U256& a) {
     U256 x2, x22, x223;
     fe_chain_head(a, x2, x22, x223);
     U256 t = fe_mul(fe_sqr_n(x223, 23), x22);
@@ -238,7 +242,7 @@ BFT_FN U256 fe_inv(const U256& a) {
     return fe_mul(fe_sqr_n(t, 2), a);
 }
 // a^((p+1)/4): a square root when one exists (the caller checks r^2 == a)
-BFT_FN U256 fe_sqrt(const U256& a) {
+SECP_FN U256 fe_sqrt(const U256& a) {
     U256 x2, x22, x223;
     fe_chain_head(a, x2, x22, x223);
     U256 t = fe_mul(fe_sqr_n(x223, 23), x22);
@@ -249,7 +253,7 @@ BFT_FN U256 fe_sqrt(const U256& a) {
 // ------------------------------------------------------------------------------ scalars mod n
 // lo(8) + hi(len) * (2^256 - n) into out (8 + len + 4 limbs)
 template <int LEN>
-BFT_FN void sc_fold(const uint32_t* lo, const uint32_t* hi, uint32_t* out) {
+SECP_FN void sc_fold(const uint32_t* lo, const uint32_t* hi, uint32_t* out) {
     constexpr int OL = 8 + LEN + 4;
     const uint32_t nc[5] = {NC0, NC1, NC2, NC3, 1u};
     for (int i = 0; i < OL; ++i) out[i] = i < 8 ? lo[i] : 0u;
@@ -270,7 +274,7 @@ BFT_FN void sc_fold(const uint32_t* lo, const uint32_t* hi, uint32_t* out) {
         }
     }
 }
-BFT_FN U256 sc_reduce_wide(const uint32_t t[16]) {
+SECP_FN U256 sc_reduce_wide(const uint32_t t[16]) {
     uint32_t a[20], b[17], c[14];
     sc_fold<8>(t, t + 8, a);        // < 2^386: 13 limbs used
     sc_fold<5>(a, a + 8, b);        // < 2^260: 9 limbs used
@@ -288,47 +292,73 @@ BFT_FN U256 sc_reduce_wide(const uint32_t t[16]) {
     if (!u_sub(s, r, c_n())) r = s;
     return r;
 }
-BFT_FN U256 sc_mul(const U256& a, const U256& b) {
+SECP_FN U256 sc_mul(const U256& a, const U256& b) {
     uint32_t t[16];
     u_mul_wide(t, a, b);
     return sc_reduce_wide(t);
 }
-BFT_FN U256 sc_sqr(const U256& a) {
+SECP_FN U256 sc_sqr(const U256& a) {
     uint32_t t[16];
     u_sqr_wide(t, a);
     return sc_reduce_wide(t);
 }
-BFT_FN U256 sc_add(const U256& a, const U256& b) {
+SECP_FN U256 sc_add(const U256& a, const U256& b) {
     U256 r, s;
     uint32_t c = u_add(r, a, b);
     uint32_t br = u_sub(s, r, c_n());
     return (c || !br) ? s : r;
 }
-BFT_FN U256 sc_neg(const U256& a) {
+SECP_FN U256 sc_neg(const U256& a) {
     if (u_is_zero(a)) return a;
     U256 r;
     u_sub(r, c_n(), a);
     return r;
 }
 // x mod n for x < 2^256
-BFT_FN U256 sc_from_u256(const U256& a) {
+SECP_FN U256 sc_from_u256(const U256& a) {
     U256 s;
     return u_sub(s, a, c_n()) ? a : s;
 }
-// a^(n-2) (Fermat), 4-bit fixed window over the exponent
-BFT_FN U256 sc_inv(const U256& a) {
-    U256 tbl[16];
-    tbl[0] = u_small(1);
-    tbl[1] = a;
-    for (int i = 2; i < 16; ++i) tbl[i] = sc_mul(tbl[i - 1], a);
-    U256 e = c_n();
-    e.v[0] -= 2u;                   // n - 2 (no borrow: low limb 0xD0364141)
-    U256 r = u_small(1);
-    for (int w = 63; w >= 0; --w) {
-        if (w != 63) { r = sc_sqr(r); r = sc_sqr(r); r = sc_sqr(r); r = sc_sqr(r); }
-        uint32_t d = u_nibble(e, (uint32_t)w);
-        if (d) r = sc_mul(r, tbl[d]);
-    }
+// a^(n-2) (Fermat): sliding-window chain over the constant exponent (generated offline: 252 squarings,
+// 58 multiplications by the odd powers u1..u15, all at compile-time-constant indices, so no scratch)
+SECP_FN U256 sc_sqr_n(U256 a, int n) {
+    for (int i = 0; i < n; ++i) a = sc_sqr(a);
+    return a;
+}
+SECP_FN U256 sc_inv(const U256& a) {
+    const U256 u1 = a;
+    const U256 u2 = sc_sqr(a);
+    const U256 u3 = sc_mul(u2, u1), u5 = sc_mul(u3, u2), u7 = sc_mul(u5, u2), u9 = sc_mul(u7, u2);
+    const U256 u11 = sc_mul(u9, u2), u13 = sc_mul(u11, u2), u15 = sc_mul(u13, u2);
+    U256 r = u15;
+    for (int i = 0; i < 30; ++i) r = sc_mul(sc_sqr_n(r, 4), u15);   // the run of ones at the top
+    r = sc_mul(sc_sqr_n(r, 3), u7);
+    r = sc_mul(sc_sqr_n(r, 5), u11);
+    r = sc_mul(sc_sqr_n(r, 3), u5);
+    r = sc_mul(sc_sqr_n(r, 4), u5);
+    r = sc_mul(sc_sqr_n(r, 4), u7);
+    r = sc_mul(sc_sqr_n(r, 5), u13);
+    r = sc_mul(sc_sqr_n(r, 2), u3);
+    r = sc_mul(sc_sqr_n(r, 5), u7);
+    r = sc_mul(sc_sqr_n(r, 6), u13);
+    r = sc_mul(sc_sqr_n(r, 5), u11);
+    r = sc_mul(sc_sqr_n(r, 4), u13);
+    r = sc_mul(sc_sqr_n(r, 3), u1);
+    r = sc_mul(sc_sqr_n(r, 6), u5);
+    r = sc_mul(sc_sqr_n(r, 10), u7);
+    r = sc_mul(sc_sqr_n(r, 4), u7);
+    r = sc_mul(sc_sqr_n(r, 5), u15);
+    r = sc_mul(sc_sqr_n(r, 4), u15);
+    r = sc_mul(sc_sqr_n(r, 5), u9);
+    r = sc_mul(sc_sqr_n(r, 6), u11);
+    r = sc_mul(sc_sqr_n(r, 4), u13);
+    r = sc_mul(sc_sqr_n(r, 5), u3);
+    r = sc_mul(sc_sqr_n(r, 6), u13);
+    r = sc_mul(sc_sqr_n(r, 10), u13);
+    r = sc_mul(sc_sqr_n(r, 4), u9);
+    r = sc_mul(sc_sqr_n(r, 9), u9);
+    r = sc_mul(sc_sqr_n(r, 4), u15);
+    r = sc_mul(sc_sqr_n(r, 1), u1);
     return r;
 }
 
@@ -340,11 +370,11 @@ struct Jac {
 struct Aff {
     U256 x, y;
 };
-BFT_FN Jac jac_inf() { Jac r; r.x = u_small(1); r.y = u_small(1); r.z = u_zero(); r.inf = 1; return r; }
-BFT_FN Jac jac_from_aff(const Aff& a) { Jac r; r.x = a.x; r.y = a.y; r.z = u_small(1); r.inf = 0; return r; }
+SECP_FN Jac jac_inf() { Jac r; r.x = u_small(1); r.y = u_small(1); r.z = u_zero(); r.inf = 1; return r; }
+SECP_FN Jac jac_from_aff(const Aff& a) { Jac r; r.x = a.x; r.y = a.y; r.z = u_small(1); r.inf = 0; return r; }
 
 // dbl-2009-l: 2M + 5S
-BFT_FN Jac jac_dbl(const Jac& p) {
+SECP_FN Jac jac_dbl(const Jac& p) {
     if (p.inf) return p;
     U256 A = fe_sqr(p.x);
     U256 B = fe_sqr(p.y);
@@ -366,7 +396,7 @@ BFT_FN Jac jac_dbl(const Jac& p) {
     return r;
 }
 // madd-2007-bl: p + q with q affine (7M + 4S)
-BFT_FN Jac jac_add_aff(const Jac& p, const Aff& q) {
+SECP_FN Jac jac_add_aff(const Jac& p, const Aff& q) {
     if (p.inf) return jac_from_aff(q);
     U256 Z1Z1 = fe_sqr(p.z);
     U256 U2 = fe_mul(q.x, Z1Z1);
@@ -392,7 +422,7 @@ BFT_FN Jac jac_add_aff(const Jac& p, const Aff& q) {
     return r;
 }
 // add-2007-bl: general Jacobian addition (11M + 5S)
-BFT_FN Jac jac_add(const Jac& p, const Jac& q) {
+SECP_FN Jac jac_add(const Jac& p, const Jac& q) {
     if (p.inf) return q;
     if (q.inf) return p;
     U256 Z1Z1 = fe_sqr(p.z), Z2Z2 = fe_sqr(q.z);
@@ -418,7 +448,7 @@ BFT_FN Jac jac_add(const Jac& p, const Jac& q) {
     r.inf = 0;
     return r;
 }
-BFT_FN bool jac_to_aff(const Jac& p, Aff& a) {
+SECP_FN bool jac_to_aff(const Jac& p, Aff& a) {
     if (p.inf) return false;
     U256 zi = fe_inv(p.z);
     U256 zi2 = fe_sqr(zi);
@@ -431,7 +461,7 @@ BFT_FN bool jac_to_aff(const Jac& p, Aff& a) {
 constexpr uint32_t GTAB_WINDOWS = 32, GTAB_ENTRIES = 255;
 constexpr uint32_t GTAB_POINTS = GTAB_WINDOWS * GTAB_ENTRIES;
 
-BFT_FN Jac mul_g(const U256& k, const Aff* gtab) {
+SECP_FN Jac mul_g(const U256& k, const Aff* gtab) {
     Jac acc = jac_inf();
     for (uint32_t w = 0; w < GTAB_WINDOWS; ++w) {
         uint32_t j = u_byte(k, w);
@@ -439,23 +469,30 @@ BFT_FN Jac mul_g(const U256& k, const Aff* gtab) {
     }
     return acc;
 }
-// k * P, 4-bit fixed window (table of 1P..15P)
-BFT_FN Jac mul_var(const U256& k, const Aff& p) {
-    Jac tbl[16];
-    tbl[0] = jac_inf();
-    tbl[1] = jac_from_aff(p);
-    for (int i = 2; i < 16; ++i) tbl[i] = jac_add_aff(tbl[i - 1], p);
-    Jac acc = jac_inf();
+// k * P with signed 4-bit digits: k' = k + 0x88..8 (64 nibbles of 8) gives k = sum (nib_i(k') - 8) 16^i
+// + carry * 16^64, digits in [-8, 7] read most-significant first; table 1P..8P, negation by -y
+SECP_FN Jac mul_var(const U256& k, const Aff& p) {
+    Jac tbl[8];
+    tbl[0] = jac_from_aff(p);
+    for (int i = 1; i < 8; ++i) tbl[i] = jac_add_aff(tbl[i - 1], p);
+    U256 eights, kp;
+    for (int i = 0; i < 8; ++i) eights.v[i] = 0x88888888u;
+    const uint32_t top = u_add(kp, k, eights);
+    Jac acc = top ? tbl[0] : jac_inf();
     for (int w = 63; w >= 0; --w) {
         if (!acc.inf) { acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); }
-        uint32_t d = u_nibble(k, (uint32_t)w);
-        if (d) acc = jac_add(acc, tbl[d]);
+        const int d = (int)u_nibble(kp, (uint32_t)w) - 8;
+        if (d != 0) {
+            Jac t = tbl[(d > 0 ? d : -d) - 1];
+            if (d < 0) t.y = fe_neg(t.y);
+            acc = jac_add(acc, t);
+        }
     }
     return acc;
 }
 
 // ------------------------------------------------------------------------------ SHA-256 / HMAC
-BFT_FN uint32_t ror32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+SECP_FN uint32_t ror32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 BFT_FN void sha256_compress(uint32_t st[8], const uint32_t blk[16]) {
     const uint32_t K[64] = {
         0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
@@ -491,7 +528,7 @@ BFT_FN void sha256_compress(uint32_t st[8], const uint32_t blk[16]) {
     }
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
-BFT_FN void sha256_init(uint32_t st[8]) {
+SECP_FN void sha256_init(uint32_t st[8]) {
     st[0] = 0x6a09e667u; st[1] = 0xbb67ae85u; st[2] = 0x3c6ef372u; st[3] = 0xa54ff53au;
     st[4] = 0x510e527fu; st[5] = 0x9b05688cu; st[6] = 0x1f83d9abu; st[7] = 0x5be0cd19u;
 }
@@ -500,15 +537,15 @@ struct Sha256 {
     uint32_t st[8];
     uint32_t blk[16];
     uint32_t nbytes;
-    BFT_FN void init() { sha256_init(st); nbytes = 0; for (int i = 0; i < 16; ++i) blk[i] = 0; }
-    BFT_FN void byte(uint32_t b) {
+    SECP_FN void init() { sha256_init(st); nbytes = 0; for (int i = 0; i < 16; ++i) blk[i] = 0; }
+    SECP_FN void byte(uint32_t b) {
         uint32_t pos = nbytes & 63u;
         uint32_t sh = 24u - 8u * (pos & 3u);
         blk[pos >> 2] = (pos & 3u) == 0 ? (b << sh) : (blk[pos >> 2] | (b << sh));
         ++nbytes;
         if ((nbytes & 63u) == 0) sha256_compress(st, blk);
     }
-    BFT_FN void words(const uint32_t* w, int n) {       // n big-endian words (byte-aligned or not)
+    SECP_FN void words(const uint32_t* w, int n) {       // n big-endian words (byte-aligned or not)
         for (int i = 0; i < n; ++i) {
             if ((nbytes & 3u) == 0) {
                 blk[(nbytes & 63u) >> 2] = w[i];
@@ -519,7 +556,7 @@ struct Sha256 {
             }
         }
     }
-    BFT_FN void final(uint32_t out[8]) {
+    SECP_FN void final(uint32_t out[8]) {
         uint64_t bits = (uint64_t)nbytes * 8u;
         byte(0x80u);
         while ((nbytes & 63u) != 56u) byte(0);
@@ -555,7 +592,7 @@ BFT_FN void hmac_kv(const uint32_t key[8], const uint32_t v[8], int sep, const u
 struct Rfc6979 {
     uint32_t K[8], V[8];
     bool retry;
-    BFT_FN void init(const U256& d, const U256& e_mod_n) {
+    SECP_FN void init(const U256& d, const U256& e_mod_n) {
         uint32_t kd[16];
         for (int i = 0; i < 8; ++i) { kd[i] = d.v[7 - i]; kd[8 + i] = e_mod_n.v[7 - i]; }
         for (int i = 0; i < 8; ++i) { V[i] = 0x01010101u; K[i] = 0; }
@@ -570,7 +607,7 @@ struct Rfc6979 {
         for (int i = 0; i < 8; ++i) V[i] = t[i];
         retry = false;
     }
-    BFT_FN U256 next() {
+    SECP_FN U256 next() {
         uint32_t t[8];
         if (retry) {
             hmac_kv(K, V, 0x00, nullptr, t);
@@ -589,7 +626,7 @@ struct Rfc6979 {
 
 // ------------------------------------------------------------------------------ Keccak address
 // public_to_address: Keccak-256(X || Y)[12:32] (X, Y big-endian 32 bytes each)
-BFT_FN void pub_address(const Aff& q, uint8_t addr[20]) {
+SECP_FN void pub_address(const Aff& q, uint8_t addr[20]) {
     uint8_t pub[64];
     u_to_be(q.x, pub);
     u_to_be(q.y, pub + 32);
@@ -608,13 +645,13 @@ BFT_FN void pub_address(const Aff& q, uint8_t addr[20]) {
 
 // ------------------------------------------------------------------------------ ECDSA
 // secret -> public key; false for an invalid secret (0 or >= n)
-BFT_FN bool secret_to_pub(const uint8_t* sec32, const Aff* gtab, Aff& q) {
+SECP_FN bool secret_to_pub(const uint8_t* sec32, const Aff* gtab, Aff& q) {
     U256 d = u_from_be(sec32);
     if (u_is_zero(d) || u_ge(d, c_n())) return false;
     return jac_to_aff(mul_g(d, gtab), q);
 }
 // recoverable signature r || s || recid of a 32-byte digest (libsecp256k1 ecdsa_sign_recoverable)
-BFT_FN bool sign(const uint8_t* sec32, const uint8_t* msg32, const Aff* gtab, uint8_t sig[65]) {
+SECP_FN bool sign(const uint8_t* sec32, const uint8_t* msg32, const Aff* gtab, uint8_t sig[65]) {
     U256 d = u_from_be(sec32);
     if (u_is_zero(d) || u_ge(d, c_n())) return false;
     U256 e = sc_from_u256(u_from_be(msg32));
@@ -639,7 +676,7 @@ BFT_FN bool sign(const uint8_t* sec32, const uint8_t* msg32, const Aff* gtab, ui
     return false;
 }
 // public key of a recoverable signature (libsecp256k1 ecdsa_recover); false if invalid
-BFT_FN bool recover(const uint8_t* msg32, const uint8_t* sig65, const Aff* gtab, Aff& q) {
+SECP_FN bool recover(const uint8_t* msg32, const uint8_t* sig65, const Aff* gtab, Aff& q) {
     U256 r = u_from_be(sig65), s = u_from_be(sig65 + 32);
     uint32_t recid = sig65[64];
     if (recid > 3u || u_is_zero(r) || u_is_zero(s) || u_ge(r, c_n()) || u_ge(s, c_n())) return false;
