@@ -13,6 +13,10 @@ Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the roofline mode
 131,072 instances per GPU (1,048,576 on 8 GPUs), windowed rows (bftsim_set_window) with in-kernel
 hashes; the rounds-to-commit and commit-latency histograms are all-reduced over RCCL and printed.
 One step takes ~11 s on one MI355X: run it with --steps 1 --warmup 0.
+
+`--workload sig` measures the real-crypto row (not the headline): one step =
+secp256k1 public-key recovery (`GossipMessage::address`, src/protocol/mod.rs:103-116) of a batch of
+262,144 signed 32-byte digests per GPU resident in HBM (libbftsig, include/bftsig.h).
 """
 from __future__ import annotations
 
@@ -80,7 +84,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=("cfg3", "cfg5"), default="cfg3")
+    ap.add_argument("--workload", choices=("cfg3", "cfg5", "sig"), default="cfg3")
     ap.add_argument("--instances", type=int, default=None, help="instances per GPU")
     ap.add_argument("--heights", type=int, default=None)
     ap.add_argument("--window", type=int, default=256, help="cfg5: canonical rows kept per instance")
@@ -89,6 +93,8 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each step's block-hash pass on the launch stream (no overlap across steps)")
     args = ap.parse_args()
+    if args.workload == "sig":
+        return main_sig(args)
 
     import torch
     import torch.distributed as dist
@@ -225,6 +231,98 @@ def main():
                 out["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(out), flush=True)
     sim.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+METRIC_SIG = "secp256k1 public-key recoveries/sec (whole node), GossipMessage::address; bit-exact"
+# 32x32->64 multiply-adds of one recovery, counted on the host build of the same source
+# (tests/sig_lib.counts(): 1478.65 fe_mul x 73 + 2240.8 fe_sqr x 45 + 66 sc_mul x 134 + 253 sc_sqr x 106)
+SIG_RECOVER_MADS = 244_439
+MAD_PEAK = 256 * 32 * 2.4e9             # v_mad_u64_u32 per s: quarter rate (build/mad_peak measured 1.963e13)
+
+
+def sig_cpu_baseline(digs, sigs, sample: int, threads: int):
+    """The C oracle (oracle/secp_oracle.c: 64-bit limbs, double-and-add) on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    t = time.perf_counter()
+    _, ok = O.secp_recover_batch(digs[:sample], sigs[:sample], threads)
+    secs = time.perf_counter() - t
+    assert ok.all()
+    return dict(value=sample / secs, unit="recoveries/s", cores=threads, kind="port",
+                sample=f"{sample} recoveries of the same batch by the C oracle on {threads} threads, {secs:.1f} s")
+
+
+def main_sig(args):
+    import torch
+    import torch.distributed as dist
+    from bftsim.sig import Signer
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    n = args.instances or 262_144
+    keys = 64
+    g = torch.Generator().manual_seed(1000 + rank)       # each rank its own shard of messages
+    secs = torch.randint(0, 256, (keys, 32), dtype=torch.uint8, generator=g)
+    secs[:, 0] &= 0x7f
+    digs = torch.randint(0, 256, (n, 32), dtype=torch.uint8, generator=g).to(dev)
+    kidx = (torch.arange(n, dtype=torch.int32) % keys).to(dev)
+    sg = Signer(local)
+    sigs, ok = sg.sign(secs.to(dev), digs, key_index=kidx)
+    assert bool((ok == 1).all())
+    _, kaddr, _ = sg.secret_to_address(secs.to(dev))
+    want = kaddr[kidx.long()]
+    for _ in range(args.warmup):
+        sg.recover(digs, sigs, want_pub=False)
+    _, addr, ok = sg.recover(digs, sigs, want_pub=False)
+    assert bool((ok == 1).all()) and bool((addr == want).all()), "recovery mismatch"
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record()
+        sg.recover(digs, sigs, want_pub=False)
+        e1.record()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    tmax = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    dt = float(tmax.item())
+    kms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    if rank == 0:
+        achieved = SIG_RECOVER_MADS * n / (kms / 1e3) / 1e12
+        out = {
+            "metric": METRIC_SIG, "value": n * world * args.steps / dt, "unit": "recoveries/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * dt / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (seeded secrets and digests; signatures made by bftsig_sign)",
+            "config": {"workload": f"sig: {n} recoverable signatures per GPU (64 signers), recover + address",
+                       "batch_per_gpu": n, "parallelism": f"batch-sharded x{world}"},
+            "roofline": {"bound": "valu", "kernel": "sig_recover_kernel", "achieved": achieved,
+                         "peak": MAD_PEAK / 1e12, "unit": "T mad_u64_u32/s", "frac": achieved / (MAD_PEAK / 1e12),
+                         "traffic": None, "kernel_ms": kms,
+                         "ops_model": f"{SIG_RECOVER_MADS} 32x32->64 multiply-adds per recovery (host-counted)"},
+        }
+        if not args.no_cpu:
+            try:
+                d, s_ = digs.cpu().numpy(), sigs.cpu().numpy()
+                out["cpu_baseline"] = sig_cpu_baseline(d, s_, args.cpu_sample or 65536, min(16, os.cpu_count() or 1))
+            except Exception as e:
+                out["cpu_baseline"] = {"error": str(e)}
+        print(json.dumps(out), flush=True)
+    sg.close()
     if world > 1:
         dist.destroy_process_group()
 

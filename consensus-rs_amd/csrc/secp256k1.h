@@ -24,6 +24,13 @@ namespace secp {
 // Everything on the arithmetic path is forced inline: an out-of-line call passes its by-reference
 // points through scratch memory and spills the callee-saved VGPRs (measured: 2.5 KB scratch per lane).
 #define SECP_FN __attribute__((always_inline)) BFT_FN
+// host test builds count the multiplications of one operation (the roofline's work model)
+#ifdef SECP_COUNT_OPS
+extern uint64_t secp_op_count[4];      // fe_mul, fe_sqr, sc_mul, sc_sqr
+#define SECP_COUNT(k) (++secp_op_count[k])
+#else
+#define SECP_COUNT(k) ((void)0)
+#endif
 
 struct U256 {
     uint32_t v[8];
@@ -192,11 +199,13 @@ SECP_FN U256 fe_reduce_wide(const uint32_t t[16]) {
     return br ? r : s;
 }
 SECP_FN U256 fe_mul(const U256& a, const U256& b) {
+    SECP_COUNT(0);
     uint32_t t[16];
     u_mul_wide(t, a, b);
     return fe_reduce_wide(t);
 }
 SECP_FN U256 fe_sqr(const U256& a) {
+    SECP_COUNT(1);
     uint32_t t[16];
     u_sqr_wide(t, a);
     return fe_reduce_wide(t);
@@ -293,11 +302,13 @@ SECP_FN U256 sc_reduce_wide(const uint32_t t[16]) {
     return r;
 }
 SECP_FN U256 sc_mul(const U256& a, const U256& b) {
+    SECP_COUNT(2);
     uint32_t t[16];
     u_mul_wide(t, a, b);
     return sc_reduce_wide(t);
 }
 SECP_FN U256 sc_sqr(const U256& a) {
+    SECP_COUNT(3);
     uint32_t t[16];
     u_sqr_wide(t, a);
     return sc_reduce_wide(t);

@@ -6,7 +6,10 @@
 
 #include <vector>
 
+#define SECP_COUNT_OPS
 #include "../../consensus-rs_amd/csrc/secp256k1.h"
+
+uint64_t bft::secp::secp_op_count[4];
 
 using namespace bft::secp;
 
@@ -20,6 +23,10 @@ static std::vector<Aff>& gtab() {
 }
 
 extern "C" {
+// multiplications since the last call (fe_mul, fe_sqr, sc_mul, sc_sqr)
+void sig_host_counts(uint64_t out[4]) {
+    for (int i = 0; i < 4; ++i) { out[i] = secp_op_count[i]; secp_op_count[i] = 0; }
+}
 // field / scalar primitives on big-endian 32-byte operands (op: 0 fe_mul, 1 fe_sqr, 2 fe_add, 3 fe_sub,
 // 4 fe_inv, 5 fe_sqrt, 6 sc_mul, 7 sc_inv, 8 sc_add, 9 sc_neg)
 void sig_host_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {

@@ -167,3 +167,28 @@ def keccak256(data: bytes) -> bytes:
     o = (ctypes.c_uint8 * 32)()
     lib().orc_keccak256(data, len(data), o)
     return bytes(o)
+
+
+def secp_pubkey(secret: bytes):
+    """C oracle (oracle/secp_oracle.c): 64-byte public key or None."""
+    out = (ctypes.c_uint8 * 64)()
+    return bytes(out) if lib().orc_secp_pubkey(secret, out) else None
+
+
+def secp_recover(msg: bytes, sig: bytes):
+    out = (ctypes.c_uint8 * 64)()
+    return bytes(out) if lib().orc_secp_recover(msg, sig, out) else None
+
+
+def secp_recover_batch(msgs: np.ndarray, sigs: np.ndarray, threads: int = 1):
+    """[n,32] digests, [n,65] signatures -> ([n,64] public keys, [n] ok) on `threads` threads."""
+    msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+    sigs = np.ascontiguousarray(sigs, dtype=np.uint8)
+    n = msgs.shape[0]
+    pubs = np.zeros((n, 64), dtype=np.uint8)
+    ok = np.zeros(n, dtype=np.uint8)
+    L = lib()
+    L.orc_secp_recover_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_int]
+    L.orc_secp_recover_batch(msgs.ctypes.data, sigs.ctypes.data, n, pubs.ctypes.data, ok.ctypes.data, threads)
+    return pubs, ok

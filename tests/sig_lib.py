@@ -69,3 +69,10 @@ def sign(secret: bytes, msg: bytes):
 def recover(msg: bytes, sig: bytes):
     p, a = (ctypes.c_uint8 * 64)(), (ctypes.c_uint8 * 20)()
     return (bytes(p), bytes(a)) if lib().sig_host_recover(msg, sig, p, a) else None
+
+
+def counts():
+    """(fe_mul, fe_sqr, sc_mul, sc_sqr) executed since the previous call."""
+    out = (ctypes.c_uint64 * 4)()
+    lib().sig_host_counts(out)
+    return tuple(out)

@@ -115,3 +115,23 @@ def test_full_batch_round_trip(signer):
     assert not bool(signer.verify_address(want, d2, sig).any())
     for i in (0, 12345, n - 1):                        # spot checks against the oracle
         assert bytes(s[i]) == S.sign(bytes(secs[i % keys].numpy()), bytes(digs[i].numpy()))
+
+
+def test_recover_matches_c_oracle_4096(signer):
+    """4,096 recoveries with random recovery ids (about half do not recover, or recover another key):
+    GPU and the C oracle (oracle/secp_oracle.c, an independent implementation) agree item by item."""
+    import torch
+    g = torch.Generator().manual_seed(17)
+    n, keys = 4096, 32
+    secs = torch.randint(0, 256, (keys, 32), dtype=torch.uint8, generator=g)
+    secs[:, 0] &= 0x7f
+    digs = torch.randint(0, 256, (n, 32), dtype=torch.uint8, generator=g)
+    sig, ok = signer.sign(secs, digs, key_index=torch.arange(n, dtype=torch.int32) % keys)
+    assert bool((ok == 1).all())
+    s = sig.cpu().numpy().copy()
+    s[:, 64] = torch.randint(0, 4, (n,), generator=g).numpy()
+    pub, _, ok = signer.recover(digs, s)
+    want, wok = O.secp_recover_batch(digs.numpy(), s, threads=16)
+    assert (ok.cpu().numpy() == wok).all()
+    assert (pub.cpu().numpy()[wok == 1] == want[wok == 1]).all()
+    assert (pub.cpu().numpy()[wok == 0] == 0).all()
