@@ -17,6 +17,10 @@ One step takes ~11 s on one MI355X: run it with --steps 1 --warmup 0.
 `--workload sig` measures the real-crypto row (not the headline): one step =
 secp256k1 public-key recovery (`GossipMessage::address`, src/protocol/mod.rs:103-116) of a batch of
 262,144 signed 32-byte digests per GPU resident in HBM (libbftsig, include/bftsig.h).
+
+`--workload wire` measures the wire-codec row: one step = encode (frames + sign
+digest + message hash) and decode of 262,144 Prepare / Commit / RoundChange messages per GPU
+(libbftwire, include/bftwire.h).
 """
 from __future__ import annotations
 
@@ -84,7 +88,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=("cfg3", "cfg5", "sig"), default="cfg3")
+    ap.add_argument("--workload", choices=("cfg3", "cfg5", "sig", "wire"), default="cfg3")
     ap.add_argument("--instances", type=int, default=None, help="instances per GPU")
     ap.add_argument("--heights", type=int, default=None)
     ap.add_argument("--window", type=int, default=256, help="cfg5: canonical rows kept per instance")
@@ -95,6 +99,8 @@ def main():
     args = ap.parse_args()
     if args.workload == "sig":
         return main_sig(args)
+    if args.workload == "wire":
+        return main_wire(args)
 
     import torch
     import torch.distributed as dist
@@ -325,6 +331,120 @@ def main_sig(args):
     sg.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+METRIC_WIRE = "consensus wire messages/sec (whole node): encode + 2 Keccak digests + decode; bit-exact"
+
+
+def wire_algo_bytes(frame_bytes: int, n: int, n_commit: int) -> int:
+    """Algorithmic HBM bytes of one encode + decode step: the input fields read (code 1, round /
+    height / create_time / ttl / raw_time 5x8, digest 32, signature 65, seal 65 for Commits), the
+    frames written, the two 32-byte digests written, the frames read back and the fields written."""
+    fields = n * (1 + 40 + 32 + 65) + n_commit * 65
+    return 2 * fields + 2 * frame_bytes + 64 * n + 8 * (n + 1) * 2
+
+
+def main_wire(args):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from bftsim.wire import Codec
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    n = args.instances or 262_144
+    rng = np.random.default_rng(2000 + rank)
+    code = rng.choice(np.array([2, 3, 4], dtype=np.uint8), n)          # Prepare / Commit / RoundChange
+    batch = {"code": code, "round": rng.integers(0, 4, n), "height": rng.integers(1, 1 << 20, n),
+             "digest": rng.integers(0, 256, (n, 32), dtype=np.uint8),
+             "create_time": 1536517089000 + rng.integers(0, 1 << 30, n),
+             "signature": rng.integers(0, 256, (n, 65), dtype=np.uint8),
+             "commit_seal": rng.integers(0, 256, (n, 65), dtype=np.uint8)}
+    cd = Codec(local)
+    b = {k: cd._t(v, torch.uint8 if v.dtype == np.uint8 else torch.int64) for k, v in batch.items()}
+    cap = n * 1028
+    out, offs, sd, mh, ok = cd.encode(b, cap=cap)
+    assert bool((ok == 1).all())
+    total = int(offs[-1])
+    fields, ok2 = cd.decode(out, offs)
+    assert bool((ok2 == 1).all()) and torch.equal(fields["digest"], b["digest"])
+
+    def step():
+        o, f, _, _, _ = cd.encode(b, cap=cap)
+        cd.decode(o, f)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record()
+        step()
+        e1.record()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    tmax = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    dt = float(tmax.item())
+    kms = sum(a.elapsed_time(c) for a, c in evs) / len(evs)
+    if rank == 0:
+        algo = wire_algo_bytes(total, n, int((code == 3).sum()))
+        achieved = algo / (kms / 1e3) / 1e9
+        out_j = {
+            "metric": METRIC_WIRE, "value": n * world * args.steps / dt, "unit": "messages/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * dt / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (seeded Prepare/Commit/RoundChange fields, random 65-byte signatures and seals)",
+            "config": {"workload": f"wire: {n} messages per GPU, encode (frames + sign digest + message hash) "
+                                   f"+ decode", "batch_per_gpu": n, "frame_bytes": total,
+                       "parallelism": f"batch-sharded x{world}"},
+            "roofline": {"bound": "hbm", "kernel": "bftwire encode+decode (encode, scan, pack, hash, decode)",
+                         "achieved": achieved, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                         "frac": achieved / (HBM_PEAK / 1e9), "traffic": None, "kernel_ms": kms,
+                         "algorithmic_bytes_per_step": algo},
+        }
+        if not args.no_cpu:
+            try:
+                out_j["cpu_baseline"] = wire_cpu_baseline(batch, args.cpu_sample or 20000)
+            except Exception as e:
+                out_j["cpu_baseline"] = {"error": str(e)}
+        print(json.dumps(out_j), flush=True)
+    cd.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def wire_cpu_baseline(batch, sample: int):
+    """The msgpack oracle (oracle/wire_ref.py: encode + both Keccak digests + decode) on one core."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    import wire_ref as R
+    msgs = [dict(code=int(batch["code"][i]), round=int(batch["round"][i]), height=int(batch["height"][i]),
+                 digest=bytes(batch["digest"][i]), create_time=int(batch["create_time"][i]),
+                 signature=bytes(batch["signature"][i]),
+                 commit_seal=bytes(batch["commit_seal"][i]) if batch["code"][i] == 3 else None,
+                 raw_time=int(batch["create_time"][i])) for i in range(sample)]
+    t = time.perf_counter()
+    for m in msgs:
+        f, g, sp = R.encode(m)
+        O.keccak256(g)
+        O.keccak256(sp)
+        R.decode(f)
+    secs = time.perf_counter() - t
+    return dict(value=sample / secs, unit="messages/s", cores=1, kind="port",
+                sample=f"{sample} messages through the msgpack oracle on 1 core, {secs:.1f} s")
 
 
 if __name__ == "__main__":

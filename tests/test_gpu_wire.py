@@ -1,0 +1,136 @@
+"""Consensus wire codec on the GPU through the C ABI (include/bftwire.h): frames, sign digests and message
+hashes bit-exact against the msgpack-based oracle (oracle/wire_ref.py) and the oracle's Keccak; decode
+against the oracle's decoder; at full batch size the encode -> split -> decode round trip."""
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "consensus-rs_amd"))
+import wire_ref as R  # noqa: E402
+import oracle_lib as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+EDGE = [0, 1, 127, 128, 255, 256, 65535, 65536, 2 ** 32 - 1, 2 ** 32, 2 ** 63, 2 ** 64 - 1]
+
+
+@pytest.fixture(scope="module")
+def codec():
+    from bftsim.wire import Codec
+    c = Codec(0)
+    yield c
+    c.close()
+
+
+def make_batch(n, seed, sig=True, seal=True, edge=True):
+    rng = np.random.default_rng(seed)
+    code = rng.choice(np.array([2, 3, 4], dtype=np.uint8), n)
+    u = lambda hi: rng.integers(0, hi, n, dtype=np.uint64)   # noqa: E731
+    rnd, height, ctime = u(4), u(1 << 20) + 1, u(1 << 41)
+    if edge:
+        e = np.array(EDGE, dtype=np.uint64)
+        rnd[: len(e)], height[: len(e)], ctime[-len(e):] = e, e[::-1], e
+    b = dict(code=code, round=rnd.view(np.int64), height=height.view(np.int64),
+             digest=rng.integers(0, 256, (n, 32), dtype=np.uint8), create_time=ctime.view(np.int64),
+             ttl=np.full(n, 10, dtype=np.int64), raw_time=(ctime + np.uint64(7)).view(np.int64))
+    if sig:
+        b["signature"] = rng.integers(0, 256, (n, 65), dtype=np.uint8)
+    if seal:
+        b["commit_seal"] = rng.integers(0, 256, (n, 65), dtype=np.uint8)
+    return b
+
+
+def oracle_msg(b, i):
+    code = int(b["code"][i])
+    return dict(code=code, round=int(b["round"][i].view(np.uint64)), height=int(b["height"][i].view(np.uint64)),
+                digest=bytes(b["digest"][i]), create_time=int(b["create_time"][i].view(np.uint64)),
+                signature=bytes(b["signature"][i]) if "signature" in b else None,
+                commit_seal=bytes(b["commit_seal"][i]) if ("commit_seal" in b and code == 3) else None,
+                ttl=int(b["ttl"][i]), raw_time=int(b["raw_time"][i].view(np.uint64)))
+
+
+@pytest.mark.parametrize("sig,seal", [(True, True), (False, True), (True, False), (False, False)])
+def test_encode_matches_oracle(codec, sig, seal):
+    n = 700
+    b = make_batch(n, 11 + 2 * sig + seal, sig, seal)
+    out, offs, sd, mh, ok = codec.encode(b)
+    out, offs, sd, mh = out.cpu().numpy(), offs.cpu().numpy(), sd.cpu().numpy(), mh.cpu().numpy()
+    assert (ok.cpu().numpy() == 1).all()
+    for i in range(n):
+        m = oracle_msg(b, i)
+        f, g, sp = R.encode(m)
+        assert bytes(out[offs[i]:offs[i + 1]]) == f, i
+        assert bytes(mh[i]) == O.keccak256(g), i
+        assert bytes(sd[i]) == O.keccak256(sp), i
+    assert offs[0] == 0 and offs[n] == sum(len(R.encode(oracle_msg(b, i))[0]) for i in range(n))
+
+
+def test_decode_matches_oracle_and_rejects_malformed(codec):
+    n = 500
+    b = make_batch(n, 5)
+    stream, offs, _, _, ok = codec.encode(b, hashes=False)
+    s = bytearray(stream.cpu().numpy()[: int(offs[-1])].tobytes())
+    o = offs.cpu().numpy()
+    rng = random.Random(2)
+    broken = set(rng.sample(range(n), 40))
+    for i in broken:                      # corrupt one byte inside the frame
+        j = int(o[i]) + rng.randrange(4, int(o[i + 1] - o[i]))
+        s[j] ^= 1 << rng.randrange(8)
+    out, ok = codec.decode(np.frombuffer(bytes(s), np.uint8), o.astype(np.int64))
+    ok = ok.cpu().numpy()
+    fields = {k: v.cpu().numpy() for k, v in out.items()}
+    for i in range(n):
+        want = R.decode(bytes(s[o[i]:o[i + 1]]))
+        assert ok[i] == (want is not None), i
+        if want is None:
+            assert fields["code"][i] == 0 and not fields["digest"][i].any()
+            continue
+        assert fields["code"][i] == want["code"] and bytes(fields["digest"][i]) == want["digest"]
+        assert int(fields["round"][i].view(np.uint64)) == want["round"]
+        assert int(fields["height"][i].view(np.uint64)) == want["height"]
+        assert int(fields["create_time"][i].view(np.uint64)) == want["create_time"]
+        assert int(fields["raw_time"][i].view(np.uint64)) == want["raw_time"] and fields["ttl"][i] == want["ttl"]
+        assert (bytes(fields["signature"][i]) if fields["has_sig"][i] else None) == want["signature"]
+        assert (bytes(fields["commit_seal"][i]) if fields["has_seal"][i] else None) == want["commit_seal"]
+
+
+def test_invalid_codes_and_capacity(codec):
+    n = 64
+    b = make_batch(n, 9)
+    b["code"][[3, 10]] = [1, 7]          # Preprepare (out of scope) and an unknown code
+    out, offs, sd, mh, ok = codec.encode(b, cap=20 * 1028)
+    ok, offs = ok.cpu().numpy(), offs.cpu().numpy()
+    assert ok[3] == 0 and ok[10] == 0 and offs[4] == offs[3] and offs[11] == offs[10]
+    assert not sd.cpu().numpy()[3].any()
+    fits = offs[1:] <= 20 * 1028
+    good = np.array([i not in (3, 10) for i in range(n)])
+    assert (ok == (fits & good)).all()
+
+
+def test_full_batch_round_trip(codec):
+    """262,144 messages (16 heights of prepare + commit traffic of a 16,384-instance cfg3 batch would be
+    far more; this is one GPU's bench batch): encode -> host split_frames -> decode returns the input."""
+    import torch
+    from bftsim import wire
+    n = 262_144
+    b = make_batch(n, 1)
+    stream, offs, sd, mh, ok = codec.encode(b)
+    assert bool((ok == 1).all())
+    total = int(offs[-1])
+    host = stream[:total].cpu().numpy()
+    split = wire.split_frames(host, max_frames=n)
+    assert np.array_equal(split.astype(np.int64), offs.cpu().numpy())
+    out, ok2 = codec.decode(stream[:total], offs)
+    assert bool((ok2 == 1).all())
+    for k in ("code", "round", "height", "create_time", "ttl", "raw_time", "digest", "signature"):
+        assert torch.equal(out[k].cpu(), torch.from_numpy(np.ascontiguousarray(b[k])).to(out[k].dtype)), k
+    is_commit = torch.from_numpy(b["code"] == 3)
+    assert torch.equal(out["has_seal"].cpu().bool(), is_commit)
+    assert torch.equal(out["commit_seal"].cpu()[is_commit], torch.from_numpy(b["commit_seal"])[is_commit])
+    for i in (0, 77777, n - 1):                              # digests against the oracle
+        f, g, sp = R.encode(oracle_msg(b, i))
+        assert bytes(sd[i].cpu().numpy()) == O.keccak256(sp) and bytes(mh[i].cpu().numpy()) == O.keccak256(g)
