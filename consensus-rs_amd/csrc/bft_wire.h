@@ -209,13 +209,10 @@ struct Decoded {
     uint8_t peer[MAX_PEER];
 };
 
-// one frame (size prefix included, `len` bytes available) -> fields; false if malformed, not a
-// Consensus RawMessage, not a Subject-carrying GossipMessage, or with trailing bytes
-BFT_FN bool decode_frame(const uint8_t* f, uint32_t len, Decoded& d) {
-    if (len < 4) return false;
-    uint32_t body = ((uint32_t)f[0] << 24) | ((uint32_t)f[1] << 16) | ((uint32_t)f[2] << 8) | f[3];
-    if (body != len - 4u) return false;
-    Mem m{f + 4, body, 0};
+// a RawMessage body -> fields; false if malformed, not a Consensus RawMessage, not a
+// Subject-carrying GossipMessage, or with trailing bytes
+template <class M>
+BFT_FN bool decode_body(M& m, Decoded& d) {
     uint32_t n, idx;
     if (!rd_arr(m, n) || n != 2 || !rd_arr(m, n) || n != 4) return false;
     if (!rd_unit_variant(m, idx) || idx != P2P_CONSENSUS) return false;
@@ -236,14 +233,14 @@ BFT_FN bool decode_frame(const uint8_t* f, uint32_t len, Decoded& d) {
     // payload: the GossipMessage bytes, one array element each
     uint32_t glen;
     if (!rd_arr(m, glen)) return false;
-    Arr<Mem> g{&m, glen, false};
+    Arr<M> g{&m, glen, false};
     if (!rd_arr(g, n) || n != 5) return false;
     if (!rd_unit_variant(g, idx) || idx < 1 || idx > 3) return false;     // Prepare, Commit, RoundChange
     d.code = idx + 1u;
     if (!rd_uint(g, d.create_time)) return false;
     uint32_t slen;
     if (!rd_arr(g, slen)) return false;
-    Arr<Arr<Mem>> s{&g, slen, false};
+    Arr<Arr<M>> s{&g, slen, false};
     if (!rd_arr(s, n) || n != 2 || !rd_arr(s, n) || n != 2) return false;
     if (!rd_uint(s, d.round) || !rd_uint(s, d.height)) return false;
     if (!rd_bytes_fixed(s, 32, d.digest)) return false;
@@ -252,6 +249,15 @@ BFT_FN bool decode_frame(const uint8_t* f, uint32_t len, Decoded& d) {
     if (!rd_opt_bytes(g, 65, d.seal, d.has_seal)) return false;
     if (g.left != 0 || g.bad) return false;
     return m.i == m.n;
+}
+BFT_FN uint32_t frame_size(const uint8_t* f) {
+    return ((uint32_t)f[0] << 24) | ((uint32_t)f[1] << 16) | ((uint32_t)f[2] << 8) | f[3];
+}
+// one frame (size prefix included, `len` bytes available) -> fields
+BFT_FN bool decode_frame(const uint8_t* f, uint32_t len, Decoded& d) {
+    if (len < 4 || frame_size(f) != len - 4u) return false;
+    Mem m{f + 4, len - 4u, 0};
+    return decode_body(m, d);
 }
 
 }  // namespace wire

@@ -134,3 +134,69 @@ def test_full_batch_round_trip(codec):
     for i in (0, 77777, n - 1):                              # digests against the oracle
         f, g, sp = R.encode(oracle_msg(b, i))
         assert bytes(sd[i].cpu().numpy()) == O.keccak256(sp) and bytes(mh[i].cpu().numpy()) == O.keccak256(g)
+
+
+def _frame_with_wide_element(g: bytes, idx: int, tag: int, pad: int = 0) -> bytes:
+    """A Consensus frame whose payload encodes element idx of G non-canonically (0xcd/0xce/0xcf with
+    `pad` in the leading bytes): MessagePack decoders accept it when pad == 0 (the value still fits u8)."""
+    import msgpack
+    import struct
+    width = {0xcd: 2, 0xce: 4, 0xcf: 8}[tag]
+    els = bytearray()
+    for j, x in enumerate(g):
+        if j == idx:
+            els += bytes([tag, pad]) + bytes(width - 2) + bytes([x])
+        else:
+            els += msgpack.packb(x)
+    hdr = b"\xdc" + struct.pack(">H", len(g)) if len(g) < 65536 else b"\xdd" + struct.pack(">I", len(g))
+    body = b"\x92" + msgpack.packb([[4, []], 10, 0, None]) + hdr + bytes(els)
+    return struct.pack(">I", len(body)) + body
+
+
+def test_wave_and_lane_decoders_agree_on_hostile_frames(monkeypatch):
+    """The lane decoder (product) and the wave-cooperative decoder (BFTWIRE_DECODE=wave) agree
+    with the oracle on non-canonical integer encodings, wide padding, bit flips and truncations."""
+    from bftsim.wire import Codec
+    rng = random.Random(12)
+    b = make_batch(64, 21)
+    frames = []
+    for i in range(64):
+        m = oracle_msg(b, i)
+        f, g, _ = R.encode(m)
+        kind = i % 8
+        if kind == 1:
+            f = _frame_with_wide_element(g, rng.randrange(len(g)), rng.choice([0xcd, 0xce, 0xcf]))
+        elif kind == 2:
+            f = _frame_with_wide_element(g, rng.randrange(len(g)), rng.choice([0xcd, 0xce, 0xcf]), pad=1)
+        elif kind == 3:
+            f = bytearray(f)
+            f[rng.randrange(4, len(f))] ^= 1 << rng.randrange(8)
+            f = bytes(f)
+        elif kind == 4:
+            cut = rng.randrange(5, len(f))
+            f = struct_size(f[4:cut]) + f[4:cut]
+        frames.append(f)
+    stream = b"".join(frames)
+    offs = np.cumsum([0] + [len(f) for f in frames]).astype(np.int64)
+    results = []
+    for mode in ("wave", "lane"):          # "lane" is any value but "wave"
+        monkeypatch.setenv("BFTWIRE_DECODE", mode)
+        c = Codec(0)
+        out, ok = c.decode(np.frombuffer(stream, np.uint8), offs)
+        results.append(({k: v.cpu().numpy() for k, v in out.items()}, ok.cpu().numpy()))
+        c.close()
+    (fw, okw), (fl, okl) = results
+    assert (okw == okl).all()
+    for k in fw:
+        assert np.array_equal(fw[k], fl[k]), k
+    for i, f in enumerate(frames):
+        want = R.decode(f)
+        assert okw[i] == (want is not None), (i, i % 8)
+        if want is not None:
+            assert bytes(fw["digest"][i]) == want["digest"] and fw["code"][i] == want["code"]
+    assert okw[1::8].all() and not okw[2::8].any()
+
+
+def struct_size(body: bytes) -> bytes:
+    import struct
+    return struct.pack(">I", len(body))
