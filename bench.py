@@ -243,8 +243,9 @@ def main():
 
 METRIC_SIG = "secp256k1 public-key recoveries/sec (whole node), GossipMessage::address; bit-exact"
 # 32x32->64 multiply-adds of one recovery, counted on the host build of the same source
-# (tests/sig_lib.counts(): 1478.65 fe_mul x 73 + 2240.8 fe_sqr x 45 + 66 sc_mul x 134 + 253 sc_sqr x 106)
-SIG_RECOVER_MADS = 244_439
+# (tests/sig_lib.counts(): 1224 fe_mul x 73 + 1584.8 fe_sqr x 45 + 69 sc_mul x 134 + 253 sc_sqr x 106;
+# GLV split: 128 doublings)
+SIG_RECOVER_MADS = 196_732
 MAD_PEAK = 256 * 32 * 2.4e9             # v_mad_u64_u32 per s: quarter rate (build/mad_peak measured 1.963e13)
 
 

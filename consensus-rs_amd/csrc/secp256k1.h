@@ -13,7 +13,7 @@
 // mod p = 2^256 - 2^32 - 977 kept fully reduced; products by 32x32->64 multiply-adds
 // (v_mad_u64_u32) and the special-form reduction 2^256 = 2^32 + 977 (mod p). Points in Jacobian
 // coordinates (a = 0 formulas); k*G through a fixed-base table of 32 windows x 255 affine points
-// (8-bit windows, 510 KB, L2-resident), k*R through signed 4-bit digits. Written once as host+device code
+// (8-bit windows, 510 KB, L2-resident), k*R through the GLV split and signed 4-bit digits. Written once as host+device code
 // (BFT_FN): the same source runs on the GPU and, host-compiled, in the CPU tests.
 #pragma once
 #include "bft_common.h"
@@ -480,22 +480,70 @@ SECP_FN Jac mul_g(const U256& k, const Aff* gtab) {
     }
     return acc;
 }
-// k * P with signed 4-bit digits: k' = k + 0x88..8 (64 nibbles of 8) gives k = sum (nib_i(k') - 8) 16^i
-// + carry * 16^64, digits in [-8, 7] read most-significant first; table 1P..8P, negation by -y
+// GLV endomorphism (secp256k1 has lambda * (x, y) = (beta * x, y)): k = k1 + k2 * lambda (mod n) with
+// |k1|, |k2| < 2^128 (libsecp256k1's lattice constants; checked in tests/test_sig_cpu.py), so
+// k * P = k1 * P + k2 * (lambda P) takes 128 doublings instead of 256.
+SECP_FN U256 c_lambda() { return U256{{0x1B23BD72u, 0xDF02967Cu, 0x20816678u, 0x122E22EAu, 0x8812645Au, 0xA5261C02u, 0xC05C30E0u, 0x5363AD4Cu}}; }
+SECP_FN U256 c_beta() { return U256{{0x719501EEu, 0xC1396C28u, 0x12F58995u, 0x9CF04975u, 0xAC3434E9u, 0x6E64479Eu, 0x657C0710u, 0x7AE96A2Bu}}; }
+SECP_FN U256 c_g1() { return U256{{0x45DBB031u, 0xE893209Au, 0x71E8CA7Fu, 0x3DAA8A14u, 0x9284EB15u, 0xE86C90E4u, 0xA7D46BCDu, 0x3086D221u}}; }
+SECP_FN U256 c_g2() { return U256{{0x8AC47F71u, 0x1571B4AEu, 0x9DF506C6u, 0x221208ACu, 0x0ABFE4C4u, 0x6F547FA9u, 0x010E8828u, 0xE4437ED6u}}; }
+SECP_FN U256 c_mb1() { return U256{{0x0ABFE4C3u, 0x6F547FA9u, 0x010E8828u, 0xE4437ED6u, 0u, 0u, 0u, 0u}}; }
+SECP_FN U256 c_mb2() { return U256{{0x3DB1562Cu, 0xD765CDA8u, 0x0774346Du, 0x8A280AC5u, 0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}}; }
+// round(k * g / 2^384)
+SECP_FN U256 mul_shift_384(const U256& k, const U256& g) {
+    uint32_t t[16];
+    u_mul_wide(t, k, g);
+    U256 r = u_zero();
+    uint64_t c = (uint64_t)(t[11] >> 31);
+    for (int i = 0; i < 4; ++i) { c += t[12 + i]; r.v[i] = (uint32_t)c; c >>= 32; }
+    r.v[4] = (uint32_t)c;
+    return r;
+}
+SECP_FN void split_lambda(const U256& k, U256& r1, U256& r2) {
+    const U256 c1 = mul_shift_384(k, c_g1()), c2 = mul_shift_384(k, c_g2());
+    r2 = sc_add(sc_mul(c1, c_mb1()), sc_mul(c2, c_mb2()));
+    r1 = sc_add(k, sc_neg(sc_mul(r2, c_lambda())));
+}
+// k * P: GLV split, then signed 4-bit digits of both 128-bit halves (k' = k + 0x88..8, 32 nibbles) in
+// one doubling chain; table 1P..8P (Jacobian), the lambda table derived on the fly as (beta X, +-Y, Z)
 SECP_FN Jac mul_var(const U256& k, const Aff& p) {
+    U256 k1, k2;
+    split_lambda(k, k1, k2);
+    const bool n1 = !u_ge(c_nhalf(), k1), n2 = !u_ge(c_nhalf(), k2);
+    if (n1) k1 = sc_neg(k1);
+    if (n2) k2 = sc_neg(k2);
+    Aff q = p;
+    if (n1) q.y = fe_neg(q.y);
+    const bool flip2 = n1 != n2;                 // lambda table = lambda * (i q), negated when the signs differ
     Jac tbl[8];
-    tbl[0] = jac_from_aff(p);
-    for (int i = 1; i < 8; ++i) tbl[i] = jac_add_aff(tbl[i - 1], p);
-    U256 eights, kp;
-    for (int i = 0; i < 8; ++i) eights.v[i] = 0x88888888u;
-    const uint32_t top = u_add(kp, k, eights);
-    Jac acc = top ? tbl[0] : jac_inf();
-    for (int w = 63; w >= 0; --w) {
+    tbl[0] = jac_from_aff(q);
+    for (int i = 1; i < 8; ++i) tbl[i] = jac_add_aff(tbl[i - 1], q);
+    U256 eights = u_zero(), k1p, k2p;
+    for (int i = 0; i < 4; ++i) eights.v[i] = 0x88888888u;
+    u_add(k1p, k1, eights);
+    u_add(k2p, k2, eights);
+    const U256 beta = c_beta();
+    Jac acc = jac_inf();
+    if (k1p.v[4] & 1u) acc = jac_add(acc, tbl[0]);
+    if (k2p.v[4] & 1u) {
+        Jac t = tbl[0];
+        t.x = fe_mul(t.x, beta);
+        if (flip2) t.y = fe_neg(t.y);
+        acc = jac_add(acc, t);
+    }
+    for (int w = 31; w >= 0; --w) {
         if (!acc.inf) { acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); }
-        const int d = (int)u_nibble(kp, (uint32_t)w) - 8;
-        if (d != 0) {
-            Jac t = tbl[(d > 0 ? d : -d) - 1];
-            if (d < 0) t.y = fe_neg(t.y);
+        const int d1 = (int)u_nibble(k1p, (uint32_t)w) - 8;
+        if (d1 != 0) {
+            Jac t = tbl[(d1 > 0 ? d1 : -d1) - 1];
+            if (d1 < 0) t.y = fe_neg(t.y);
+            acc = jac_add(acc, t);
+        }
+        const int d2 = (int)u_nibble(k2p, (uint32_t)w) - 8;
+        if (d2 != 0) {
+            Jac t = tbl[(d2 > 0 ? d2 : -d2) - 1];
+            t.x = fe_mul(t.x, beta);
+            if ((d2 < 0) != flip2) t.y = fe_neg(t.y);
             acc = jac_add(acc, t);
         }
     }

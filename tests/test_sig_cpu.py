@@ -144,3 +144,15 @@ def test_c_oracle_matches_python_oracle():
     for i in range(len(msgs)):
         want = S.recover(msgs[i], sigs[i])
         assert bool(ok[i]) == (want is not None) and (want is None or bytes(pubs[i]) == want)
+
+
+def test_glv_mul_var_edge_scalars():
+    """k*P through the GLV split (secp256k1.h mul_var) at scalars where the split or the signed digits
+    hit their edges: 1, n-1, n/2, lambda, n-lambda, 2^128 +- 1, all-ones nibbles."""
+    lam = 0x5363AD4CC05C30E0A5261C028812645A122E22EA20816678DF02967C1B23BD72
+    pub = S.pubkey((12345).to_bytes(32, "big"))
+    P = (int.from_bytes(pub[:32], "big"), int.from_bytes(pub[32:], "big"))
+    for k in (1, 2, 15, 16, 17, S.N - 1, S.N - 2, S.N // 2, S.N // 2 + 1, lam, S.N - lam, 2 ** 128 - 1, 2 ** 128,
+              2 ** 128 + 1, int("7" * 64, 16), int("8" * 63, 16), (lam * 3) % S.N):
+        q = S.point_mul(k, P)
+        assert H.mul_var(k, pub) == q[0].to_bytes(32, "big") + q[1].to_bytes(32, "big"), hex(k)
