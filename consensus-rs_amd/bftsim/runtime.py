@@ -15,6 +15,7 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("BFTSIM_LIB") or os.path.join(PKG_DIR, "build", "libbftsim.so")
 
 _lib = None
+HEADER_SLOT = 288                       # BFTSIM_HEADER_SLOT (include/bftsim.h)
 
 
 class BftsimError(RuntimeError):
@@ -54,6 +55,7 @@ def lib():
         L.bftsim_keccak256.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p]
         L.bftsim_genesis_hash.argtypes = [ctypes.POINTER(_abi.CConfig), ctypes.c_void_p]
         L.bftsim_view_cmp.argtypes = [ctypes.c_uint64] * 4
+        L.bftsim_export_headers.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -145,6 +147,18 @@ class Simulator:
         r, arrs = _abi.alloc_result(n, self.cfg.heights)
         _check(self.h, lib().bftsim_fetch(self.h, ctypes.byref(r)), "bftsim_fetch")
         return _abi.shape_result(arrs, n, self.cfg.heights)
+
+    def export_headers(self, n: int):
+        """Ledger export of the last run / launch (core/ledger.rs:193-245): ([n, H] list of the Header
+        bytes of every committed height, empty beyond it). Keccak-256 of each is its block hash."""
+        H = self.cfg.heights
+        slot = HEADER_SLOT
+        buf = np.zeros(n * H * slot, np.uint8)
+        lens = np.zeros(n * H, np.uint32)
+        _check(self.h, lib().bftsim_export_headers(self.h, buf.ctypes.data, lens.ctypes.data), "bftsim_export_headers")
+        buf = buf.reshape(n, H, slot)
+        lens = lens.reshape(n, H)
+        return [[bytes(buf[i, x, :lens[i, x]]) for x in range(H)] for i in range(n)]
 
     def sync(self):
         _check(self.h, lib().bftsim_sync(self.h), "bftsim_sync")

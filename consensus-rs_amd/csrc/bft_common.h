@@ -502,11 +502,10 @@ struct HdrWriter {
     }
 };
 
-// Header of block (x, prop, var) with parent hash `prev` (8 LE words) at `time`, into wb; returns
-// the number of rate blocks (2 or 3). Field order = Header declaration order (types/block.rs:16-36).
-BFT_FN uint32_t header_words(uint64_t* wb, const uint32_t prev[8], const uint8_t* addr20, uint64_t seed,
-                             uint32_t inst, uint32_t h, uint32_t prop, uint32_t var, uint64_t time) {
-    HdrWriter w(wb);
+// The fields of the header of block (x, prop, var) with parent hash `prev` (8 LE words) at `time`.
+// Field order = Header declaration order (types/block.rs:16-36).
+BFT_FN void header_fields(HdrWriter& w, const uint32_t prev[8], const uint8_t* addr20, uint64_t seed,
+                          uint32_t inst, uint32_t h, uint32_t prop, uint32_t var, uint64_t time) {
     w.put(0x2000dc9dull, 4);                           // array(13); prev_hash: array16(32)
 #pragma unroll
     for (int i = 0; i < 8; ++i) w.put_hash_word(prev[i]);
@@ -526,7 +525,22 @@ BFT_FN uint32_t header_words(uint64_t* wb, const uint32_t prev[8], const uint8_t
     w.put_uint(time);
     w.put(0x2065736e696f439bull, 8);                   // extra = "Coinse base" (minner/mod.rs:113)
     w.put(0xc065736162ull, 5);                         //   ... + votes: None
+}
+// the header into wb, padded for Keccak; returns the number of rate blocks (2 or 3)
+BFT_FN uint32_t header_words(uint64_t* wb, const uint32_t prev[8], const uint8_t* addr20, uint64_t seed,
+                             uint32_t inst, uint32_t h, uint32_t prop, uint32_t var, uint64_t time) {
+    HdrWriter w(wb);
+    header_fields(w, prev, addr20, seed, inst, h, prop, var, time);
     return w.finish();
+}
+// the header bytes alone (the ledger's stored Header, votes None); returns their length
+BFT_FN uint32_t header_raw(uint64_t* wb, const uint32_t prev[8], const uint8_t* addr20, uint64_t seed,
+                           uint32_t inst, uint32_t h, uint32_t prop, uint32_t var, uint64_t time) {
+    HdrWriter w(wb);
+    header_fields(w, prev, addr20, seed, inst, h, prop, var, time);
+    const uint32_t len = 8u * w.wi + w.fill;
+    if (w.fill) wb[w.wi] = w.acc;
+    return len;
 }
 
 // Keccak-256 of a candidate header (SPEC.md §7) by ONE lane. `buf`: LANE_HASH_BUF bytes, 8-aligned

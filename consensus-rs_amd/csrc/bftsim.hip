@@ -331,6 +331,30 @@ __global__ __launch_bounds__(64) void bft_hash_pair_kernel(Params p) {
 #endif
 }
 
+// ledger export (core/ledger.rs:193-245): the Header bytes of every committed height, thread per
+// (instance, height), parent hash from the hash table; into 8-aligned BFTSIM_HEADER_SLOT-byte slots
+__global__ __launch_bounds__(256) void bft_export_kernel(Params p, uint8_t* out, uint32_t* lens) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint64_t H = p.heights;
+    if (t >= (uint64_t)p.n_instances * H) return;
+    const uint32_t il = (uint32_t)(t / H), x = (uint32_t)(t % H) + 1u;
+    if (x > p.committed_height[il]) { lens[t] = 0; return; }
+    uint32_t prev[8];
+    if (x == 1) {
+        for (int i = 0; i < 8; ++i)
+            prev[i] = (uint32_t)p.genesis_hash[4 * i] | ((uint32_t)p.genesis_hash[4 * i + 1] << 8) |
+                      ((uint32_t)p.genesis_hash[4 * i + 2] << 16) | ((uint32_t)p.genesis_hash[4 * i + 3] << 24);
+    } else {
+        const uint32_t* ph = (const uint32_t*)(p.hash + ((uint64_t)il * p.rows + (x - 1)) * 32);
+        for (int i = 0; i < 8; ++i) prev[i] = ph[i];
+    }
+    const uint32_t* row = p.rec + ((uint64_t)il * p.rows + x) * 4;
+    const uint32_t prop = row[1] & 0xffffu, var = (row[1] >> 16) & 1u;
+    const uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)row[2] + 1ull);
+    lens[t] = header_raw((uint64_t*)(out + t * BFTSIM_HEADER_SLOT), prev, p.addresses + 20u * prop, p.seed,
+                         p.first_instance + il, x, prop, var, time);
+}
+
 // totals: [0] instances [1] committed [2] views [3] ticks [4..10] flag counts (the histograms are
 // accumulated by the consensus kernel); block-level reduction in LDS, then one global atomic per
 // counter per block
@@ -809,6 +833,29 @@ int bftsim_fetch(bftsim_t* h, bftsim_result* out) {
         size_t tb = n * (size_t)h->trace_ticks * h->cfg.n * 8;
         HIPCHECK(h, hipMemcpy(h->h_trace, h->d_trace, tb, hipMemcpyDeviceToHost));
     }
+    return BFTSIM_OK;
+}
+
+int bftsim_export_headers(bftsim_t* h, uint8_t* hdr, uint32_t* hdr_len) {
+    if (!h || !hdr || !hdr_len) return BFTSIM_EINVAL;
+    if (h->window) return fail(h, BFTSIM_EINVAL, "windowed run: per-height rows are not kept");
+    if (h->last_n == 0) return fail(h, BFTSIM_EINVAL, "nothing launched");
+    if (int rc = sync_all(h)) return rc;
+    const uint64_t n = h->last_n, H = h->cfg.heights, cnt = n * H;
+    bft::Params p = make_params(h, h->last_first, n);
+    uint8_t* d_out = nullptr;
+    uint32_t* d_len = nullptr;
+    HIPCHECK(h, hipMalloc(&d_out, cnt * BFTSIM_HEADER_SLOT));
+    HIPCHECK(h, hipMalloc(&d_len, cnt * 4));
+    hipLaunchKernelGGL(bft::bft_export_kernel, dim3((uint32_t)((cnt + 255) / 256)), dim3(256), 0, h->last_stream, p,
+                       d_out, d_len);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(h->last_stream);
+    if (e == hipSuccess) e = hipMemcpy(hdr, d_out, cnt * BFTSIM_HEADER_SLOT, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(hdr_len, d_len, cnt * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d_out);
+    (void)hipFree(d_len);
+    if (e != hipSuccess) return fail(h, BFTSIM_EHIP, std::string("bftsim_export_headers: ") + hipGetErrorString(e));
     return BFTSIM_OK;
 }
 

@@ -131,6 +131,15 @@ void bftsim_keccak256(const uint8_t *data, size_t len, uint8_t out[32]);
 void bftsim_genesis_hash(const bftsim_config *cfg, uint8_t out[32]); /* core/genesis.rs:44-55 */
 int bftsim_view_cmp(uint64_t h1, uint64_t r1, uint64_t h2, uint64_t r2); /* consensus/types.rs:81-98 */
 
+/* Ledger export (core/ledger.rs:193-245 `add_block`: the `headers` map Hash -> Header of
+ * store/schema.rs:66-68; the `block_hashes_by_height` list is bftsim_result.block_hash): after a
+ * launch or run, the MessagePack Header bytes (SPEC.md §7, votes None: commit seals are not
+ * modelled) of every committed height of the last launch, host buffers:
+ * hdr[(i*H + x-1) * BFTSIM_HEADER_SLOT ...] with hdr_len[i*H + x-1] bytes (0 beyond the committed
+ * height); Keccak-256 of those bytes is that height's block hash. */
+#define BFTSIM_HEADER_SLOT 288
+int bftsim_export_headers(bftsim_t *h, uint8_t *hdr, uint32_t *hdr_len);
+
 #ifdef __cplusplus
 }
 #endif
