@@ -21,6 +21,11 @@ secp256k1 public-key recovery (`GossipMessage::address`, src/protocol/mod.rs:103
 `--workload wire` measures the wire-codec row: one step = encode (frames + sign
 digest + message hash) and decode of 262,144 Prepare / Commit / RoundChange messages per GPU
 (libbftwire, include/bftwire.h).
+
+`--workload msgpath` composes both rows into the reference's per-message path (sign per
+broadcast, decode + recover per received message): one step = 262,144 Prepare / Commit / RoundChange
+messages of 64 validators: sign digest, seal and signature (bftsig_sign), frames, then on the receiving
+side decode, sign-payload re-encode, recover and address check.
 """
 from __future__ import annotations
 
@@ -88,7 +93,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=("cfg3", "cfg5", "sig", "wire"), default="cfg3")
+    ap.add_argument("--workload", choices=("cfg3", "cfg5", "sig", "wire", "msgpath"), default="cfg3")
     ap.add_argument("--instances", type=int, default=None, help="instances per GPU")
     ap.add_argument("--heights", type=int, default=None)
     ap.add_argument("--window", type=int, default=256, help="cfg5: canonical rows kept per instance")
@@ -101,6 +106,8 @@ def main():
         return main_sig(args)
     if args.workload == "wire":
         return main_wire(args)
+    if args.workload == "msgpath":
+        return main_msgpath(args)
 
     import torch
     import torch.distributed as dist
@@ -446,6 +453,93 @@ def wire_cpu_baseline(batch, sample: int):
     secs = time.perf_counter() - t
     return dict(value=sample / secs, unit="messages/s", cores=1, kind="port",
                 sample=f"{sample} messages through the msgpack oracle on 1 core, {secs:.1f} s")
+
+
+METRIC_MSGPATH = ("consensus messages/sec through the per-message path (whole node): encode + sign digest + "
+                  "sign + frame | decode + re-encode + recover + address check; bit-exact")
+
+
+def main_msgpath(args):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from bftsim.sig import Signer
+    from bftsim.wire import Codec
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    n, n_val = args.instances or 262_144, 64
+    rng = np.random.default_rng(3000 + rank)
+    secs = torch.from_numpy(rng.integers(0, 128, (n_val, 32), dtype=np.uint8)).to(dev)
+    sender = torch.arange(n, dtype=torch.int32, device=dev) % n_val
+    batch = {"code": torch.from_numpy(rng.choice(np.array([2, 3, 4], dtype=np.uint8), n)).to(dev),
+             "round": torch.from_numpy(rng.integers(0, 4, n)).to(dev),
+             "height": torch.from_numpy(rng.integers(1, 1 << 20, n)).to(dev),
+             "digest": torch.from_numpy(rng.integers(0, 256, (n, 32), dtype=np.uint8)).to(dev),
+             "create_time": torch.from_numpy(1536517089000 + rng.integers(0, 1 << 30, n)).to(dev)}
+    sg, cd = Signer(local), Codec(local)
+    _, vaddr, _ = sg.secret_to_address(secs)
+    want = vaddr[sender.long()]
+
+    def step():
+        seal, _ = sg.sign(secs, batch["digest"], key_index=sender)          # commit seals (votes.rs:94-101)
+        b = {**batch, "commit_seal": seal}
+        _, _, sd, _, _ = cd.encode(b)                                        # sign digest (+ message hash)
+        sig, _ = sg.sign(secs, sd, key_index=sender)                         # set_sign
+        frames, offs, _, _, _ = cd.encode({**b, "signature": sig}, hashes=False)
+        dec, _ = cd.decode(frames, offs)                                     # receiver
+        rx = {k: dec[k] for k in ("code", "round", "height", "digest", "create_time", "commit_seal")}
+        _, _, sd_rx, _, _ = cd.encode(rx)
+        _, addr, ok = sg.recover(sd_rx, dec["signature"], want_pub=False)   # GossipMessage::address
+        return addr, ok
+    addr, ok = step()
+    assert bool((ok == 1).all()) and torch.equal(addr, want), "per-message path mismatch"
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(args.steps):
+        step()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    tmax = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    dt = float(tmax.item())
+    gpu_ms = e0.elapsed_time(e1) / args.steps
+    if rank == 0:
+        mads = 2 * 69_848 + SIG_RECOVER_MADS                # two signatures + one recovery per message
+        achieved = mads * n / (gpu_ms / 1e3) / 1e12
+        out = {
+            "metric": METRIC_MSGPATH, "value": n * world * args.steps / dt, "unit": "messages/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * dt / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (seeded validator keys, message fields and digests)",
+            "config": {"workload": f"msgpath: {n} messages per GPU from 64 validators, sender + receiver path",
+                       "batch_per_gpu": n, "parallelism": f"batch-sharded x{world}"},
+            "roofline": {"bound": "valu", "kernel": "sig_sign x2 + sig_recover + wire encode x3 + decode",
+                         "achieved": achieved, "peak": MAD_PEAK / 1e12, "unit": "T mad_u64_u32/s",
+                         "frac": achieved / (MAD_PEAK / 1e12), "traffic": None, "step_gpu_ms": gpu_ms,
+                         "ops_model": f"{mads} multiply-adds per message (2 signatures + 1 recovery)"},
+        }
+        print(json.dumps(out), flush=True)
+    sg.close()
+    cd.close()
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
