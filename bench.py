@@ -83,9 +83,31 @@ def cpu_baseline(cfg, sample: int, threads: int, name: str = "cfg3"):
         r = O.run(cfg, 0, sample, threads=threads)
         secs = r["seconds"]
     views = int(r["views"].sum())
-    return dict(value=views / secs, unit="instance-rounds/s", cores=threads, kind="port",
-                sample=f"{sample} {name} instances ({views} instance-rounds) on {threads} threads, "
-                       f"{secs:.1f} s")
+    out = dict(value=views / secs, unit="instance-rounds/s", cores=threads, kind="port",
+               sample=f"{sample} {name} instances ({views} instance-rounds) on {threads} threads, "
+                      f"{secs:.1f} s", host=host_cpu())
+    if name != "cfg5":                        # also the single-thread rate
+        s1 = max(1, sample // 16)
+        t1 = time.perf_counter()
+        r1 = O.run(cfg, 0, s1, threads=1)
+        t1 = time.perf_counter() - t1
+        v1 = int(r1["views"].sum())
+        out["single_thread"] = dict(value=v1 / t1, sample=f"{s1} instances on 1 thread, {t1:.2f} s")
+    return out
+
+
+def host_cpu() -> str:
+    """lscpu model name and the CPU count this process may use (SURVEY §8d asks for both)."""
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return f"{model} ({n} usable CPUs)"
 
 
 def main():
