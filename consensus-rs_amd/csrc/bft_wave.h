@@ -890,9 +890,15 @@ struct Sim {
         ps.k_pp = seg_bits(ballot((f & F_PP) != 0));
         ps.k_pr = seg_bits(ballot((f & F_PR) != 0));
         ps.k_cm = seg_bits(ballot((f & F_CM) != 0));
-        ps.k_ocm = seg_bits(ballot((f & F_OCM) != 0));
-        ps.k_rc = seg_bits(ballot((f & F_RC) != 0));
-        ps.k_sync = seg_bits(ballot((f & F_SYNC) != 0));
+        if constexpr (FAST) {
+            // these kinds always take the general path, which hands the instance over: one ballot
+            ps.k_ocm = seg_bits(ballot((f & (F_OCM | F_RC | F_SYNC)) != 0));
+            ps.k_rc = ps.k_sync = M::zero();
+        } else {
+            ps.k_ocm = seg_bits(ballot((f & F_OCM) != 0));
+            ps.k_rc = seg_bits(ballot((f & F_RC) != 0));
+            ps.k_sync = seg_bits(ballot((f & F_SYNC) != 0));
+        }
         ps.k_blk = seg_bits(ballot((f & F_BLK) != 0));
         const bool pr = (f & F_PR) != 0, cm = (f & F_CM) != 0, bk = (f & F_BLK) != 0, pq = (f & F_PP) != 0;
         const bool prw = (f & F_PR_W) != 0, cmw = (f & F_CM_W) != 0;
@@ -903,8 +909,11 @@ struct Sim {
         ps.pp_src = ps.pp_h = ps.pp_r = ps.pp_eq = 0;
         ps.pp_b = 0;
         // leader of each kind (the first sender of the segment) and uniformity against it
-        bool any_pr = ballot(pr).any(), any_cm = ballot(cm).any(), any_bk = ballot(bk).any();
-        bool any_pp = ballot(pq).any();
+        // (the wave-wide ballots equal the segment masks when the segment is the whole wave)
+        bool any_pr = S == 64 ? ps.k_pr.any() : ballot(pr).any();
+        bool any_cm = S == 64 ? ps.k_cm.any() : ballot(cm).any();
+        bool any_bk = S == 64 ? ps.k_blk.any() : ballot(bk).any();
+        bool any_pp = S == 64 ? ps.k_pp.any() : ballot(pq).any();
         bool mm_pr = false, mm_cm = false, mm_blk = false;
         if ((BFT_PP_PATH || FAST) && any_pp) {
             uint32_t j = ps.k_pp.any() ? ps.k_pp.ctz_nz() : 0u;
