@@ -721,6 +721,34 @@ struct Sim {
         bool c = commit_x != 0;
         M bal = ballot(c);
         if (bal.none()) return;
+        if constexpr (S == 64) {
+            // one instance per wave: the first committer's values by readlane, and when every committer
+            // commits that same height (the common case) the canonical update is computed by all lanes
+            // alike from uniform values — no LDS hand-off, no syncs; only the record stores are the
+            // leader's. Same results as the general hand-off below (which handles mixed heights).
+            const uint32_t lead = bal.ctz_nz();
+            const uint32_t x0 = wv.readlane(commit_x, lead);
+            const bool other_h = c && commit_x != x0;
+            if (!seg_done && ballot(other_h).none()) {
+                const uint64_t b0 = (uint64_t)wv.readlane((uint32_t)commit_blk, lead) |
+                                    ((uint64_t)wv.readlane((uint32_t)(commit_blk >> 32), lead) << 32);
+                const uint32_t r0 = wv.readlane(commit_round, lead), s0 = wv.readlane(commit_seed, lead);
+                const bool x0_known = x0 <= canon_h;
+                const uint64_t ref = x0_known ? canon_blk(x0) : b0;
+                const M badm = ballot(c && !blk_eq(commit_blk, ref));
+                bool fr = badm.any();
+                if (!x0_known && x0 < P.hcap && (!fr || badm.ctz() > lead)) {
+                    if (lane == lead)
+                        record_canon(x0, b0, r0, s0, (const uint32_t*)(lds + LDS_CHASH_OFF + lead * 32), canon_tick);
+                    views_acc += x0 <= P.heights ? (uint64_t)r0 + 1u : 0u;
+                    canon_h = x0; canon_tip = b0; canon_tip_seed = s0; canon_tick = (uint32_t)tick;
+                }
+                if (x0 >= P.hcap) fr = true;
+                if (fr) { frozen = true; seg_flags |= FLAG_SAFETY; }
+                commit_x = 0;
+                return;
+            }
+        }
         uint32_t* cm = (uint32_t*)(lds + LDS_CMT_OFF) + lane * LY::CMT_STRIDE;
         if (c) {
             cm[0] = commit_x; cm[1] = (uint32_t)commit_blk; cm[2] = (uint32_t)(commit_blk >> 32);

@@ -23,6 +23,9 @@ CASES = [
     ("n64-fast-handover-crash", lambda: BftConfig(n=64, heights=10, seed=22, drop_ppm=100_000,
                                                   proposer_crash_ppm=300_000), 0, 2),
     ("cfg4-n64", lambda: cfg4(64, heights=12), 0, 3),
+    # f >= N/3 equivocators at N = 64: forks freeze instances (the S = 64 commit resolution's safety path)
+    ("n64-byz32-fork", lambda: BftConfig(n=64, heights=12, seed=31, byz_count=32), 0, 4),
+    ("n64-byz40-drop5-fork", lambda: BftConfig(n=64, heights=12, seed=31, byz_count=40, drop_ppm=50_000), 0, 3),
     # workgroup segments (N > 64: 2 or 4 waves per instance, multi-word sender bitmaps)
     ("cfg4-n65", lambda: cfg4(65, heights=10), 5, 2),
     ("cfg4-n100", lambda: cfg4(100, heights=8), 0, 1),

@@ -28,6 +28,8 @@ CASES = [
     ("cfg3-tail", lambda: cfg3(), 16_300, 16),
     ("cfg5", lambda: cfg5(heights=300), 0, 64),
     ("n4-byz2-unsafe", lambda: BftConfig(n=4, heights=40, seed=9, byz_count=2), 0, 64),
+    ("n64-byz32-fork", lambda: BftConfig(n=64, heights=20, seed=31, byz_count=32), 0, 32),
+    ("n64-byz40-drop5-fork", lambda: BftConfig(n=64, heights=20, seed=31, byz_count=40, drop_ppm=50_000), 0, 16),
     ("n7-byz3-drop", lambda: BftConfig(n=7, heights=40, seed=9, byz_count=3, drop_ppm=100_000), 0, 64),
     ("n10-mix", lambda: BftConfig(n=10, heights=40, seed=11, byz_count=3, drop_ppm=200_000,
                                   proposer_crash_ppm=200_000), 0, 32),
