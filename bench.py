@@ -70,6 +70,23 @@ def pmc_traffic():
         os.path.relpath(files[-1], ROOT)
 
 
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2   # wave64 VALU instructions/s: one per 2 cycles per SIMD (SIMD-32)
+
+
+def pmc_issue():
+    """Per dispatch VALU / SALU wave-instructions of the FAST consensus kernel from the newest PMC
+    summary (SQ_INSTS_VALU, SQ_INSTS_SALU of scripts/gpu_profile.sh's SQ pass), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")))
+    if not files:
+        return None
+    k = json.load(open(files[-1])).get("kernels", {})
+    e = k.get("bft_consensus_fast_kernel") or k.get("bft_consensus_kernel") or {}
+    if "SQ_INSTS_VALU" not in e:
+        return None
+    return {"valu": e["SQ_INSTS_VALU"], "salu": e.get("SQ_INSTS_SALU")}
+
+
 def cpu_baseline(cfg, sample: int, threads: int, name: str = "cfg3"):
     """The C oracle (oracle/, a scalar restatement of the reference handlers) timed on this
     host's cores over a bounded sample of the same workload."""
@@ -250,6 +267,12 @@ def main():
                 "bound": "valu", "kernel": dom, "achieved": achieved, "peak": peak,
                 "unit": "Tops/s", "frac": achieved / peak,
                 "traffic": (traffic or {}).get(dom),
+                # what the hardware issues, beside the algorithmic model: VALU wave-instructions of
+                # the profiled launch (PMC) per second of this run's kernel time vs the issue peak
+                "issue": (lambda q: None if q is None or c5 or dom != "bft_consensus_kernel" else {
+                    "valu_wave_instr_per_launch": q["valu"], "salu_wave_instr_per_launch": q["salu"],
+                    "valu_per_s": q["valu"] / (ms / 1e3), "valu_peak_per_s": VALU_ISSUE_PEAK,
+                    "valu_frac": q["valu"] / (ms / 1e3) / VALU_ISSUE_PEAK})(pmc_issue()),
                 "traffic_source": traffic_src,
                 "hbm": {"algorithmic_bytes": algo_bytes, "achieved_GBps": algo_bytes / (ms / 1e3) / 1e9,
                         "peak_GBps": HBM_PEAK / 1e9, "frac": algo_bytes / (ms / 1e3) / HBM_PEAK},
