@@ -154,7 +154,8 @@ def _frame_with_wide_element(g: bytes, idx: int, tag: int, pad: int = 0) -> byte
 
 
 def test_wave_and_lane_decoders_agree_on_hostile_frames(monkeypatch):
-    """The lane decoder (product) and the wave-cooperative decoder (BFTWIRE_DECODE=wave) agree
+    """The lane decoder (product), the LDS-staged lane decoder (BFTWIRE_DECODE=lds) and the
+    wave-cooperative decoder (BFTWIRE_DECODE=wave) agree
     with the oracle on non-canonical integer encodings, wide padding, bit flips and truncations."""
     from bftsim.wire import Codec
     rng = random.Random(12)
@@ -179,16 +180,16 @@ def test_wave_and_lane_decoders_agree_on_hostile_frames(monkeypatch):
     stream = b"".join(frames)
     offs = np.cumsum([0] + [len(f) for f in frames]).astype(np.int64)
     results = []
-    for mode in ("wave", "lane"):          # "lane" is any value but "wave"
+    for mode in ("wave", "global", "lds"):     # "global" (any other value): the product decoder
         monkeypatch.setenv("BFTWIRE_DECODE", mode)
         c = Codec(0)
         out, ok = c.decode(np.frombuffer(stream, np.uint8), offs)
         results.append(({k: v.cpu().numpy() for k, v in out.items()}, ok.cpu().numpy()))
         c.close()
-    (fw, okw), (fl, okl) = results
-    assert (okw == okl).all()
+    (fw, okw), (fl, okl), (fs, oks) = results
+    assert (okw == okl).all() and (oks == okl).all()
     for k in fw:
-        assert np.array_equal(fw[k], fl[k]), k
+        assert np.array_equal(fw[k], fl[k]) and np.array_equal(fs[k], fl[k]), k
     for i, f in enumerate(frames):
         want = R.decode(f)
         assert okw[i] == (want is not None), (i, i % 8)
