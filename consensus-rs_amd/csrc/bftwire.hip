@@ -383,7 +383,7 @@ __global__ __launch_bounds__(64 * WAVES) void wire_decode_wave_kernel(const uint
     // GossipMessage header: [[code, []], create_time, msg array
     if (lane == 0 && good) {
         Mem m{G, glen, 0};
-        uint32_t nn, idx, slen = 0;
+        uint32_t nn = 0, idx = 0, slen = 0;
         bool g = rd_arr(m, nn) && nn == 5 && rd_unit_variant(m, idx) && idx >= 1 && idx <= 3 && rd_uint(m, sc.ctime) &&
                  rd_arr(m, slen) && slen <= MAX_S;
         sc.code = idx + 1u;
