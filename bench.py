@@ -87,28 +87,38 @@ def pmc_issue():
     return {"valu": e["SQ_INSTS_VALU"], "salu": e.get("SQ_INSTS_SALU")}
 
 
+def usable_cpus() -> int:
+    return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+
+
 def cpu_baseline(cfg, sample: int, threads: int, name: str = "cfg3"):
     """The C oracle (oracle/, a scalar restatement of the reference handlers) timed on this
-    host's cores over a bounded sample of the same workload."""
+    host's cores over a bounded sample of the same workload: every usable core (`value`),
+    beside a 16-thread and a single-thread rate."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    if name == "cfg5":
-        t = time.perf_counter()
-        r = O.run_stream(cfg, 0, sample, threads=threads)
-        secs = time.perf_counter() - t
-    else:
-        r = O.run(cfg, 0, sample, threads=threads)
-        secs = r["seconds"]
-    views = int(r["views"].sum())
+
+    def timed(n_inst, nthr):
+        if name == "cfg5":
+            t = time.perf_counter()
+            r = O.run_stream(cfg, 0, n_inst, threads=nthr)
+            secs = time.perf_counter() - t
+        else:
+            t = time.perf_counter()
+            r = O.run(cfg, 0, n_inst, threads=nthr)
+            secs = r["seconds"] if nthr > 1 else time.perf_counter() - t
+        return int(r["views"].sum()), secs
+
+    views, secs = timed(sample, threads)
     out = dict(value=views / secs, unit="instance-rounds/s", cores=threads, kind="port",
                sample=f"{sample} {name} instances ({views} instance-rounds) on {threads} threads, "
                       f"{secs:.1f} s", host=host_cpu())
+    if threads != 16:
+        v16, s16 = timed(sample, 16)
+        out["threads_16"] = dict(value=v16 / s16, sample=f"{sample} instances on 16 threads, {s16:.1f} s")
     if name != "cfg5":                        # SURVEY §8d: also the single-thread rate
-        s1 = max(1, sample // 16)
-        t1 = time.perf_counter()
-        r1 = O.run(cfg, 0, s1, threads=1)
-        t1 = time.perf_counter() - t1
-        v1 = int(r1["views"].sum())
+        s1 = max(1, sample // 64)
+        v1, t1 = timed(s1, 1)
         out["single_thread"] = dict(value=v1 / t1, sample=f"{s1} instances on 1 thread, {t1:.2f} s")
     return out
 
@@ -123,8 +133,7 @@ def host_cpu() -> str:
                 break
     except OSError:
         pass
-    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    return f"{model} ({n} usable CPUs)"
+    return f"{model} ({usable_cpus()} usable CPUs)"
 
 
 def main():
@@ -140,6 +149,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each step's block-hash pass on the launch stream (no overlap across steps)")
+    ap.add_argument("--seed-order", choices=("be", "le"), default="be",
+                    help="U128 byte order of randon_seed (validator.rs:39-48; include/bftsim.h BFTSIM_SEED_*)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: --instances per GPU; strong: --instances in total, split over the ranks "
+                         "(BASELINE configs[2]: 16,384 sharded over 1/2/4/8 GPUs)")
     args = ap.parse_args()
     if args.workload == "sig":
         return main_sig(args)
@@ -171,14 +185,21 @@ def main():
     torch.cuda.set_device(dev)
 
     cfg = cfg5(heights=args.heights) if c5 else cfg3(heights=args.heights)
+    if args.seed_order == "le":
+        import dataclasses
+        cfg = dataclasses.replace(cfg, seed_byte_order=1, name=cfg.name + "-le")
     sim = Simulator(cfg, device=local)
     pipelined = not c5 and not args.no_pipeline
     sim.set_pipeline(pipelined)
-    I = args.instances
+    if args.scaling == "strong":
+        from bftsim.distributed import strong_shard
+        first, I = strong_shard(rank, world, args.instances)
+    else:
+        I = args.instances
+        first = rank * I
     if c5:
         sim.set_window(args.window)
     sim.prepare(I)
-    first = rank * I
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     for _ in range(args.warmup):
@@ -221,7 +242,7 @@ def main():
         # dominant kernel by device time
         c_ops = consensus_ops_per_view(cfg.n) * views_rank
         h_ops = HEADER_HASH_OPS * st["committed_heights"]
-        if c5:                            # windowed runs hash inside the consensus kernel
+        if c5 or cfg.seed_byte_order:     # windowed runs / LE seeds hash inside the consensus kernel
             c_ops, h_ops = c_ops + h_ops, 0
         if cms >= hms:
             dom, ops, ms = "bft_consensus_kernel", c_ops, cms
@@ -245,7 +266,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (seeded Philox schedule, SPEC.md)",
@@ -253,8 +274,10 @@ def main():
                 "workload": (f"cfg5: {I} instances per GPU, N=7, 5% drop, {args.heights} heights, "
                              f"window {args.window}") if c5 else
                             (f"cfg3: {I} instances per GPU, N=64, f=21 equivocating, "
-                             f"{args.heights} heights"),
+                             f"{args.heights} heights" + (", little-endian U128 seeds" if cfg.seed_byte_order else "")),
                 "instances_per_gpu": I, "n_validators": cfg.n, "byzantine": cfg.byz_count,
+                "instances_total": args.instances if args.scaling == "strong" else args.instances * world,
+                "seed_byte_order": "le" if cfg.seed_byte_order else "be",
                 "heights": args.heights, "parallelism": f"instance-sharded x{world}",
                 "pipelined": pipelined,
                 "instance_rounds_per_step": views_all,
@@ -283,8 +306,7 @@ def main():
         }
         if not args.no_cpu:
             try:
-                threads = min(16, os.cpu_count() or 1)
-                out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample, threads, args.workload)
+                out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample, usable_cpus(), args.workload)
             except Exception as e:  # the baseline is reported, never the target
                 out["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(out), flush=True)

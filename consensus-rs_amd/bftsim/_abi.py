@@ -16,6 +16,8 @@ class CConfig(ctypes.Structure):
         ("proposer_crash_ppm", ctypes.c_uint32), ("phase_cap", ctypes.c_uint32),
         ("silent_mask", ctypes.c_uint64 * 4), ("addresses", ctypes.c_void_p),
         ("genesis_proposer", ctypes.c_uint8 * 20), ("genesis_gas_used", ctypes.c_uint64),
+        ("seed_byte_order", ctypes.c_uint32), ("header_encoding", ctypes.c_uint32),
+        ("backlog_mode", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
     ]
 
 
@@ -46,12 +48,15 @@ def to_cconfig(cfg: BftConfig):
     for i, b in enumerate(cfg.genesis_proposer):
         c.genesis_proposer[i] = b
     c.genesis_gas_used = cfg.genesis_gas_used
+    c.seed_byte_order = cfg.seed_byte_order
+    c.header_encoding = 0
+    c.backlog_mode = cfg.backlog_mode
     return c, addr
 
 
 def alloc_result(n_inst: int, heights: int):
     arrs = dict(
-        committed_height=np.zeros(n_inst, np.uint32), flags=np.zeros(n_inst, np.uint32),
+        committed_height=np.zeros(n_inst, np.uint64), flags=np.zeros(n_inst, np.uint32),
         ticks=np.zeros(n_inst, np.uint32), views=np.zeros(n_inst, np.uint64),
         round=np.zeros(n_inst * heights, np.uint16), proposer=np.zeros(n_inst * heights, np.uint16),
         variant=np.zeros(n_inst * heights, np.uint8), time_tick=np.zeros(n_inst * heights, np.uint32),

@@ -64,6 +64,11 @@ class BftConfig:
         default_factory=lambda: string_to_address(GENESIS_PROPOSER))
     genesis_gas_used: int = GENESIS_GAS_USED
     name: str = ""
+    # conventions the reference leaves to unvendored crates (include/bftsim.h BFTSIM_SEED_*):
+    # 0 = U128::from([u8;16]) big-endian (validator.rs:39-48 read as bigint's byte-slice order), 1 = LE
+    seed_byte_order: int = 0
+    # BackLogActor semantics (back_log.rs:38-91): 0 = reference (dropped), 1 = replay (SPEC.md §10)
+    backlog_mode: int = 0
 
     def __post_init__(self):
         if self.addresses is None:
@@ -74,6 +79,8 @@ class BftConfig:
             raise ValueError("addresses must be sorted ascending (validator index order)")
         if self.max_ticks == 0:
             self.max_ticks = 4 * self.heights + 64
+        if self.seed_byte_order not in (0, 1) or self.backlog_mode not in (0, 1):
+            raise ValueError("seed_byte_order / backlog_mode must be 0 or 1")
 
     @property
     def quorum(self) -> int:

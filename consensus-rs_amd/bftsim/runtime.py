@@ -49,6 +49,8 @@ def lib():
         L.bftsim_two_thirds_majority.restype = ctypes.c_uint32
         L.bftsim_seed_from_hash.restype = ctypes.c_uint32
         L.bftsim_seed_from_hash.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
+        L.bftsim_seed_from_hash_order.restype = ctypes.c_uint32
+        L.bftsim_seed_from_hash_order.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]
         L.bftsim_two_thirds_majority.argtypes = [ctypes.c_uint32]
         L.bftsim_calc_proposer.restype = ctypes.c_uint32
         L.bftsim_calc_proposer.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint64]
@@ -113,7 +115,7 @@ class Simulator:
         _check(self.h, lib().bftsim_set_window(self.h, window), "bftsim_set_window")
 
     def fetch_summary(self, n: int, tips: bool = True):
-        out = dict(committed_height=np.zeros(n, np.uint32), flags=np.zeros(n, np.uint32),
+        out = dict(committed_height=np.zeros(n, np.uint64), flags=np.zeros(n, np.uint32),
                    ticks=np.zeros(n, np.uint32), views=np.zeros(n, np.uint64))
         if tips:
             out["tip_hash"] = np.zeros((n, 32), np.uint8)

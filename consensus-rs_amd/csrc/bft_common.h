@@ -63,7 +63,9 @@ struct Params {
     uint32_t* save;                   // [n_inst * 64][SAVE_WORDS] per-lane state
     uint64_t save_stride;             // unused (kept for the layout)
     uint32_t resume_mode;             // CPU emulator only: run the MODE_RESUME body
-    uint32_t pad2;
+    uint32_t seed_le;                 // BFTSIM_SEED_LE: randon_seed reads U128 little-endian (bftsim.h)
+    uint32_t backlog_replay;          // BFTSIM_BACKLOG_REPLAY (SPEC.md §10)
+    uint32_t pad3;
 };
 
 // flags (same bits as the oracle)
@@ -73,6 +75,22 @@ constexpr uint32_t HIST_BINS = 130;      // [0,65) rounds-to-commit, [65,130) co
 
 // State (src/protocol/mod.rs:25-30)
 constexpr uint32_t ST_ACCEPT_REQUEST = 1, ST_PREPREPARED = 2, ST_PREPARED = 3, ST_COMMITTED = 4;
+
+// MessageType (src/protocol/mod.rs:36-41; ordered Preprepare < Prepare < Commit < RoundChange, the
+// derive(PartialOrd) the reference tests at :241-250) and the error classes of Core::check_message.
+constexpr int MT_PREPREPARE = 1, MT_PREPARE = 2, MT_COMMIT = 3, MT_ROUND_CHANGE = 4;
+constexpr int CM_OK = 0, CM_UNKNOWN = 1, CM_FUTURE_BLOCK = 2, CM_OLD = 3, CM_FUTURE_MSG = 4;
+// Core::check_message (core.rs:366-399): a message of `code` for height `vh` at a Core of height `h`
+// in state `st`. RoundChange compares only the height; the others need the same height, and in
+// AcceptRequest only a Preprepare (the smallest MessageType) is accepted. The round is not compared.
+BFT_FN int check_message_class(int code, uint32_t vh, uint32_t h, uint32_t st) {
+    if (vh == 0) return CM_UNKNOWN;
+    if (code == MT_ROUND_CHANGE) { if (vh > h) return CM_FUTURE_BLOCK; if (vh < h) return CM_OLD; return CM_OK; }
+    if (vh > h) return CM_FUTURE_BLOCK;
+    if (vh < h) return CM_OLD;
+    if (st == ST_ACCEPT_REQUEST) return code > MT_PREPREPARE ? CM_FUTURE_MSG : CM_OK;
+    return CM_OK;
+}
 
 // ---------------------------------------------------------------------------------------------
 // Block identity (SPEC.md §4) packed in 64 bits:
@@ -564,13 +582,26 @@ BFT_FN void lane_block_hash(uint8_t* buf, const uint32_t prev[8], const uint8_t*
     for (int i = 0; i < 4; ++i) { out[2 * i] = (uint32_t)a[i]; out[2 * i + 1] = (uint32_t)(a[i] >> 32); }
 }
 
-// randon_seed (validator.rs:39-48): (BE64(hash[0..8]) * 2^64) mod n
-BFT_FN uint32_t seed_from_hash(const uint8_t* h, uint32_t n) {
+// randon_seed (validator.rs:39-48): U128::from(hash[0..8] ++ 0^8) mod n. `le` selects how the
+// 16-byte buffer is read (bftsim.h BFTSIM_SEED_*): big-endian (BE64(hash[0..8]) * 2^64) mod n, or
+// little-endian LE64(hash[0..8]) mod n.
+BFT_FN uint32_t seed_from_hash(const uint8_t* h, uint32_t n, bool le = false) {
+    if (le) {
+        uint64_t v = 0;
+        for (int i = 7; i >= 0; --i) v = (v << 8) | h[i];
+        return (uint32_t)(v % n);
+    }
     uint64_t be = 0;
     for (int i = 0; i < 8; ++i) be = (be << 8) | h[i];
     uint64_t a = be % n;
     uint64_t t = (0xffffffffffffffffull % n + 1ull) % n;   // 2^64 mod n
     return (uint32_t)((a * t) % n);
+}
+// the same from the first two little-endian hash words (the kernels' register form)
+BFT_FN uint32_t seed_from_words(uint32_t w0, uint32_t w1, uint32_t n, bool le) {
+    uint8_t hb[8];
+    for (int q = 0; q < 4; ++q) { hb[q] = (uint8_t)(w0 >> (8 * q)); hb[4 + q] = (uint8_t)(w1 >> (8 * q)); }
+    return seed_from_hash(hb, n, le);
 }
 
 }  // namespace bft

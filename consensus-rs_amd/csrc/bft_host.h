@@ -80,7 +80,11 @@ inline Params params_from_config(const bftsim_config& c, uint32_t seg, uint32_t 
     p.crash_thr32 = (uint32_t)(((uint64_t)c.proposer_crash_ppm << 32) / 1000000u);
     p.crash_on = c.proposer_crash_ppm ? 1u : 0u;
     p.phase_cap = c.phase_cap;
-    p.need_seed = (c.n & (c.n - 1)) != 0 ? 1u : 0u;
+    // the next view's proposer depends on the committed block hash unless the seed is identically 0
+    // (big-endian U128 and a power-of-two N, SPEC.md §1)
+    p.seed_le = c.seed_byte_order == BFTSIM_SEED_LE ? 1u : 0u;
+    p.need_seed = ((c.n & (c.n - 1)) != 0 || (p.seed_le && c.n > 1)) ? 1u : 0u;
+    p.backlog_replay = c.backlog_mode == BFTSIM_BACKLOG_REPLAY ? 1u : 0u;
     for (int k = 0; k < 4; ++k) p.silent_mask[k] = c.silent_mask[k];
     p.first_instance = (uint32_t)first;
     p.n_instances = (uint32_t)n;

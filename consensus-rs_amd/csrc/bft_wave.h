@@ -357,11 +357,8 @@ struct Sim {
                                 P.seed, inst, x, blk_prop(b), blk_var(b), time, out);
             }
             uint32_t* hs = (uint32_t*)(lds + LDS_CHASH_OFF + lane * 32);
-            uint8_t hb[8];
             for (int i = 0; i < 8; ++i) hs[i] = out[i];
-            for (int i = 0; i < 2; ++i)
-                for (int q = 0; q < 4; ++q) hb[4 * i + q] = (uint8_t)(out[i] >> (8 * q));
-            sd = seed_from_hash(hb, nval());
+            sd = seed_from_words(out[0], out[1], nval(), P.seed_le != 0);
         }
         commit_seed = sd;
         last = x;
@@ -416,14 +413,7 @@ struct Sim {
     }   // proposer index
 
     // Core::check_message (core.rs:366-399): 0 ok, 1 unknown, 2 future block, 3 old, 4 future msg
-    BFT_FN int check_message(int code, uint32_t vh) const {
-        if (vh == 0) return 1;
-        if (code == 4) { if (vh > h) return 2; if (vh < h) return 3; return 0; }
-        if (vh > h) return 2;
-        if (vh < h) return 3;
-        if (st == ST_ACCEPT_REQUEST) return code > 1 ? 4 : 0;
-        return 0;
-    }
+    BFT_FN int check_message(int code, uint32_t vh) const { return check_message_class(code, vh, h, st); }
     BFT_FN void note_future_block(uint32_t vh) { if (vh > sync_pending) sync_pending = vh; }
     BFT_FN void lock_hash() { if (blk_valid(pp)) lock = pp; }               // round_state.rs:100-110
 

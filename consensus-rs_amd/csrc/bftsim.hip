@@ -425,6 +425,7 @@ struct bftsim {
     uint64_t* d_trace = nullptr;
     uint64_t* h_trace = nullptr;
     uint32_t trace_ticks = 0;
+    uint64_t n_req = 0;               // instances of the next launch (bftsim_prepare); <= cap_inst
     uint64_t last_n = 0, last_first = 0;
     hipStream_t last_stream = nullptr;
     // pipelined launches (bftsim_set_pipeline): two row-table sets used alternately, the hash pass of
@@ -469,6 +470,16 @@ static void free_bufs(bftsim* h) {
     h->d_ch = h->d_flags = h->d_ticks = nullptr; h->d_views = nullptr;
     h->d_rec = nullptr; h->d_hash = nullptr; h->d_trace = nullptr; h->d_tips = nullptr;
     h->cap_inst = 0;
+    h->n_req = 0;
+    h->last_n = 0;                    // nothing left to fetch: the buffers of the last launch are gone
+    h->last_first = 0;
+}
+
+static int sync_all(bftsim* h) {
+    HIPCHECK(h, hipSetDevice(h->device));
+    HIPCHECK(h, hipStreamSynchronize(h->last_stream));
+    if (h->hs) HIPCHECK(h, hipStreamSynchronize(h->hs));
+    return BFTSIM_OK;
 }
 
 #ifdef BFT_STAMPS
@@ -493,12 +504,20 @@ int bftsim_debug_stamps(uint64_t out[12]) {
 
 uint32_t bftsim_two_thirds_majority(uint32_t n) { return (2u * n) / 3u; }
 uint32_t bftsim_seed_from_hash(const uint8_t hash[32], uint32_t n) { return n ? bft::seed_from_hash(hash, n) : 0; }
+uint32_t bftsim_seed_from_hash_order(const uint8_t hash[32], uint32_t n, uint32_t order) {
+    return n ? bft::seed_from_hash(hash, n, order == BFTSIM_SEED_LE) : 0;
+}
 uint32_t bftsim_calc_proposer(const uint8_t prev_hash[32], uint32_t n, uint64_t round) {
     if (n == 0) return 0;
     return (uint32_t)(((uint64_t)bft::seed_from_hash(prev_hash, n) + round % n) % n);
 }
 void bftsim_keccak256(const uint8_t* data, size_t len, uint8_t out[32]) { host_keccak(data, len, out); }
 void bftsim_genesis_hash(const bftsim_config* cfg, uint8_t out[32]) { host_genesis_hash(cfg, out); }
+int bftsim_check_message(uint32_t code, uint64_t msg_height, uint64_t core_height, uint32_t state) {
+    if (code < 1 || code > 4 || state < 1 || state > 4 || msg_height >= (1ull << 32) || core_height >= (1ull << 32))
+        return BFTSIM_EINVAL;
+    return bft::check_message_class((int)code, (uint32_t)msg_height, (uint32_t)core_height, state);
+}
 int bftsim_view_cmp(uint64_t h1, uint64_t r1, uint64_t h2, uint64_t r2) {
     if (h1 != h2) return h1 < h2 ? -1 : 1;
     if (r1 != r2) return r1 < r2 ? -1 : 1;
@@ -516,13 +535,16 @@ int bftsim_create(const bftsim_config* cfg, int hip_device, bftsim_t** out) {
         return BFTSIM_EINVAL;
     for (uint32_t i = 1; i < cfg->n; ++i)
         if (memcmp(cfg->addresses + 20 * (i - 1), cfg->addresses + 20 * i, 20) >= 0) return BFTSIM_EINVAL;
+    if (cfg->seed_byte_order > BFTSIM_SEED_LE || cfg->header_encoding != BFTSIM_ENC_RMP_COMPACT ||
+        cfg->backlog_mode > BFTSIM_BACKLOG_REPLAY || cfg->reserved != 0)
+        return BFTSIM_EINVAL;
     bftsim* h = new bftsim();
     h->cfg = *cfg;
     h->addresses.assign(cfg->addresses, cfg->addresses + 20 * cfg->n);
     h->cfg.addresses = h->addresses.data();
     h->device = hip_device;
     host_genesis_hash(&h->cfg, h->genesis_hash);
-    h->genesis_seed = bft::seed_from_hash(h->genesis_hash, cfg->n);
+    h->genesis_seed = bft::seed_from_hash(h->genesis_hash, cfg->n, cfg->seed_byte_order == BFTSIM_SEED_LE);
     h->seg = bft::segment_size(cfg->n);
     h->hcap = cfg->heights + 64;
     {
@@ -567,7 +589,8 @@ void bftsim_destroy(bftsim_t* h) {
 int bftsim_prepare(bftsim_t* h, uint64_t n) {
     if (!h || n == 0 || n > (1ull << 31)) return fail(h, BFTSIM_EINVAL, "bad instance count");
     HIPCHECK(h, hipSetDevice(h->device));
-    if (n <= h->cap_inst) return BFTSIM_OK;
+    if (n <= h->cap_inst) { h->n_req = n; return BFTSIM_OK; }
+    if (h->last_n) if (int rc = sync_all(h)) return rc;   // the last launch may still use them
     free_bufs(h);
     HIPCHECK(h, hipMalloc(&h->d_ch, n * 4));
     HIPCHECK(h, hipMalloc(&h->d_flags, n * 4));
@@ -594,6 +617,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         HIPCHECK(h, hipMalloc(&h->alt_hash, n * h->hcap * 32));
     }
     h->cap_inst = n;
+    h->n_req = n;
     return BFTSIM_OK;
 }
 
@@ -640,8 +664,8 @@ static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
 }
 
 int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
-    if (!h || h->cap_inst == 0) return fail(h, BFTSIM_EINVAL, "bftsim_prepare not called");
-    uint64_t n = h->cap_inst;
+    if (!h || h->cap_inst == 0 || h->n_req == 0) return fail(h, BFTSIM_EINVAL, "bftsim_prepare not called");
+    const uint64_t n = h->n_req;
     if (first + n > (1ull << 32)) return fail(h, BFTSIM_EINVAL, "instance ids must fit in 32 bits");
     HIPCHECK(h, hipSetDevice(h->device));
     hipStream_t s = (hipStream_t)stream;
@@ -744,13 +768,6 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     return BFTSIM_OK;
 }
 
-static int sync_all(bftsim* h) {
-    HIPCHECK(h, hipSetDevice(h->device));
-    HIPCHECK(h, hipStreamSynchronize(h->last_stream));
-    if (h->hs) HIPCHECK(h, hipStreamSynchronize(h->hs));
-    return BFTSIM_OK;
-}
-
 int bftsim_set_pipeline(bftsim_t* h, int on) {
     if (!h) return BFTSIM_EINVAL;
     if ((on != 0) == (h->pipeline != 0)) return BFTSIM_OK;
@@ -803,11 +820,13 @@ int bftsim_last_kernel_ms(bftsim_t* h, float* cms, float* hms) {
 int bftsim_fetch(bftsim_t* h, bftsim_result* out) {
     if (!h || !out) return BFTSIM_EINVAL;
     if (h->window) return fail(h, BFTSIM_EINVAL, "windowed run: per-height rows are not kept (bftsim_fetch_summary)");
-    if (h->last_n == 0) return fail(h, BFTSIM_EINVAL, "nothing launched");
+    if (h->last_n == 0 || !h->d_ch) return fail(h, BFTSIM_EINVAL, "nothing launched");
     if (int rc = sync_all(h)) return rc;
     uint64_t n = h->last_n;
     uint32_t H = h->cfg.heights, hc = h->hcap;
-    HIPCHECK(h, hipMemcpy(out->committed_height, h->d_ch, n * 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> ch32(n);
+    HIPCHECK(h, hipMemcpy(ch32.data(), h->d_ch, n * 4, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < n; ++i) out->committed_height[i] = ch32[i];
     HIPCHECK(h, hipMemcpy(out->flags, h->d_flags, n * 4, hipMemcpyDeviceToHost));
     HIPCHECK(h, hipMemcpy(out->ticks, h->d_ticks, n * 4, hipMemcpyDeviceToHost));
     HIPCHECK(h, hipMemcpy(out->views, h->d_views, n * 8, hipMemcpyDeviceToHost));
@@ -839,7 +858,7 @@ int bftsim_fetch(bftsim_t* h, bftsim_result* out) {
 int bftsim_export_headers(bftsim_t* h, uint8_t* hdr, uint32_t* hdr_len) {
     if (!h || !hdr || !hdr_len) return BFTSIM_EINVAL;
     if (h->window) return fail(h, BFTSIM_EINVAL, "windowed run: per-height rows are not kept");
-    if (h->last_n == 0) return fail(h, BFTSIM_EINVAL, "nothing launched");
+    if (h->last_n == 0 || !h->d_ch) return fail(h, BFTSIM_EINVAL, "nothing launched");
     if (int rc = sync_all(h)) return rc;
     const uint64_t n = h->last_n, H = h->cfg.heights, cnt = n * H;
     bft::Params p = make_params(h, h->last_first, n);
@@ -862,17 +881,14 @@ int bftsim_export_headers(bftsim_t* h, uint8_t* hdr, uint32_t* hdr_len) {
 int bftsim_run(bftsim_t* h, uint64_t first, uint64_t n, bftsim_result* out) {
     int rc = bftsim_prepare(h, n);
     if (rc) return rc;
-    if (h->cap_inst != n) {          // exact-size buffers for a synchronous run
-        free_bufs(h);
-        if ((rc = bftsim_prepare(h, n))) return rc;
-    }
     if ((rc = bftsim_launch(h, first, nullptr))) return rc;
     return bftsim_fetch(h, out);
 }
 
-int bftsim_fetch_summary(bftsim_t* h, uint32_t* committed_height, uint32_t* flags, uint32_t* ticks,
+int bftsim_fetch_summary(bftsim_t* h, uint64_t* committed_height, uint32_t* flags, uint32_t* ticks,
                          uint64_t* views, uint8_t* tip_hash) {
-    if (!h || h->last_n == 0) return BFTSIM_EINVAL;
+    if (!h) return BFTSIM_EINVAL;
+    if (h->last_n == 0 || !h->d_ch) return fail(h, BFTSIM_EINVAL, "nothing launched");
     if (int rc = sync_all(h)) return rc;                // the hash pass may run on its own stream
     uint64_t n = h->last_n;
     if (tip_hash) {
@@ -882,7 +898,11 @@ int bftsim_fetch_summary(bftsim_t* h, uint32_t* committed_height, uint32_t* flag
         HIPCHECK(h, hipGetLastError());
     }
     HIPCHECK(h, hipStreamSynchronize(h->last_stream));
-    if (committed_height) HIPCHECK(h, hipMemcpy(committed_height, h->d_ch, n * 4, hipMemcpyDeviceToHost));
+    if (committed_height) {
+        std::vector<uint32_t> ch32(n);
+        HIPCHECK(h, hipMemcpy(ch32.data(), h->d_ch, n * 4, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < n; ++i) committed_height[i] = ch32[i];
+    }
     if (flags) HIPCHECK(h, hipMemcpy(flags, h->d_flags, n * 4, hipMemcpyDeviceToHost));
     if (ticks) HIPCHECK(h, hipMemcpy(ticks, h->d_ticks, n * 4, hipMemcpyDeviceToHost));
     if (views) HIPCHECK(h, hipMemcpy(views, h->d_views, n * 8, hipMemcpyDeviceToHost));
@@ -891,7 +911,8 @@ int bftsim_fetch_summary(bftsim_t* h, uint32_t* committed_height, uint32_t* flag
 }
 
 int bftsim_stats_get(bftsim_t* h, bftsim_stats* out) {
-    if (!h || !out || h->last_n == 0) return BFTSIM_EINVAL;
+    if (!h || !out) return BFTSIM_EINVAL;
+    if (h->last_n == 0 || !h->d_ch) return fail(h, BFTSIM_EINVAL, "nothing launched");
     HIPCHECK(h, hipSetDevice(h->device));
     bft::Params p = make_params(h, h->last_first, h->last_n);
     HIPCHECK(h, hipMemsetAsync(h->d_stats, 0, 16 * 8, h->last_stream));

@@ -43,6 +43,23 @@ extern "C" {
 #define BFTSIM_FLAG_RCS_OVERFLOW 32u /* more round-change rounds than the GPU table holds */
 #define BFTSIM_FLAG_WINDOW 64u       /* windowed run: a lookup older than the row ring (result unpinned) */
 
+/* Conventions the reference leaves to unvendored crates (SPEC.md §1, §7): they are
+ * parity-unpinned, so they are explicit switches here rather than silent assumptions.
+ *   seed_byte_order: how `U128::from(seed_buf)` reads the 16-byte buffer hash[0..8] ++ 0^8 in
+ *     randon_seed (src/consensus/validator.rs:39-48; `bigint = "4.4.1"`, Cargo.toml:16).
+ *     BE: seed = (BE64(hash[0..8]) * 2^64) mod N  (seed == 0 for every power-of-two N);
+ *     LE: seed = LE64(hash[0..8]) mod N           (every N needs the block hash in-kernel).
+ *   header_encoding: the StorageValue serialization of `Header` behind `hash()` (block.rs:76-80);
+ *     only the compact rmp-serde form of SPEC.md §7 exists today.
+ *   backlog_mode: what BackLogActor does with FutureMessage / FutureRoundMessage
+ *     (src/consensus/pbft/core/back_log.rs:38-91). DROP is the reference (stored, never re-delivered);
+ *     REPLAY is the opt-in liveness variant of SPEC.md §10 (not a parity target of the reference). */
+#define BFTSIM_SEED_BE 0u
+#define BFTSIM_SEED_LE 1u
+#define BFTSIM_ENC_RMP_COMPACT 0u
+#define BFTSIM_BACKLOG_DROP 0u
+#define BFTSIM_BACKLOG_REPLAY 1u
+
 typedef struct bftsim_config {
     uint32_t n;                  /* validators per instance: 1..256 */
     uint32_t heights;            /* stop once the canonical chain reaches this height */
@@ -58,10 +75,14 @@ typedef struct bftsim_config {
     const uint8_t *addresses;    /* n*20 bytes, ascending = validator index order */
     uint8_t genesis_proposer[20];
     uint64_t genesis_gas_used;
+    uint32_t seed_byte_order;    /* BFTSIM_SEED_BE (default) | BFTSIM_SEED_LE */
+    uint32_t header_encoding;    /* BFTSIM_ENC_RMP_COMPACT */
+    uint32_t backlog_mode;       /* BFTSIM_BACKLOG_DROP (reference) | BFTSIM_BACKLOG_REPLAY */
+    uint32_t reserved;           /* must be 0 */
 } bftsim_config;
 
 typedef struct bftsim_result {   /* host buffers, caller-owned; H = config.heights */
-    uint32_t *committed_height;  /* [n_inst] canonical chain length (<= H) */
+    uint64_t *committed_height;  /* [n_inst] canonical chain length (<= H) */
     uint32_t *flags;             /* [n_inst] */
     uint32_t *ticks;             /* [n_inst] ticks used */
     uint64_t *views;             /* [n_inst] instance-rounds: sum of (commit round + 1) */
@@ -120,16 +141,27 @@ int bftsim_set_trace(bftsim_t *h, uint64_t *host_out, uint32_t trace_ticks);
 int bftsim_set_window(bftsim_t *h, uint32_t window);
 /* per-instance outputs of the last launch (any pointer may be NULL); tip_hash[i*32..] = hash of
  * the block at committed_height[i] (the genesis hash at 0), which commits to the whole chain */
-int bftsim_fetch_summary(bftsim_t *h, uint32_t *committed_height, uint32_t *flags, uint32_t *ticks,
+int bftsim_fetch_summary(bftsim_t *h, uint64_t *committed_height, uint32_t *flags, uint32_t *ticks,
                          uint64_t *views, uint8_t *tip_hash);
 
 /* ValidatorSet / block helpers on the host (validator.rs, types/block.rs) */
 uint32_t bftsim_two_thirds_majority(uint32_t n);                    /* validator.rs:149-154 */
-uint32_t bftsim_seed_from_hash(const uint8_t hash[32], uint32_t n); /* validator.rs:39-48 */
-uint32_t bftsim_calc_proposer(const uint8_t prev_hash[32], uint32_t n, uint64_t round); /* :33-37,74-77 */
+uint32_t bftsim_seed_from_hash(const uint8_t hash[32], uint32_t n); /* validator.rs:39-48 (BE) */
+uint32_t bftsim_seed_from_hash_order(const uint8_t hash[32], uint32_t n, uint32_t seed_byte_order);
+uint32_t bftsim_calc_proposer(const uint8_t prev_hash[32], uint32_t n, uint64_t round); /* :33-37,74-77 (BE) */
 void bftsim_keccak256(const uint8_t *data, size_t len, uint8_t out[32]);
 void bftsim_genesis_hash(const bftsim_config *cfg, uint8_t out[32]); /* core/genesis.rs:44-55 */
 int bftsim_view_cmp(uint64_t h1, uint64_t r1, uint64_t h2, uint64_t r2); /* consensus/types.rs:81-98 */
+/* Core::check_message (src/consensus/pbft/core/core.rs:366-399) as the kernels run it: code =
+ * MessageType (protocol/mod.rs:36-41: 1 Preprepare, 2 Prepare, 3 Commit, 4 RoundChange), state =
+ * State (protocol/mod.rs:25-30: 1 AcceptRequest .. 4 Committed). Returns BFTSIM_CHECK_* (>= 0), or
+ * BFTSIM_EINVAL for codes / states outside those enums. */
+#define BFTSIM_CHECK_OK 0
+#define BFTSIM_CHECK_UNKNOWN 1        /* ConsensusError::UnknownMessageType (height 0) */
+#define BFTSIM_CHECK_FUTURE_BLOCK 2   /* FutureBlockMessage(h) */
+#define BFTSIM_CHECK_OLD 3            /* OldMessage */
+#define BFTSIM_CHECK_FUTURE_MSG 4     /* FutureMessage (backlog) */
+int bftsim_check_message(uint32_t code, uint64_t msg_height, uint64_t core_height, uint32_t state);
 
 /* Ledger export (core/ledger.rs:193-245 `add_block`: the `headers` map Hash -> Header of
  * store/schema.rs:66-68; the `block_hashes_by_height` list is bftsim_result.block_hash): after a

@@ -119,6 +119,14 @@ uint32_t orc_seed_from_hash(const uint8_t hash[32], uint32_t n) {
     v <<= 64;
     return (uint32_t)(v % n);
 }
+/* the same with the byte order of U128::from([u8; 16]) as a switch (bftsim.h BFTSIM_SEED_*):
+ * little-endian reads seed_buf = hash[0..8] ++ 0^8 as LE64(hash[0..8]) + 0 * 2^64. */
+uint32_t orc_seed_from_hash_order(const uint8_t hash[32], uint32_t n, uint32_t order) {
+    if (order == 0) return orc_seed_from_hash(hash, n);
+    unsigned __int128 v = 0;
+    for (int i = 15; i >= 0; --i) v = (v << 8) | (i < 8 ? hash[i] : 0);
+    return (uint32_t)(v % n);
+}
 
 /* ------------------------------------------------------------------------------------------ */
 /* Header encoding + block hash (src/types/block.rs:16-36,76-84; SPEC.md §7)                   */
@@ -506,6 +514,14 @@ static int check_message(val *v, int code, uint32_t vh) {
         return E_OK;
     }
     return E_OK;
+}
+
+int orc_check_message(int code, uint32_t msg_height, uint32_t core_height, int state) {
+    val v;
+    memset(&v, 0, sizeof v);
+    v.h = core_height;
+    v.st = state;
+    return check_message(&v, code, msg_height);
 }
 
 /* handle_msg_middle: FutureBlockMessage(h) → SyncBlock after 1 s (core.rs:58-69) */
@@ -898,7 +914,7 @@ static void set_hash(world *w, uint32_t x) {
     size_t len = orc_encode_header(buf, canon_at(w, x - 1)->hash, cfg->addresses + 20u * c->b.prop, tx,
                                    x, 0, 0, time, CAND_EXTRA, 11);
     orc_keccak256(buf, len, c->hash);
-    c->seed = orc_seed_from_hash(c->hash, w->n);
+    c->seed = orc_seed_from_hash_order(c->hash, w->n, cfg->seed_byte_order);
 }
 
 /* per-instance summary of a streamed run (orc_run_stream) */
@@ -930,7 +946,7 @@ static int run_instance_ex(const orc_config *cfg, uint32_t inst, const orc_resul
     canon_entry *g = canon_at(w, 0);
     g->set = 1; g->b.h = 0; g->b.valid = 1; g->T = -1; g->round = 0; g->commit_tick = 0;
     orc_genesis_hash(cfg, g->hash);
-    g->seed = orc_seed_from_hash(g->hash, n);
+    g->seed = orc_seed_from_hash_order(g->hash, n, cfg->seed_byte_order);
     uint64_t byz[4];
     orc_byz_mask(cfg, inst, byz);
     for (uint32_t i = 0; i < n; ++i) {

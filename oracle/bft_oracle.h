@@ -38,6 +38,10 @@ typedef struct orc_config {
     const uint8_t *addresses;    /* n * 20 bytes, ascending (sorted validator set) */
     uint8_t genesis_proposer[20];
     uint64_t genesis_gas_used;   /* gas_limit = gas_used + 10 (genesis.rs:51-53) */
+    uint32_t seed_byte_order;    /* 0: U128 read big-endian, 1: little-endian (validator.rs:39-48) */
+    uint32_t header_encoding;    /* 0: compact MessagePack (SPEC.md §7) */
+    uint32_t backlog_mode;       /* 0: reference (never re-delivered), 1: replay (SPEC.md §10) */
+    uint32_t reserved;
 } orc_config;
 
 typedef struct orc_result {
@@ -63,7 +67,9 @@ typedef struct orc_result {
 void orc_keccak256(const uint8_t *data, size_t len, uint8_t out[32]);
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 uint32_t orc_two_thirds_majority(uint32_t n);
-uint32_t orc_seed_from_hash(const uint8_t hash[32], uint32_t n);
+int orc_check_message(int code, uint32_t msg_height, uint32_t core_height, int state); /* core.rs:366-399 */
+uint32_t orc_seed_from_hash(const uint8_t hash[32], uint32_t n);                 /* big-endian U128 */
+uint32_t orc_seed_from_hash_order(const uint8_t hash[32], uint32_t n, uint32_t order); /* 1 = LE */
 size_t orc_encode_header(uint8_t *out, const uint8_t prev_hash[32], const uint8_t proposer[20],
                          const uint8_t tx_hash[32], uint64_t height, uint64_t gas_limit,
                          uint64_t gas_used, uint64_t time, const uint8_t *extra, size_t extra_len);

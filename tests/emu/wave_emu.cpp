@@ -243,7 +243,7 @@ extern "C" int emu_run_stream(const bftsim_config* cfg, uint64_t first, uint64_t
     if (cfg->n < 1 || cfg->n > 256 || window < 64 || (window & (window - 1))) return -4;
     uint8_t gh[32];
     bft::host_genesis_hash(cfg, gh);
-    uint32_t gseed = bft::seed_from_hash(gh, cfg->n);
+    uint32_t gseed = bft::seed_from_hash(gh, cfg->n, cfg->seed_byte_order == BFTSIM_SEED_LE);
     uint32_t seg = bft::segment_size(cfg->n);
     bft::Params P = bft::params_from_config(*cfg, seg, cfg->heights + 64, gseed, first, n);
     P.window_mask = window - 1;
@@ -283,7 +283,7 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
     if (cfg->n < 1 || cfg->n > 256) return -4;
     uint8_t gh[32];
     bft::host_genesis_hash(cfg, gh);
-    uint32_t gseed = bft::seed_from_hash(gh, cfg->n);
+    uint32_t gseed = bft::seed_from_hash(gh, cfg->n, cfg->seed_byte_order == BFTSIM_SEED_LE);
     uint32_t seg = bft::segment_size(cfg->n);
     uint32_t hcap = cfg->heights + 64;
     bft::Params P = bft::params_from_config(*cfg, seg, hcap, gseed, first, n);

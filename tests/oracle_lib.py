@@ -23,6 +23,8 @@ class OrcConfig(ctypes.Structure):
         ("proposer_crash_ppm", ctypes.c_uint32), ("phase_cap", ctypes.c_uint32),
         ("silent_mask", ctypes.c_uint64 * 4), ("addresses", ctypes.c_void_p),
         ("genesis_proposer", ctypes.c_uint8 * 20), ("genesis_gas_used", ctypes.c_uint64),
+        ("seed_byte_order", ctypes.c_uint32), ("header_encoding", ctypes.c_uint32),
+        ("backlog_mode", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
     ]
 
 
@@ -55,6 +57,8 @@ def lib():
                                            ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                            ctypes.c_char_p, ctypes.c_size_t]
         _lib.orc_seed_from_hash.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
+        _lib.orc_seed_from_hash_order.restype = ctypes.c_uint32
+        _lib.orc_seed_from_hash_order.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]
         _lib.orc_two_thirds_majority.argtypes = [ctypes.c_uint32]
     return _lib
 
@@ -72,6 +76,9 @@ def to_orc(cfg: BftConfig):
     for i, b in enumerate(cfg.genesis_proposer):
         c.genesis_proposer[i] = b
     c.genesis_gas_used = cfg.genesis_gas_used
+    c.seed_byte_order = cfg.seed_byte_order
+    c.header_encoding = 0
+    c.backlog_mode = cfg.backlog_mode
     return c, addr
 
 
@@ -113,9 +120,9 @@ def verify_chains(cfg: BftConfig, first: int, res: dict, threads: int = 8) -> in
     of instances that do not verify."""
     n = len(res["committed_height"])
     c, keep = to_orc(cfg)
-    arrs = {k: np.ascontiguousarray(res[k]).reshape(-1) for k in (
-        "committed_height", "flags", "ticks", "views", "round", "proposer", "variant", "time_tick",
-        "block_hash")}
+    dt = dict(committed_height=np.uint32, flags=np.uint32, ticks=np.uint32, views=np.uint64, round=np.uint16,
+              proposer=np.uint16, variant=np.uint8, time_tick=np.uint32, block_hash=np.uint8)
+    arrs = {k: np.ascontiguousarray(res[k], dtype=t).reshape(-1) for k, t in dt.items()}
     r = OrcResult()
     for k, a in arrs.items():
         setattr(r, k, a.ctypes.data)

@@ -7,6 +7,11 @@ import emu_lib as E
 from bftsim.configs import BftConfig, cfg1, cfg2, cfg3, cfg4, cfg5
 from parity_util import assert_same
 
+
+def _le(cfg):
+    import dataclasses
+    return dataclasses.replace(cfg, seed_byte_order=1, name=cfg.name + "-le")
+
 CASES = [
     ("cfg1-n5", lambda: cfg1(True, heights=40), 0, 1),
     ("cfg2", lambda: cfg2(heights=25), 0, 16),
@@ -33,6 +38,12 @@ CASES = [
     ("n130-byz43-drop", lambda: BftConfig(n=130, heights=8, seed=31, byz_count=43, drop_ppm=100_000), 0, 1),
     ("n200-silent-crash", lambda: BftConfig(n=200, heights=6, seed=32, silent=[0, 77, 199],
                                             proposer_crash_ppm=300_000), 0, 1),
+    # little-endian U128 seed (bftsim.h BFTSIM_SEED_LE): every N needs in-kernel block hashes
+    ("cfg1-n5-le", lambda: _le(cfg1(True, heights=30)), 0, 1),
+    ("cfg2-le", lambda: _le(cfg2(heights=20)), 0, 16),
+    ("cfg3-le", lambda: _le(cfg3(heights=8)), 0, 2),
+    ("cfg4-n64-le", lambda: _le(cfg4(64, heights=10)), 0, 2),
+    ("cfg4-n128-le", lambda: _le(cfg4(128, heights=6)), 0, 1),
 ]
 
 

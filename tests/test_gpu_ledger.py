@@ -1,8 +1,8 @@
 """Ledger export (core/ledger.rs:193-245 add_block -> the `headers` map of
 store/schema.rs:66-68): the Header bytes the GPU exports for every committed height equal the oracle's
 header encoder (oracle/bft_oracle.c orc_encode_header, itself pinned to the msgpack package by
-tests/test_oracle_kat.py) and hash to the block hashes of the run — for a power-of-two N (hash pass) and
-for N = 5 / 7 (hashes computed inside the consensus kernel)."""
+tests/test_oracle_kat.py) and hash to the block hashes of the run — for a power-of-two N (hash pass: cfg3, cfg1-n4) and
+for N = 5 / 7 and little-endian seeds (hashes computed inside the consensus kernel)."""
 import ctypes
 
 import numpy as np
@@ -13,6 +13,11 @@ from bftsim.runtime import Simulator
 import oracle_lib as O
 
 pytestmark = pytest.mark.gpu
+
+
+def _le(cfg):
+    import dataclasses
+    return dataclasses.replace(cfg, seed_byte_order=1, name=cfg.name + "-le")
 
 
 def expected_header(cfg, inst, x, prop, var, tick, prev):
@@ -31,7 +36,9 @@ def expected_header(cfg, inst, x, prop, var, tick, prev):
 
 
 @pytest.mark.parametrize("name,mk,first,n", [("cfg3", lambda: cfg3(heights=12), 0, 6),
-                                             ("cfg1-n5", lambda: cfg1(False, heights=15), 0, 1),
+                                             ("cfg1-n4", lambda: cfg1(False, heights=15), 0, 1),
+                                             ("cfg1-n5", lambda: cfg1(True, heights=15), 0, 1),
+                                             ("cfg3-le", lambda: _le(cfg3(heights=8)), 0, 4),
                                              ("cfg4-n7-crash", lambda: cfg4(7, heights=10), 3, 8)])
 def test_exported_headers(name, mk, first, n):
     cfg = mk()

@@ -10,6 +10,11 @@ from parity_util import assert_same
 pytestmark = pytest.mark.gpu
 
 
+def _le(cfg):
+    import dataclasses
+    return dataclasses.replace(cfg, seed_byte_order=1, name=cfg.name + "-le")
+
+
 def gpu_run(cfg, first, n, trace_ticks=0):
     from bftsim.runtime import Simulator
     sim = Simulator(cfg)
@@ -44,6 +49,13 @@ CASES = [
     ("n256-byz85", lambda: BftConfig(n=256, heights=20, seed=17, byz_count=85), 0, 4),
     ("n129-silent-crash", lambda: BftConfig(n=129, heights=30, seed=18, silent=[0, 64, 128],
                                             proposer_crash_ppm=300_000, drop_ppm=20_000), 0, 8),
+    # little-endian U128 seeds (include/bftsim.h BFTSIM_SEED_LE): block hashes in-kernel for every N
+    ("cfg1-n5-le", lambda: _le(cfg1(True)), 0, 1),
+    ("cfg2-le", lambda: _le(cfg2()), 0, 128),
+    ("cfg3-le", lambda: _le(cfg3()), 0, 48),
+    ("cfg4-n64-le", lambda: _le(cfg4(64, heights=60)), 0, 24),
+    ("cfg4-n7-le", lambda: _le(cfg4(7, heights=60)), 0, 24),
+    ("cfg4-n256-le", lambda: _le(cfg4(256, heights=30)), 0, 4),
 ] + [(f"cfg4-n{n}", (lambda n=n: cfg4(n, heights=60)), 0, 24)
      for n in (4, 7, 10, 16, 31, 32, 33, 63, 64, 65, 100, 128, 200, 256)]
 

@@ -58,11 +58,57 @@ def test_view_ordering_reference(a, b, want):
 
 
 def test_message_type_order_reference():
-    # protocol/mod.rs:36-41, 241-250: Preprepare=1 < Prepare < Commit < RoundChange
-    import importlib.util, os
-    spec = os.path.join(os.path.dirname(os.path.dirname(__file__)), "consensus-rs_amd", "csrc", "bft_wave.h")
-    src = open(spec).read()
-    assert "check_message(1," in src and "check_message(2," in src and "check_message(3," in src
+    """protocol/mod.rs:36-41, 241-250: Preprepare=1 < Prepare < Commit < RoundChange. The order is what
+    Core::check_message (core.rs:366-399) acts on: in AcceptRequest only the smallest type (Preprepare)
+    passes, every larger one is a FutureMessage; RoundChange compares the height only. Checked as
+    behaviour, through the kernels' check_message (libbftsim) and the oracle's, on a grid."""
+    L = runtime.lib()
+    L.bftsim_check_message.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
+    OL = O.lib()
+    OL.orc_check_message.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]
+    OK, UNKNOWN, FUTURE_BLOCK, OLD, FUTURE_MSG = range(5)
+    PREPREPARE, PREPARE, COMMIT, ROUND_CHANGE = 1, 2, 3, 4
+    ACCEPT, PREPREPARED, PREPARED, COMMITTED = 1, 2, 3, 4
+    for code in (PREPREPARE, PREPARE, COMMIT, ROUND_CHANGE):
+        for st in (ACCEPT, PREPREPARED, PREPARED, COMMITTED):
+            for core_h in (1, 2, 7):
+                for vh in (0, 1, 2, 3, 7, 8):
+                    got = L.bftsim_check_message(code, vh, core_h, st)
+                    assert got == OL.orc_check_message(code, vh, core_h, st), (code, st, core_h, vh)
+                    if vh == 0:
+                        assert got == UNKNOWN
+                    elif vh > core_h:
+                        assert got == FUTURE_BLOCK
+                    elif vh < core_h:
+                        assert got == OLD
+                    elif code == ROUND_CHANGE:
+                        assert got == OK                   # round change ignores the state
+                    elif st == ACCEPT:
+                        # MessageType order: only the smallest code passes before a Preprepare
+                        assert got == (OK if code < PREPARE else FUTURE_MSG)
+                    else:
+                        assert got == OK
+    # the order itself: the set of codes a fresh (AcceptRequest) Core accepts at its height is the
+    # prefix {Preprepare} of Preprepare < Prepare < Commit, plus RoundChange which skips the state test
+    accepted = [c for c in (1, 2, 3, 4) if L.bftsim_check_message(c, 5, 5, ACCEPT) == OK]
+    assert accepted == [PREPREPARE, ROUND_CHANGE]
+    assert L.bftsim_check_message(9, 5, 5, ACCEPT) < 0     # not a MessageType: EINVAL
+
+
+def test_proposer_seed_byte_orders():
+    """randon_seed (validator.rs:39-48) under both readings of U128::from([u8; 16]) (bigint 4.4.1,
+    unvendored): libbftsim's helper, the oracle's and Python integers agree."""
+    L = runtime.lib()
+    for n in (1, 4, 5, 7, 10, 64, 100, 256):
+        for seed in range(40):
+            h = bytes(((seed * 53 + i * 29 + 7) & 0xff) for i in range(32))
+            buf = h[:8] + bytes(8)
+            be = int.from_bytes(buf, "big") % n
+            le = int.from_bytes(buf, "little") % n
+            assert L.bftsim_seed_from_hash_order(h, n, 0) == O.lib().orc_seed_from_hash_order(h, n, 0) == be
+            assert L.bftsim_seed_from_hash_order(h, n, 1) == O.lib().orc_seed_from_hash_order(h, n, 1) == le
+    # little-endian: a power-of-two N takes the low bits of hash[0] — not identically 0
+    assert len({L.bftsim_seed_from_hash_order(bytes([r] * 32), 64, 1) for r in range(256)}) == 64
 
 
 def test_proposer_seed_helpers_agree():
