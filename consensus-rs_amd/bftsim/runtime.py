@@ -43,6 +43,7 @@ def lib():
         L.bftsim_kernel_ms_sum.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]
         L.bftsim_set_pipeline.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.bftsim_set_fast.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.bftsim_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
         L.bftsim_set_window.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         L.bftsim_fetch_summary.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5
@@ -176,6 +177,10 @@ class Simulator:
         _check(self.h, lib().bftsim_kernel_ms_sum(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)),
                "kernel_ms_sum")
         return a.value, b.value, n.value
+
+    def set_fast(self, on: bool):
+        """Verification switch: False runs N = 64 through the full kernel alone (identical results)."""
+        _check(self.h, lib().bftsim_set_fast(self.h, 1 if on else 0), "bftsim_set_fast")
 
     def set_pipeline(self, on: bool):
         """Batch throughput mode: hash pass of launch k overlaps the consensus of launch k+1."""

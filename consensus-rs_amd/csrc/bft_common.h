@@ -228,6 +228,16 @@ constexpr uint32_t DOM_DROP = 1, DOM_SPLIT = 2, DOM_CRASH = 3, DOM_BYZ = 4, DOM_
 
 BFT_FN uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 
+// A value held in a scalar register that the compiler must treat as unknown at this point (no-op on
+// the host). Used on the launch seed before Philox calls inside the kernels' tick / phase loops:
+// otherwise LLVM hoists the 20-word key schedule (and partial rounds on constant counters) out of the
+// loops and keeps it live in SGPRs across the whole body, which spills.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define BFT_OPAQUE_SGPR(x) asm volatile("" : "+s"(x))
+#else
+#define BFT_OPAQUE_SGPR(x) do { } while (0)
+#endif
+
 // Philox4x32-10 (Salmon et al. SC'11); 10 rounds of two 32x32→64 multiplies.
 BFT_FN void philox(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t out[4]) {
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);

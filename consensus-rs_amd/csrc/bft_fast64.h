@@ -1,0 +1,706 @@
+// bft_fast64.h — the N = 64 consensus kernel body of the benchmark workload (cfg3), one 64-lane
+// wavefront per instance, lane = validator (= one reference `Core`, core.rs:119-140).
+//
+// It runs the same state machine as the general body (bft_wave.h `Sim`), restricted to the phases
+// whose delivery has a closed form — a single Preprepare, Prepare/Commit phases with one view and one
+// digest class per kind, block gossip with one range, and message-less event phases. Any other phase
+// (RoundChange, Sync, old-block Commits, mixed kinds) hands the instance over to the full kernel
+// (`Sim<..., MODE_RESUME>`), which continues from that phase: the hand-over area holds the full
+// kernel's state layout, so results are bit-identical by construction (tested by the emulator and
+// GPU parity suites against the oracle).
+//
+// Why a separate body: restricted to these phases, most of a validator's state is implied —
+// * the round is 0 (only start_new_round, reached from a RoundChange, changes it), so the proposer of
+//   every view is validator 0 (seed ≡ 0 for big-endian U128 seeds and N a power of two, SPEC.md §1);
+// * every Preprepare / Prepare / Commit a validator sends carries its current view (h, 0), a Prepare
+//   or Commit the digest `pp`, a Preprepare its own candidate: an outbox is flags + the candidate's
+//   time tick + one block range;
+// * `lock` is either None or equal to `pp` (lock_hash copies pp; pp changes only while unlocked or to
+//   the locked block itself), `pend` is None or (h, me, 0, T);
+// * a Core commit is `pp` at round 0: one flag bit.
+// That leaves ~25 live 32-bit values per lane (the general body keeps ~90), so the kernel runs without
+// spills at 8 waves per SIMD, and the phase logic is short, mostly branch-free selects.
+#pragma once
+#include "bft_common.h"
+#include "bft_wave.h"
+
+namespace bft {
+
+// LDS per wave (bytes)
+struct F64Layout {
+    static constexpr uint32_t CACHE_OFF = 0;                   // outbound cache, SoA [word][lane]: per kind {h, d32}
+    static constexpr uint32_t CACHE_WORDS = 8;                 // 4 kinds (PP, PR, CM, old CM) x 2
+    static constexpr uint32_t RING_OFF = CACHE_OFF + CACHE_WORDS * 64 * 4;   // 64 canonical rows x 16 B
+    static constexpr uint32_t LAT_OFF = RING_OFF + 64 * 16;    // commit-latency histogram (65 words)
+    static constexpr uint32_t BYTES = LAT_OFF + 65 * 4 + 4;
+};
+constexpr uint32_t lds_bytes_fast64() { return F64Layout::BYTES; }
+
+template <class W>
+struct Fast64 {
+    static constexpr uint32_t N = 64, Q = 42;   // floor(2N/3) (validator.rs:149-154)
+    // lane flag bits
+    static constexpr uint32_t L_ST = 7u, L_WAIT = 8u, L_LOCK = 16u, L_BYZ = 32u, L_RUN = 64u, L_DEAD = 128u,
+                              L_PENDV = 256u, L_CMT = 512u;
+    enum : uint32_t { P_GENERAL = 0, P_BLK = 1, P_PC = 2, P_PP = 3, P_NONE = 4 };
+
+    const Params& P;
+    uint8_t* lds;
+    W wv;
+    // identity
+    uint32_t me;                       // lane = validator index
+    uint32_t inst_local, inst, off_inst, off_tick;
+    // wave-uniform
+    bool seg_done, frozen;
+    uint32_t canon_h, canon_tick, done_tick, seg_flags, flushed;
+    uint64_t canon_tip, views_acc;
+    uint64_t byz_mask;                 // Byzantine validators of this instance (SPEC.md §6)
+    int32_t tick;
+    // per lane (Core + RoundState + chain tip + miner + timers + outbox)
+    uint32_t fl;                       // L_* bits; state in bits 0..2
+    uint32_t h;
+    uint64_t pp, prep, comm;
+    uint32_t pend_T, cand_T, proposer, last;
+    int32_t last_T, timer_tick, rc_last_tick, wake_tick;
+    uint32_t mint_height, miner_queue, sync_pending;
+    uint32_t nxf, nx_ppT, nx_blo, nx_bhi;
+    uint32_t lane_flags;
+#ifdef BFT_STAMPS
+    uint64_t st_acc[12];
+    uint64_t st_t;
+#define F64_STAMP(k) do { uint64_t t_ = wv.clock(); st_acc[k] += t_ - st_t; st_t = t_; } while (0)
+#define F64_COUNT(k) do { st_acc[k] += 1; } while (0)
+#else
+#define F64_STAMP(k) do { } while (0)
+#define F64_COUNT(k) do { } while (0)
+#endif
+
+    BFT_FN Fast64(const Params& p, uint8_t* l, uint32_t wave_global) : P(p), lds(l) {
+        wv.init(nullptr);
+        me = wv.lane();
+        inst_local = wave_global;
+        inst = p.first_instance + inst_local;
+        const bool inst_ok = inst_local < p.n_instances;
+        const bool running = inst_ok && !((p.silent_mask[0] >> me) & 1ull);
+        fl = ST_ACCEPT_REQUEST | (running ? L_RUN : 0u);
+        seg_done = !inst_ok;
+        frozen = false;
+        canon_h = 0; canon_tick = 0; done_tick = p.max_ticks; seg_flags = 0; flushed = 0;
+        canon_tip = 0; views_acc = 0; byz_mask = 0;
+        tick = 0;
+        h = 0; pp = BLK_NONE; prep = comm = 0;
+        pend_T = cand_T = 0; proposer = 0xffffffffu; last = 0;
+        last_T = -1; timer_tick = -1; rc_last_tick = 0; wake_tick = -1;
+        mint_height = 0; miner_queue = 0; sync_pending = 0;
+        nxf = 0; nx_ppT = 0; nx_blo = nx_bhi = 0;
+        lane_flags = 0;
+        for (uint32_t k = 0; k < F64Layout::CACHE_WORDS; ++k) *cache_p(k) = 0;
+        off_inst = offset_inst_part(p.seed, inst);
+        off_tick = 0;
+    }
+
+    // ------------------------------------------------------------------ small helpers
+    // the launch seed as an opaque scalar (bft_common.h BFT_OPAQUE_SGPR): keeps Philox key schedules
+    // from being hoisted out of the loops
+    BFT_FN uint64_t seed() const {
+        uint32_t lo = (uint32_t)P.seed, hi = (uint32_t)(P.seed >> 32);
+        BFT_OPAQUE_SGPR(lo);
+        BFT_OPAQUE_SGPR(hi);
+        return (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+    BFT_FN uint32_t st() const { return fl & L_ST; }
+    BFT_FN void set_st(uint32_t s) { fl = (fl & ~L_ST) | s; }
+    BFT_FN bool has(uint32_t b) const { return (fl & b) != 0; }
+    BFT_FN uint32_t uni(uint32_t v) const { return wv.uni(v); }
+    BFT_FN uint64_t ballot(bool p) { return wv.ballot(p); }
+    BFT_FN uint32_t rl(uint32_t v, uint32_t j) { return wv.readlane(v, j); }
+    BFT_FN uint64_t rl64(uint64_t v, uint32_t j) {
+        return (uint64_t)wv.readlane((uint32_t)v, j) | ((uint64_t)wv.readlane((uint32_t)(v >> 32), j) << 32);
+    }
+    BFT_FN static uint64_t rotr(uint64_t m, uint32_t off) { return off ? ((m >> off) | (m << (64u - off))) : m; }
+    BFT_FN static uint64_t low(uint32_t k) { return k >= 64u ? ~0ull : ((1ull << k) - 1ull); }
+    BFT_FN static uint32_t popc(uint64_t m) { return (uint32_t)__builtin_popcountll(m); }
+    BFT_FN static uint32_t hibit(uint64_t m) { return m ? 63u - (uint32_t)__builtin_clzll(m) : 0u; }
+    BFT_FN static uint32_t ctz64(uint64_t m) { return m ? (uint32_t)__builtin_ctzll(m) : 64u; }
+
+    // ------------------------------------------------------------------ outbound cache (backend.rs:141-148)
+    // per kind the last subject sent: {height, 32-bit block id}; the round is always 0 here
+    BFT_FN uint32_t* cache_p(uint32_t w) const { return (uint32_t*)(lds + F64Layout::CACHE_OFF) + w * 64u + me; }
+    BFT_FN bool cache_hit(uint32_t kind, uint32_t vh, uint64_t d) {
+        const uint32_t d32 = blk_d32(d);
+        uint32_t* c = cache_p(2u * kind);
+        const uint32_t sd = c[64];
+        if (sd != 0 && c[0] == vh && sd == d32) return true;
+        c[0] = vh;
+        c[64] = d32;
+        return false;
+    }
+    // the hand-over area (P.save, the full kernel's layout): cold outbox words go there at once
+    BFT_FN uint32_t* save_p() const { return P.save + ((uint64_t)inst_local * 64u + me) * SAVE_WORDS; }
+
+    BFT_FN uint64_t cand() const { return blk_make(mint_height, me, 0, cand_T); }
+
+    // Predicated style: a handler takes a per-lane predicate `c` and updates registers with selects, so
+    // the hot paths have no divergent regions that write registers (LLVM's structurizer copies every
+    // live value at each nested divergent branch). Only memory stores sit under divergent `if`s, and
+    // the rare paths (round changes, sync requests, old Preprepares) run behind uniform ballots.
+
+    // a message of `kind` (view (vh, 0), digest d) through the outbound cache into the outbox
+    BFT_FN bool send_kind(bool c, uint32_t kind, uint32_t vh, uint64_t d, uint32_t flag, uint32_t wflag) {
+        const uint32_t d32 = blk_d32(d);
+        uint32_t* cp = cache_p(2u * kind);
+        const uint32_t ch = cp[0], cd = cp[64];
+        const bool upd = c && !(cd != 0 && ch == vh && cd == d32);   // cache miss: the message goes out
+        if (upd) { cp[0] = vh; cp[64] = d32; }
+        const bool dup = upd && (nxf & flag) != 0;                     // a second one of its kind this phase
+        lane_flags |= dup ? FLAG_OUTBOX : 0u;
+        const bool put = upd && !dup;
+        nxf |= put ? (flag | (has(L_BYZ) ? wflag : 0u)) : 0u;
+        return put;
+    }
+    BFT_FN void out_preprepare_p(bool c) {                       // view (h, 0), own candidate; equivocates iff Byzantine
+        const bool put = send_kind(c, 0, h, cand(), F_PP, F_PP_EQ);
+        nx_ppT = put ? cand_T : nx_ppT;
+    }
+    BFT_FN void out_prepare_p(bool c) { send_kind(c, 1, h, pp, F_PR, F_PR_W); }   // (h, 0, pp)
+    BFT_FN void out_commit_p(bool c) { send_kind(c, 2, h, pp, F_CM, F_CM_W); }
+    BFT_FN void out_blocks_p(bool c, uint32_t lo, uint32_t hi) {  // lo <= hi
+        const bool hb = (nxf & F_BLK) != 0;
+        nx_blo = c ? (hb && nx_blo < lo ? nx_blo : lo) : nx_blo;
+        nx_bhi = c ? (hb && nx_bhi > hi ? nx_bhi : hi) : nx_bhi;
+        nxf |= c ? F_BLK : 0u;
+    }
+    // the cold kinds always hand the instance over: fields straight to the hand-over area
+    BFT_FN void out_old_commit(uint32_t vh, uint64_t d) {
+        uint32_t* cp = cache_p(6);
+        const uint32_t d32 = blk_d32(d);
+        if (cp[64] != 0 && cp[0] == vh && cp[64] == d32) return;
+        cp[0] = vh; cp[64] = d32;
+        if (nxf & F_OCM) { lane_flags |= FLAG_OUTBOX; return; }
+        nxf |= F_OCM | (has(L_BYZ) ? F_OCM_W : 0u);
+        uint32_t* s = save_p() + SAVE_COLD;
+        s[0] = vh; s[1] = 0; s[2] = (uint32_t)d; s[3] = (uint32_t)(d >> 32);
+    }
+    BFT_FN void out_round_change(uint32_t vh, uint32_t vr) {
+        if (nxf & F_RC) { lane_flags |= FLAG_OUTBOX; return; }
+        nxf |= F_RC;
+        uint32_t* s = save_p() + SAVE_COLD;
+        s[4] = vh; s[5] = vr;
+    }
+    BFT_FN void out_sync(uint32_t height) {
+        uint32_t* s = save_p() + SAVE_COLD;
+        if (nxf & F_SYNC) { if (height < s[6]) s[6] = height; return; }
+        nxf |= F_SYNC;
+        s[6] = height;
+    }
+
+    // ------------------------------------------------------------------ canonical rows
+    // rows (flushed, canon_h] live in an LDS ring of 64 and are written to HBM 64 at a time, one
+    // 16-byte row per lane (whole lines instead of single-lane stores)
+    BFT_FN uint32_t* ring_row(uint32_t x) const { return (uint32_t*)(lds + F64Layout::RING_OFF) + (x & 63u) * 4u; }
+    BFT_FN uint32_t* rec_row(uint32_t x) const { return P.rec + ((uint64_t)inst_local * P.rows + x) * 4; }
+    BFT_FN uint32_t row_word(uint32_t x, uint32_t k) {
+        if (x > flushed) return ring_row(x)[k];
+        return wv.gload(rec_row(x) + k);
+    }
+    BFT_FN uint64_t canon_blk(uint32_t x) {                      // x >= 1, recorded
+        if (x == canon_h) return canon_tip;
+        const uint32_t w1 = row_word(x, 1), T = row_word(x, 2);
+        return blk_make(x, w1 & 0xffffu, (w1 >> 16) & 1u, T);
+    }
+    BFT_FN void flush_rows() {                                   // uniform; rows (flushed, canon_h]
+        wv.sync();
+        const uint32_t x = flushed + 1u + me;
+        if (x <= canon_h) {
+            const uint32_t* r = ring_row(x);
+            wv.gstore4(rec_row(x), r[0], r[1], r[2], r[3]);
+        }
+        wv.sync();
+        flushed = canon_h;
+    }
+    // a new canonical height (uniform): row, histograms, instance-rounds
+    BFT_FN void record_canon(uint32_t x, uint64_t b) {
+        if (x <= P.heights) {
+            const uint32_t lat = (uint32_t)tick - canon_tick;
+            if (me == 0) wv.lds_add((uint32_t*)(lds + F64Layout::LAT_OFF) + (lat < 64u ? lat : 64u), 1u);
+            views_acc += 1;
+        }
+        if (me == 0) {
+            uint32_t* r = ring_row(x);
+            r[0] = 0; r[1] = blk_prop(b) | (blk_var(b) << 16) | (1u << 24); r[2] = blk_T(b); r[3] = 0;
+        }
+        wv.sync();
+        canon_h = x;
+        canon_tip = b;
+        canon_tick = (uint32_t)tick;
+        if (canon_h - flushed == 64u) flush_rows();
+    }
+
+    // ------------------------------------------------------------------ chain, miner, timers
+    BFT_FN void chain_insert_core_p(bool c) {                    // Chain::insert_block of pp (chain.rs:45-71)
+        const uint32_t x = blk_h(pp);
+        const bool nw = c && x > last;                           // else ChainError::Exists
+        const bool gap = nw && last + 1 < x;                     // Not found ancestor → SyncBlock
+        if (ballot(gap) != 0) { if (gap) out_sync(last + 1); }
+        const bool ins = nw && !gap;
+        fl |= ins ? L_CMT : 0u;
+        last_T = ins ? (int32_t)blk_T(pp) : last_T;
+        last = ins ? x : last;
+        out_blocks_p(ins, x, x);                                 // ChainEvent::NewBlock
+        miner_queue = (ins && x > miner_queue) ? x : miner_queue; // ChainEvent::NewHeader
+    }
+    // handle_msg_middle Block branch (core.rs:75-82) for the uniform range [lo, hi]
+    BFT_FN void handle_blocks_p(bool c, uint32_t lo, uint32_t hi) {
+        const bool nw = c && hi > last;
+        const bool gap = nw && lo > last + 1;
+        if (ballot(gap) != 0) { if (gap) out_sync(last + 1); }
+        const bool ins = nw && !gap;
+        // time tick of block hi: the canonical tip, or a recorded row (hi is uniform)
+        const int32_t T = hi == canon_h ? (int32_t)blk_T(canon_tip) : (int32_t)uni(row_word(hi, 2));
+        const uint32_t from = last + 1;
+        last = ins ? hi : last;
+        last_T = ins ? T : last_T;
+        out_blocks_p(ins, from, hi);
+        miner_queue = (ins && hi > miner_queue) ? hi : miner_queue;
+    }
+    BFT_FN void start_new_zero_round_p(bool c) {                 // core.rs:441-470
+        h = c ? last + 1 : h;
+        fl = c ? ((fl & ~(L_ST | L_WAIT | L_LOCK | L_PENDV)) | ST_ACCEPT_REQUEST) : fl;
+        pp = c ? BLK_NONE : pp;
+        prep = c ? 0ull : prep;
+        comm = c ? 0ull : comm;
+        proposer = c ? 0u : proposer;                            // (seed 0 + round 0) mod 64
+        timer_tick = c ? tick + 1 : timer_tick;                  // new_round_change_timer
+    }
+    BFT_FN void send_preprepare_cand_p(bool c) {                 // preprepare.rs:30-43, req = candidate
+        const bool s = c && h == mint_height && proposer == me;
+        if (ballot(s) != 0) {                                    // the proposer (validator 0) proposes
+            bool cr = false;
+            if (P.crash_on) cr = proposer_crashed(seed(), P.crash_thr32, 1u, inst, h, 0);
+            out_preprepare_p(s && !cr);
+        }
+    }
+    BFT_FN void handle_new_header_event_p(bool c) {              // core.rs:154-163 + request.rs:19-42
+        c = c && !has(L_DEAD);
+        start_new_zero_round_p(c);
+        const bool pv = c && h == mint_height;                   // accept the own candidate
+        fl |= pv ? L_PENDV : 0u;
+        pend_T = pv ? cand_T : pend_T;
+        send_preprepare_cand_p(pv);
+    }
+    BFT_FN void miner_mine_p(bool c) {                           // minner/mod.rs:95-143
+        const uint32_t x = last + 1;
+        const int32_t T = tick > last_T + 1 ? tick : last_T + 1;
+        cand_T = c ? (uint32_t)T : cand_T;
+        mint_height = c ? x : mint_height;
+        const bool now = c && T <= tick;                         // seal sleeps until header.time otherwise
+        wake_tick = c ? (now ? -1 : T) : wake_tick;
+        if (ballot(now) != 0) handle_new_header_event_p(now);
+    }
+    BFT_FN void miner_step_p() {                                 // Minner: Handler<NewHeader> (minner/mod.rs:56-69)
+        const bool ev = has(L_RUN) && wake_tick < 0;
+        const uint32_t q = miner_queue;
+        miner_queue = ev ? 0u : miner_queue;
+        const bool m = ev && q != 0 && q >= mint_height;
+        if (ballot(m) != 0) miner_mine_p(m);
+    }
+    BFT_FN void new_round_change_timer() { timer_tick = tick + 1; }
+    BFT_FN void send_round_change(uint32_t round) {              // round_change.rs:38-63 (cold)
+        if (rc_last_tick == tick) { new_round_change_timer(); return; }
+        rc_last_tick = tick;
+        if (0u < round) { fl |= L_WAIT; new_round_change_timer(); }   // catchup_round (core.rs:555-565)
+        out_round_change(h, round);
+    }
+    // send_next_round_change (round_change.rs:26-36): the RoundChangeSet is empty here (it only fills
+    // from RoundChange messages, which hand over), so max_round() = 0 and the target is round 1
+    BFT_FN void send_next_round_change() { send_round_change(1); }
+    BFT_FN void t_step() {                                       // SPEC.md §2 T-step (running validators)
+        const bool run = has(L_RUN);
+        if (tick == 0) { start_new_zero_round_p(run); miner_mine_p(run); return; }
+        const bool w = run && wake_tick == tick;                 // seal wakes up
+        wake_tick = w ? -1 : wake_tick;
+        if (ballot(w) != 0) handle_new_header_event_p(w);
+        if (ballot(run && wake_tick < 0 && miner_queue != 0) != 0) miner_step_p();
+        const bool sp = run && sync_pending != 0;
+        if (ballot(sp) != 0) {
+            if (sp && last < sync_pending) out_sync(last + 1);
+            sync_pending = sp ? 0u : sync_pending;
+        }
+        const bool tm = run && !has(L_DEAD) && timer_tick == tick;   // TimerEvent (core.rs:207-225)
+        if (ballot(tm) != 0) {
+            timer_tick = tm ? -1 : timer_tick;
+            const bool caught = tm && last >= h;
+            fl &= caught ? ~L_WAIT : ~0u;
+            if (tm && !caught) send_next_round_change();
+        }
+    }
+    BFT_FN bool pending_local() const {
+        return has(L_RUN) && (nxf != 0 || (wake_tick < 0 && miner_queue != 0 && miner_queue >= mint_height));
+    }
+
+    // ------------------------------------------------------------------ handlers
+    // HandlePreprepare::handle (preprepare.rs:45-126) of the phase's single Preprepare (uniform src, view)
+    BFT_FN void handle_preprepare_p(bool c, uint32_t src, uint32_t vh, uint64_t b, bool equiv) {
+        if (equiv) {                                             // SPEC.md §6: variant 1 to SPLIT receivers
+            const uint64_t sm = split_mask(vh);
+            b |= (me != src && ((sm >> me) & 1ull)) ? (1ull << 33) : 0ull;
+        }
+        const int res = check_message_class(MT_PREPREPARE, vh, h, st());
+        bool go = c && (res == CM_OK || res == CM_FUTURE_BLOCK);   // FutureBlockMessage falls through
+        const bool old = c && res == CM_OLD;
+        if (ballot(old) != 0) {                                  // a Preprepare of a passed height
+            if (old) {
+                const uint32_t bh = blk_h(b);
+                if (bh <= last && blk_eq(canon_blk(bh), b)) {    // else InvalidProposal
+                    if (src == 0) out_old_commit(vh, b);         // old proposer (seed 0, round 0)
+                    go = true;                                   // falls through (preprepare.rs:52-74)
+                }
+            }
+        }
+        go = go && proposer == src;                              // else NotFromProposer
+        const uint32_t bh = blk_h(b);
+        const bool bad = go && (bh == 0 || bh - 1 > last);       // Backend::verify: unknown ancestor
+        const bool acc = go && !bad && st() == ST_ACCEPT_REQUEST;
+        const bool lk = acc && has(L_LOCK);
+        const bool lk_ok = lk && blk_eq(b, pp);                  // locked: same block → commit
+        const bool unl = acc && !has(L_LOCK);                    // unlocked: accept → prepare
+        pp = (lk_ok || unl) ? b : pp;
+        fl = lk_ok ? ((fl & ~L_ST) | ST_PREPARED) : unl ? ((fl & ~L_ST) | ST_PREPREPARED) : fl;
+        out_prepare_p(unl);                                      // send_prepare
+        out_commit_p(lk_ok || (unl && has(L_BYZ)));              // send_commit / Byzantine commit (SPEC.md §6)
+        const bool rc = bad || (lk && !lk_ok);
+        if (ballot(rc) != 0) { if (rc) send_next_round_change(); }
+    }
+    BFT_FN void lock_hash() { if (blk_valid(pp)) fl |= L_LOCK; }   // round_state.rs:100-110 (lock = pp)
+
+    // SPLIT bits of receivers 0..63 for view (vh, 0) (SPEC.md §5; split_bit for v < 64): one uniform draw
+    BFT_FN uint64_t split_mask(uint32_t vh) const {
+        uint32_t w[4];
+        philox(seed(), inst, vh, 0, DOM_SPLIT, w);
+        return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+    }
+
+    // digests of class `cls` matching `target` (wildcards match both variants)
+    BFT_FN static uint64_t class_match(uint64_t cls, uint64_t v0, uint64_t v1, uint64_t w, uint64_t target) {
+        if (!blk_valid(target) || ((cls ^ target) & BLK_HP_MASK) != 0) return 0;
+        return w | (blk_var(target) ? v1 : v0);
+    }
+    // smallest p with popcount(base | a & low(p+1) | b & low(p)) > Q, else 64
+    BFT_FN static uint32_t first_over(uint64_t base, uint64_t a, uint64_t b) {
+        if (popc(base | a | (b & low(63))) <= Q) return 64;
+        uint32_t lo = 0, hi = 63;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (popc(base | (a & low(mid + 1)) | (b & low(mid))) > Q) hi = mid;
+            else lo = mid + 1;
+        }
+        return lo;
+    }
+
+    struct PC {                         // a Prepare/Commit phase (wave-uniform)
+        uint64_t kpr, kcm, v1, pr_cls, cm_cls;   // v1: senders whose digest is variant 1
+        uint32_t pr_h, cm_h;
+    };
+    // senders of `k` whose digest matches `target` of class `cls`: Byzantine wildcards match both variants
+    BFT_FN uint64_t class_match_k(uint64_t k, uint64_t v1, uint64_t cls, uint64_t target) const {
+        if (!blk_valid(target) || ((cls ^ target) & BLK_HP_MASK) != 0) return 0;
+        return k & (byz_mask | (blk_var(target) ? v1 : ~v1));
+    }
+    // prepare.rs:48-66 and commit.rs:63-82 in this receiver's rotated delivery order, as prefix masks
+    // (the closed form of bft_wave.h deliver_prepare_commit with round 0 and lock = pp)
+    BFT_FN void deliver_pc(bool rcv, const PC& c, uint64_t mk, uint32_t off) {
+        const uint64_t prd = rcv ? (mk & c.kpr) : 0ull, cmd = rcv ? (mk & c.kcm) : 0ull;
+        const uint32_t s0 = st();
+        const int rp = check_message_class(MT_PREPARE, c.pr_h, h, s0);
+        const int rm = check_message_class(MT_COMMIT, c.cm_h, h, s0);
+        // FutureBlockMessage → the delayed sync check (core.rs:58-69)
+        sync_pending = (prd != 0 && rp == CM_FUTURE_BLOCK && c.pr_h > sync_pending) ? c.pr_h : sync_pending;
+        sync_pending = (cmd != 0 && rm == CM_FUTURE_BLOCK && c.cm_h > sync_pending) ? c.cm_h : sync_pending;
+        const uint64_t PRacc = (rp == CM_OK && c.pr_h == h) ? prd : 0ull;
+        const uint64_t CMacc = (rm == CM_OK && c.cm_h == h) ? (cmd & class_match_k(c.kcm, c.v1, c.cm_cls, pp)) : 0ull;
+        // Order-free evaluation first. The delivery order (rotation by `off`) only matters when the
+        // prepare quorum is crossed by commits delivered before the last prepare, or when a trigger and a
+        // commit quorum both occur (which comes last decides Prepared vs Committed); lanes in either case
+        // take the exact rotated closed form below (a uniform branch, skipped when no lane needs it).
+        const uint64_t U = prep | comm;
+        const uint64_t mpp0 = PRacc & class_match_k(c.kpr, c.v1, c.pr_cls, pp);
+        const uint32_t nUP = popc(U | PRacc);
+        const bool cexists = CMacc != 0 && popc(comm | CMacc) > Q;
+        const bool tb_amb = PRacc != 0 && CMacc != 0 && nUP <= Q && popc(U | PRacc | CMacc) > Q;
+        bool trig = (PRacc != 0 && nUP > Q) || (has(L_LOCK) && mpp0 != 0);
+        const bool committed = s0 >= ST_COMMITTED;
+        bool fires = !trig && cexists && !committed;
+        uint32_t fin = trig ? ST_PREPARED : (fires ? ST_COMMITTED : s0);
+        const bool amb = tb_amb || (trig && cexists);
+        if (ballot(amb) != 0) {
+            if (amb) {
+                const uint64_t PR = rotr(PRacc, off), CM = rotr(CMacc, off);
+                const uint64_t U0 = rotr(U, off);
+                const uint32_t lastPR = hibit(PR), lastCM = hibit(CM);
+                const bool trigB = PR != 0 && popc(U0 | PR | (CM & low(lastPR))) > Q;
+                const uint64_t mpp = rotr(mpp0, off);
+                const uint64_t lm = has(L_LOCK) ? mpp : 0ull;       // lock == pp when locked
+                trig = trigB || lm != 0;
+                uint32_t t1 = lm ? ctz64(lm) : 64u;
+                const uint32_t lastT = trigB ? lastPR : hibit((mpp & ~low(t1)) | (t1 < 64u ? (1ull << t1) : 0ull));
+                if (trig && committed && trigB) {                  // a re-commit needs a commit after the first trigger
+                    const uint32_t pstar = first_over(U0, PR, CM);
+                    const uint64_t ge = PR & ~low(pstar);
+                    const uint32_t tB = ge ? ctz64(ge) : 64u;
+                    t1 = tB < t1 ? tB : t1;
+                }
+                fires = trig ? (committed ? (cexists && lastCM >= t1) : cexists) : (cexists && !committed);
+                fin = trig ? ((cexists && lastCM >= lastT) ? ST_COMMITTED : ST_PREPARED) : (fires ? ST_COMMITTED : s0);
+            }
+        }
+        prep |= PRacc;
+        comm |= CMacc;
+        fl |= ((trig || fires) && blk_valid(pp)) ? L_LOCK : 0u;  // lock_hash
+        out_commit_p(trig);                                      // send_commit
+        chain_insert_core_p(fires);                              // Core::commit → insert_block
+        set_st(fin);
+    }
+
+    // ------------------------------------------------------------------ commits of a phase → canonical chain
+    BFT_FN void resolve_commits() {
+        const bool c = has(L_CMT);
+        const uint64_t bal = ballot(c);
+        if (bal == 0) return;
+        fl &= ~L_CMT;
+        if (seg_done) return;
+        const uint32_t lead = ctz64(bal);
+        const uint32_t x = blk_h(pp);
+        const uint32_t x0 = uni(rl(x, lead));
+        if (ballot(c && x != x0) == 0) {
+            // every committer commits the first one's height (the common case): uniform update
+            const uint64_t b0 = rl64(pp, lead);
+            const bool known = x0 <= canon_h;
+            const uint64_t ref = known ? canon_blk(x0) : b0;
+            const uint64_t badm = ballot(c && !blk_eq(pp, ref));
+            bool fr = badm != 0;
+            if (!known && x0 < P.hcap && (!fr || ctz64(badm) > lead)) record_canon(x0, b0);
+            if (x0 >= P.hcap) fr = true;
+            if (fr) { frozen = true; seg_flags |= FLAG_SAFETY; }
+            return;
+        }
+        // mixed heights: replay the commits in lane order (the oracle's receiver order)
+        uint64_t bits = bal;
+        bool fr = false;
+        while (bits) {
+            const uint32_t j = ctz64(bits);
+            bits &= bits - 1ull;
+            const uint32_t xj = uni(rl(x, j));
+            const uint64_t bj = rl64(pp, j);
+            if (xj >= P.hcap) { fr = true; break; }
+            if (xj <= canon_h) {
+                if (!blk_eq(canon_blk(xj), bj)) { fr = true; break; }
+            } else {
+                record_canon(xj, bj);                            // xj == canon_h + 1
+            }
+        }
+        if (fr) { frozen = true; seg_flags |= FLAG_SAFETY; }
+    }
+
+    // ------------------------------------------------------------------ hand-over to the full kernel
+    // the full kernel's save layout (bft_wave.h BFT_STATE_32 / BFT_STATE_64, then prep, comm, the 12
+    // cache words, the bool bits, tick, phase); every implied field is expanded here
+    BFT_FN void save_state(uint32_t p) {
+        flush_rows();
+        uint32_t* s = save_p();
+        const uint64_t lock = has(L_LOCK) ? pp : BLK_NONE;
+        const uint64_t pend = has(L_PENDV) ? blk_make(h, me, 0, pend_T) : BLK_NONE;
+        const uint64_t cd = mint_height ? cand() : BLK_NONE;
+        const uint64_t ppb = blk_make(h, me, 0, nx_ppT);
+        const uint32_t w32[29] = {h, 0u, st(), 0u, proposer, last, 0u, (uint32_t)last_T, (uint32_t)timer_tick,
+                                  (uint32_t)rc_last_tick, (uint32_t)wake_tick, mint_height, miner_queue,
+                                  sync_pending, lane_flags, canon_h, done_tick, seg_flags, 0u, canon_tick, nxf,
+                                  h, 0u, h, 0u, h, 0u, nx_blo, nx_bhi};
+        uint32_t k = 0;
+        for (uint32_t i = 0; i < 29; ++i) s[k++] = w32[i];
+        const uint64_t w64[9] = {lock, pp, pend, cd, canon_tip, views_acc, ppb, pp, pp};
+        for (uint32_t i = 0; i < 9; ++i) { s[k++] = (uint32_t)w64[i]; s[k++] = (uint32_t)(w64[i] >> 32); }
+        s[k++] = (uint32_t)prep; s[k++] = (uint32_t)(prep >> 32);
+        s[k++] = (uint32_t)comm; s[k++] = (uint32_t)(comm >> 32);
+        for (uint32_t kind = 0; kind < 4; ++kind) {              // {height, round, d32} per kind
+            s[k++] = *cache_p(2u * kind);
+            s[k++] = 0u;
+            s[k++] = *cache_p(2u * kind + 1u);
+        }
+        s[k++] = (has(L_BYZ) ? 1u : 0u) | (has(L_DEAD) ? 2u : 0u) | (has(L_WAIT) ? 4u : 0u) | (frozen ? 8u : 0u) |
+                 (seg_done ? 16u : 0u);
+        s[k++] = (uint32_t)tick;
+        s[k++] = p;
+    }
+
+    BFT_FN void init_byzantine() {       // partial Fisher-Yates by lane 0 (SPEC.md §5), LDS scratch
+        uint8_t* perm = lds + F64Layout::RING_OFF;
+        uint32_t* mw = (uint32_t*)(lds + F64Layout::RING_OFF + 64);
+        if (me == 0 && !seg_done) {
+            for (uint32_t i = 0; i < N; ++i) perm[i] = (uint8_t)i;
+            uint64_t mask = 0;
+            const uint32_t f = P.byz_count < N ? P.byz_count : N;
+            for (uint32_t i = 0; i < f; ++i) {
+                uint32_t w[4];
+                philox(P.seed, inst, i, 0, DOM_BYZ, w);
+                const uint32_t j = i + w[0] % (N - i);
+                const uint8_t t = perm[i]; perm[i] = perm[j]; perm[j] = t;
+                mask |= 1ull << perm[i];
+            }
+            mw[0] = (uint32_t)mask; mw[1] = (uint32_t)(mask >> 32);
+        }
+        wv.sync();
+        const uint64_t mask = seg_done ? 0ull : (uint64_t)uni(mw[0]) | ((uint64_t)uni(mw[1]) << 32);
+        byz_mask = mask;
+        if ((mask >> me) & 1ull) fl |= L_BYZ;
+        wv.sync();
+    }
+
+    // ------------------------------------------------------------------ the run
+    BFT_FN void run() {
+#ifdef BFT_STAMPS
+        for (int k = 0; k < 12; ++k) st_acc[k] = 0;
+        st_t = wv.clock();
+#endif
+        if (P.byz_count > 0) init_byzantine();
+        uint32_t* lat = (uint32_t*)(lds + F64Layout::LAT_OFF);
+        for (uint32_t b = me; b < 65u; b += 64u) lat[b] = 0;
+        wv.sync();
+        bool bailed = false;
+        for (tick = 0; tick < (int32_t)P.max_ticks; ++tick) {
+            if (seg_done) break;
+            // act: this instance still runs this tick (uniform); per lane, only running validators
+            // (not silent) handle events and messages
+            bool act = !frozen;
+            off_tick = offset_tick_part(off_inst, (uint32_t)tick);
+            F64_STAMP(7);
+            // the T-step, only when some running validator has a tick event
+            if (ballot(has(L_RUN) && (tick == 0 || wake_tick == tick || (wake_tick < 0 && miner_queue != 0) ||
+                                      sync_pending != 0 || (!has(L_DEAD) && timer_tick == tick))) != 0) {
+                t_step();
+            }
+            F64_STAMP(0);
+            for (uint32_t p = 0;; ++p) {
+                if (!act || ballot(pending_local()) == 0) break;
+                if (p >= P.phase_cap) {                          // in-flight messages are dropped (SPEC.md §2)
+                    if (ballot(has(L_RUN) && nxf != 0) != 0) seg_flags |= FLAG_PHASE_CAP;
+                    nxf = 0;
+                    break;
+                }
+                // what is in flight, by kind (segment = wave)
+                const bool pr = (nxf & F_PR) != 0, cm = (nxf & F_CM) != 0;
+                const uint64_t kpp = ballot((nxf & F_PP) != 0), kpr = ballot(pr), kcm = ballot(cm);
+                const uint64_t kblk = ballot((nxf & F_BLK) != 0);
+                const uint64_t kcold = ballot((nxf & (F_OCM | F_RC | F_SYNC)) != 0);
+                uint32_t path = P_GENERAL;
+                PC c;
+                uint32_t j = 0, pp_h = 0, pp_T = 0, pp_eq = 0, blo = 0, bhi = 0;
+                if (kcold) {
+                    path = P_GENERAL;
+                } else if (kpp) {
+                    if ((kpr | kcm | kblk) == 0 && popc(kpp) == 1) {
+                        path = P_PP;
+                        j = ctz64(kpp);
+                        pp_h = uni(rl(h, j));
+                        pp_T = uni(rl(nx_ppT, j));
+                        pp_eq = uni(rl(nxf & F_PP_EQ, j));
+                    }
+                } else if ((kpr | kcm) == 0) {
+                    if (kblk == 0) {
+                        path = P_NONE;                           // only miner events this phase
+                    } else {
+                        const uint32_t jb = ctz64(kblk);
+                        blo = uni(rl(nx_blo, jb));
+                        bhi = uni(rl(nx_bhi, jb));
+                        const bool bk = (nxf & F_BLK) != 0;
+                        path = ballot(bk && (nx_blo != blo || nx_bhi != bhi)) == 0 ? P_BLK : P_GENERAL;
+                    }
+                } else if (kblk == 0) {
+                    const uint64_t cls = pp & BLK_HP_MASK;
+                    c.kpr = kpr; c.kcm = kcm;
+                    c.pr_h = c.cm_h = 0; c.pr_cls = c.cm_cls = 0;
+                    bool mm = false;
+                    if (kpr) {
+                        const uint32_t jp = ctz64(kpr);
+                        c.pr_h = uni(rl(h, jp));
+                        c.pr_cls = rl64(cls, jp);
+                        mm = pr && (h != c.pr_h || cls != c.pr_cls);
+                    }
+                    if (kcm) {
+                        const uint32_t jc = ctz64(kcm);
+                        c.cm_h = uni(rl(h, jc));
+                        c.cm_cls = rl64(cls, jc);
+                        mm = mm || (cm && (h != c.cm_h || cls != c.cm_cls));
+                    }
+                    if (ballot(mm) == 0) {
+                        path = P_PC;
+                        c.v1 = ballot(blk_var(pp) != 0);
+                    }
+                }
+                if (path == P_GENERAL) {                          // hand the instance to the full kernel
+                    save_state(p);
+                    if (me == 0) P.resume_flags[inst_local] = 1u;
+                    bailed = true;
+                    seg_done = true;
+                    break;
+                }
+                nxf = 0;
+                F64_STAMP(1);
+                F64_COUNT(8);
+                if (act) {
+                    // event step: Minner's NewHeader handler, for the validators with queued chain events
+                    if (ballot(has(L_RUN) && wake_tick < 0 && miner_queue != 0) != 0) miner_step_p();
+                    F64_STAMP(2);
+                    if (path != P_NONE) {
+                        const uint64_t mk = deliver_mask<1>(seed(), N, P.thr16, inst, (uint32_t)tick, p, me).w[0];
+                        if (path == P_PC) {
+                            const uint32_t off = offset_from_parts(seed(), N, off_tick, p, me);
+                            deliver_pc(has(L_RUN) && !has(L_DEAD), c, mk, off);
+                            F64_STAMP(4);
+                            F64_COUNT(10);
+                        } else if (path == P_PP) {
+                            handle_preprepare_p(has(L_RUN) && ((mk >> j) & 1ull) && !has(L_DEAD), j, pp_h,
+                                                blk_make(pp_h, j, 0, pp_T), pp_eq != 0);
+                            F64_STAMP(3);
+                            F64_COUNT(9);
+                        } else {                                  // P_BLK
+                            handle_blocks_p(has(L_RUN) && (mk & kblk & ~(1ull << me)) != 0, blo, bhi);
+                            F64_STAMP(5);
+                            F64_COUNT(11);
+                        }
+                    }
+                }
+                resolve_commits();
+                F64_STAMP(6);
+                if (frozen) act = false;
+            }
+            if (!seg_done && (frozen || canon_h >= P.heights)) { seg_done = true; done_tick = (uint32_t)tick + 1; }
+        }
+        if (!bailed) flush_rows();
+#ifdef BFT_STAMPS
+        F64_STAMP(7);
+        if (me == 0 && P.stamps)
+            for (int k = 0; k < 12; ++k) P.stamps[(uint64_t)inst_local * 12 + k] = st_acc[k];
+#endif
+        // this wave's histograms → the launch totals: every height recorded here was a round-0 commit
+        wv.sync();
+        if (P.hist) {
+            for (uint32_t b = me; b < 65u; b += 64u) {
+                const uint32_t v = lat[b];
+                if (v != 0) wv.gadd64(P.hist + 65u + b, v);
+            }
+            if (me == 0 && views_acc != 0) wv.gadd64(P.hist, views_acc);
+        }
+        uint32_t lf = lane_flags;
+        for (uint32_t m = 1; m < 64u; m <<= 1) lf |= wv.shfl_xor(lf, (int)m);
+        if (me == 0 && inst_local < P.n_instances && !bailed) {
+            uint32_t flags = lf | seg_flags;
+            if (!frozen && canon_h < P.heights) flags |= FLAG_TIMEOUT;
+            P.committed_height[inst_local] = canon_h < P.heights ? canon_h : P.heights;
+            P.flags[inst_local] = flags;
+            P.ticks[inst_local] = done_tick;
+            P.views[inst_local] = views_acc;
+        }
+    }
+};
+
+}  // namespace bft

@@ -20,14 +20,6 @@
 
 namespace bft {
 
-// build-time variants for A/B measurements (the defaults are the product)
-#ifndef BFT_PP_PATH
-#define BFT_PP_PATH 0          // single-Preprepare phases through the summary instead of LDS records
-#endif
-#ifndef BFT_LAZY_PUBLISH
-#define BFT_LAZY_PUBLISH 1     // publish outbox records to LDS only for general-path phases
-#endif
-
 constexpr int REC_WORDS = 22;            // LDS words per published outbox record
 
 // outbox record flags
@@ -45,7 +37,10 @@ struct Outbox {
     uint32_t blk_lo, blk_hi;
 };
 
-BFT_FN void outbox_clear(Outbox& o) {
+// Every field of a kind is written when its flag bit is set and read only while it is set, so an
+// empty outbox is f == 0 (the stale fields are never read: no per-phase register clearing).
+BFT_FN void outbox_clear(Outbox& o) { o.f = 0; }
+BFT_FN void outbox_init(Outbox& o) {
     o.f = 0;
     o.pp_h = o.pp_r = 0; o.pp_b = 0;
     o.pr_h = o.pr_r = 0; o.pr_d = 0;
@@ -74,19 +69,15 @@ BFT_FN void outbox_clear(Outbox& o) {
 //   [.., + L*32)                      per-lane commit hash
 //   [.., + 64*LANE_HASH_BUF)          per-lane header buffer of lane_block_hash (S <= 64; the
 //                                     workgroup kernels use a private buffer)
-// FAST kernel layout (F, S == 64): records are never published (a phase that would need them hands the
-// instance over first), so the record area shrinks to the commit hand-off (5 words per lane) and the
-// segment words to the one segment's 8: 4.9 KB per wave, 8 waves per SIMD (the full layout's 9.7 KB
-// allowed 4).
-template <uint32_t S, bool F = false>
+// (The N = 64 FAST kernel has its own, smaller layout: bft_fast64.h.)
+template <uint32_t S>
 struct Layout {
-    static_assert(!F || S == 64, "the FAST layout is for one instance per wave");
     static constexpr uint32_t L = S > 64 ? S : 64;
     static constexpr int NW = S > 64 ? (int)(S / 64) : 1;
     static constexpr int K = S > 64 ? 4 : 8;          // RoundChangeSet rounds kept per validator
-    static constexpr uint32_t CMT_STRIDE = F ? 5 : 8;  // words per lane of the commit hand-off
+    static constexpr uint32_t CMT_STRIDE = 8;          // words per lane of the commit hand-off
     static constexpr uint32_t REC_OFF = 0;
-    static constexpr uint32_t RC_OFF = REC_OFF + L * (F ? CMT_STRIDE : (uint32_t)REC_WORDS) * 4;
+    static constexpr uint32_t RC_OFF = REC_OFF + L * (uint32_t)REC_WORDS * 4;
     static constexpr uint32_t CMT_OFF = REC_OFF;
     static constexpr uint32_t CACHE_OFF = RC_OFF;
     static constexpr uint32_t HIST_OFF = CACHE_OFF + 12u * L * 4u;
@@ -97,7 +88,7 @@ struct Layout {
     static constexpr uint32_t GRP_OFF = SEG_OFF + 256;
     static constexpr uint32_t CHASH_OFF = SEG_OFF + 512;
     static constexpr uint32_t SCR_OFF = CHASH_OFF + L * 32;
-    static constexpr uint32_t BYTES_POW2 = F ? SEG_OFF + 32 : CHASH_OFF;
+    static constexpr uint32_t BYTES_POW2 = CHASH_OFF;
     static constexpr uint32_t BYTES_SEED = S > 64 ? SCR_OFF : SCR_OFF + 64 * LANE_HASH_BUF;
     static constexpr uint32_t bytes(bool need_seed) { return need_seed ? BYTES_SEED : BYTES_POW2; }
 };
@@ -108,24 +99,22 @@ BFT_FN uint32_t lds_bytes(uint32_t seg, bool need_seed) {
     return seg == 256 ? Layout<256>::bytes(need_seed) : seg == 128 ? Layout<128>::bytes(need_seed)
                                                                  : Layout<64>::bytes(need_seed);
 }
-BFT_FN uint32_t lds_bytes_fast() { return Layout<64, true>::BYTES_POW2; }
 
-// Kernel modes (S == 64 only for the last two):
+// Kernel modes:
 //   MODE_FULL    every path;
-//   MODE_FAST    the general one-message-at-a-time path is compiled out (a shorter hot loop and fewer
-//                live registers). A phase that needs it hands the instance over: its state is saved at
-//                the start of that phase (SAVE_WORDS per lane, P.save) and P.resume_flags is set;
-//   MODE_RESUME  the full kernel over the handed-over instances only, from their saved phase.
-constexpr int MODE_FULL = 0, MODE_FAST = 1, MODE_RESUME = 2;
+//   MODE_RESUME  (S == 64) the full kernel over the instances the N = 64 FAST kernel (bft_fast64.h)
+//                handed over, from their saved phase: the FAST kernel saves the state below
+//                (SAVE_WORDS per lane, P.save) at the start of a phase it has no closed form for and
+//                sets P.resume_flags.
+constexpr int MODE_FULL = 0, MODE_RESUME = 2;
 constexpr uint32_t SAVE_WORDS = 80;
 constexpr uint32_t SAVE_COLD = 72;   // words 72..78: outbox kinds that always take the general path
 
 template <class W, bool NEED_SEED, uint32_t S, int MODE = MODE_FULL>
 struct Sim {
-    static constexpr bool FAST = MODE == MODE_FAST;
     static constexpr bool RESUME = MODE == MODE_RESUME;
     static_assert(MODE == MODE_FULL || S == 64, "hand-over modes are for one instance per wave");
-    using LY = Layout<S, MODE == MODE_FAST>;
+    using LY = Layout<S>;
     static constexpr int NW = LY::NW;
     static constexpr int RCS_K = LY::K;
     static constexpr uint32_t LDS_REC_OFF = LY::REC_OFF, LDS_RC_OFF = LY::RC_OFF, LDS_CMT_OFF = LY::CMT_OFF,
@@ -208,7 +197,7 @@ struct Sim {
         mint_height = 0; miner_queue = 0; sync_pending = 0;
         cand = BLK_NONE;
         for (uint32_t k = 0; k < 12; ++k) *cache_p(k) = 0;
-        outbox_clear(nx);
+        outbox_init(nx);
         commit_x = 0; commit_round = 0; commit_seed = 0; commit_blk = 0;
         lane_flags = 0;
         off_inst = offset_inst_part(p.seed, inst);
@@ -280,36 +269,20 @@ struct Sim {
         if (nx.f & F_CM) { lane_flags |= FLAG_OUTBOX; return; }
         nx.f |= F_CM | (wild ? F_CM_W : 0u); nx.cm_h = vh; nx.cm_r = vr; nx.cm_d = d;
     }
-    // Old-block Commit, RoundChange and Sync always take the general path, which the FAST kernel
-    // does not have: there their fields go straight to the hand-over area (they are never read
-    // before the hand-over), keeping them out of the registers of the hot loop.
-    BFT_FN uint32_t* cold_p(uint32_t k) const {
-        return P.save + ((uint64_t)inst_local * LY::L + lane) * SAVE_WORDS + SAVE_COLD + k;
-    }
     BFT_FN void out_old_commit(uint32_t vh, uint32_t vr, uint64_t d, bool wild) {
         if (cache_hit(3, vh, vr, d)) return;
         if (nx.f & F_OCM) { lane_flags |= FLAG_OUTBOX; return; }
         nx.f |= F_OCM | (wild ? F_OCM_W : 0u);
-        if constexpr (FAST) {
-            *cold_p(0) = vh; *cold_p(1) = vr; *cold_p(2) = (uint32_t)d; *cold_p(3) = (uint32_t)(d >> 32);
-        } else {
-            nx.ocm_h = vh; nx.ocm_r = vr; nx.ocm_d = d;
-        }
+        nx.ocm_h = vh; nx.ocm_r = vr; nx.ocm_d = d;
     }
     BFT_FN void out_round_change(uint32_t vh, uint32_t vr) {
         if (nx.f & F_RC) { lane_flags |= FLAG_OUTBOX; return; }
         nx.f |= F_RC;
-        if constexpr (FAST) { *cold_p(4) = vh; *cold_p(5) = vr; }
-        else { nx.rc_h = vh; nx.rc_r = vr; }
+        nx.rc_h = vh; nx.rc_r = vr;
     }
     BFT_FN void out_sync(uint32_t height) {
-        if constexpr (FAST) {
-            if (nx.f & F_SYNC) { if (height < *cold_p(6)) *cold_p(6) = height; return; }
-            nx.f |= F_SYNC; *cold_p(6) = height;
-        } else {
-            if (nx.f & F_SYNC) { if (height < nx.sync_h) nx.sync_h = height; return; }
-            nx.f |= F_SYNC; nx.sync_h = height;
-        }
+        if (nx.f & F_SYNC) { if (height < nx.sync_h) nx.sync_h = height; return; }
+        nx.f |= F_SYNC; nx.sync_h = height;
     }
     BFT_FN void out_blocks(uint32_t lo, uint32_t hi) {
         if (lo > hi) return;
@@ -407,10 +380,7 @@ struct Sim {
 
     // ---------------------------------------------------------------- Core
     BFT_FN bool is_proposer(uint32_t who) const { return proposer == who; }
-    BFT_FN uint32_t mod_n(uint32_t x) const {
-        if constexpr (FAST) return x & 63u;
-        return P.nmask ? (x & P.nmask) : x % P.n;
-    }   // proposer index
+    BFT_FN uint32_t mod_n(uint32_t x) const { return P.nmask ? (x & P.nmask) : x % P.n; }   // proposer index
 
     // Core::check_message (core.rs:366-399): 0 ok, 1 unknown, 2 future block, 3 old, 4 future msg
     BFT_FN int check_message(int code, uint32_t vh) const { return check_message_class(code, vh, h, st); }
@@ -609,7 +579,6 @@ struct Sim {
     }
 
     BFT_FN void deliver_from(uint32_t s) {     // all messages of sender s (SPEC.md §2 order)
-        if constexpr (FAST) return;
         const uint32_t* m = rec_lds(seg_base + s);
         uint32_t f = m[0];
         if (f == 0) return;
@@ -653,9 +622,8 @@ struct Sim {
         if constexpr (S == 64) return wv.uni(v);
         else return v;
     }
-    // N and floor(2N/3): compile-time constants in the FAST kernel (launched only for N = 64)
-    BFT_FN uint32_t nval() const { if constexpr (FAST) return 64u; else return P.n; }
-    BFT_FN uint32_t qval() const { if constexpr (FAST) return 42u; else return P.q; }
+    BFT_FN uint32_t nval() const { return P.n; }
+    BFT_FN uint32_t qval() const { return P.q; }    // floor(2N/3)
     BFT_FN void sync() { wv.sync(); }
     BFT_FN uint32_t seg_max(uint32_t v) {
         if constexpr (S > 64) { return wv.grp_max(v); }
@@ -871,21 +839,15 @@ struct Sim {
         uint32_t pr_h, pr_r, cm_h, cm_r, blk_lo, blk_hi;
         uint64_t pr_cls, cm_cls;              // (height, proposer) class of the digests
         bool u_pr, u_cm, u_blk;               // one view / one digest class / one range
-        uint32_t pp_src, pp_h, pp_r, pp_eq;   // the Preprepare of a single-proposer phase
-        uint64_t pp_b;
     };
     // how a phase is delivered (segment-uniform): the closed forms read the summary only;
     // the general path reads the published LDS records in each receiver's rotated order
-    enum : uint32_t { PATH_GENERAL = 0, PATH_BLK = 1, PATH_PC = 2, PATH_PP = 3 };
+    enum : uint32_t { PATH_GENERAL = 0, PATH_BLK = 1, PATH_PC = 2 };
     BFT_FN uint32_t classify(const PhaseSummary& ps) const {
         if (!P.fast) return PATH_GENERAL;
         const bool rest = (ps.k_ocm | ps.k_rc | ps.k_sync).any();
         if (rest) return PATH_GENERAL;
-        if (ps.k_pp.any()) {
-            // one Preprepare and nothing else: arrival order cannot matter
-            if ((BFT_PP_PATH || FAST) && (ps.k_pr | ps.k_cm | ps.k_blk).none() && ps.k_pp.popc() == 1) return PATH_PP;
-            return PATH_GENERAL;
-        }
+        if (ps.k_pp.any()) return PATH_GENERAL;
         if (ps.k_pr.none() && ps.k_cm.none()) return (ps.k_blk.any() && ps.u_blk) ? PATH_BLK : PATH_GENERAL;
         if (ps.k_blk.none() && ps.u_pr && ps.u_cm) return PATH_PC;
         return PATH_GENERAL;
@@ -908,39 +870,22 @@ struct Sim {
         ps.k_pp = seg_bits(ballot((f & F_PP) != 0));
         ps.k_pr = seg_bits(ballot((f & F_PR) != 0));
         ps.k_cm = seg_bits(ballot((f & F_CM) != 0));
-        if constexpr (FAST) {
-            // these kinds always take the general path, which hands the instance over: one ballot
-            ps.k_ocm = seg_bits(ballot((f & (F_OCM | F_RC | F_SYNC)) != 0));
-            ps.k_rc = ps.k_sync = M::zero();
-        } else {
-            ps.k_ocm = seg_bits(ballot((f & F_OCM) != 0));
-            ps.k_rc = seg_bits(ballot((f & F_RC) != 0));
-            ps.k_sync = seg_bits(ballot((f & F_SYNC) != 0));
-        }
+        ps.k_ocm = seg_bits(ballot((f & F_OCM) != 0));
+        ps.k_rc = seg_bits(ballot((f & F_RC) != 0));
+        ps.k_sync = seg_bits(ballot((f & F_SYNC) != 0));
         ps.k_blk = seg_bits(ballot((f & F_BLK) != 0));
-        const bool pr = (f & F_PR) != 0, cm = (f & F_CM) != 0, bk = (f & F_BLK) != 0, pq = (f & F_PP) != 0;
+        const bool pr = (f & F_PR) != 0, cm = (f & F_CM) != 0, bk = (f & F_BLK) != 0;
         const bool prw = (f & F_PR_W) != 0, cmw = (f & F_CM_W) != 0;
         ps.pr_h = ps.pr_r = ps.cm_h = ps.cm_r = ps.blk_lo = ps.blk_hi = 0;
         ps.pr_cls = ps.cm_cls = 0;
         ps.pr_w = ps.pr_v0 = ps.pr_v1 = ps.cm_w = ps.cm_v0 = ps.cm_v1 = M::zero();
         ps.u_pr = ps.u_cm = ps.u_blk = true;
-        ps.pp_src = ps.pp_h = ps.pp_r = ps.pp_eq = 0;
-        ps.pp_b = 0;
         // leader of each kind (the first sender of the segment) and uniformity against it
         // (the wave-wide ballots equal the segment masks when the segment is the whole wave)
         bool any_pr = S == 64 ? ps.k_pr.any() : ballot(pr).any();
         bool any_cm = S == 64 ? ps.k_cm.any() : ballot(cm).any();
         bool any_bk = S == 64 ? ps.k_blk.any() : ballot(bk).any();
-        bool any_pp = S == 64 ? ps.k_pp.any() : ballot(pq).any();
         bool mm_pr = false, mm_cm = false, mm_blk = false;
-        if ((BFT_PP_PATH || FAST) && any_pp) {
-            uint32_t j = ps.k_pp.any() ? ps.k_pp.ctz_nz() : 0u;
-            ps.pp_src = j;
-            ps.pp_h = from_seg_lane(nx.pp_h, j);
-            ps.pp_r = from_seg_lane(nx.pp_r, j);
-            ps.pp_b = (uint64_t)from_seg_lane((uint32_t)nx.pp_b, j) | ((uint64_t)from_seg_lane((uint32_t)(nx.pp_b >> 32), j) << 32);
-            ps.pp_eq = from_seg_lane(f & F_PP_EQ, j);
-        }
         if (any_pr) {
             uint32_t j = ps.k_pr.any() ? ps.k_pr.ctz_nz() : 0u;
             uint64_t cls = nx.pr_d & BLK_HP_MASK;
@@ -1093,13 +1038,7 @@ struct Sim {
             BFT_STAMP(9);
             return;
         }
-        if ((BFT_PP_PATH || FAST) && path == PATH_PP) {   // deliver_from() of the single sender
-            if (mk.get(ps.pp_src) && !core_dead) handle_preprepare(ps.pp_src, ps.pp_h, ps.pp_r, ps.pp_b, ps.pp_eq != 0);
-            BFT_STAMP(8);
-            return;
-        }
         // general path: every delivered non-empty sender, in rotated order, one at a time
-        if constexpr (FAST) return;                   // never reached: FAST bails before (run)
         M any = ps.k_pp | ps.k_pr | ps.k_cm | ps.k_ocm | ps.k_rc | ps.k_sync | ps.k_blk;
         M c = rot(mk & any, off);
         while (c.any()) {
@@ -1112,36 +1051,21 @@ struct Sim {
         BFT_STAMP(10);
     }
 
-    // ---------------------------------------------------------------- bail / resume (FAST)
-    // persistent per-lane and segment state, word by word (lane g's SAVE_WORDS words contiguous:
-    // one base pointer with immediate offsets — a strided SoA made the compiler hoist 80 addresses)
+    // ---------------------------------------------------------------- resume (the FAST kernel's hand-over)
+    // persistent per-lane and segment state, word by word (lane g's SAVE_WORDS words contiguous):
+    // BFT_STATE_32, BFT_STATE_64, prep, comm, the 12 cache words, the bool bits (byz, core_dead,
+    // wait, frozen, seg_done), tick, phase; words SAVE_COLD.. hold the old-Commit / RoundChange / Sync
+    // outbox fields. Written by bft_fast64.h Fast64::save_state.
 #define BFT_STATE_32(X) X(h) X(r) X(st) X(n_rcs) X(proposer) X(last) X(last_seed) X(last_T) X(timer_tick) \
     X(rc_last_tick) X(wake_tick) X(mint_height) X(miner_queue) X(sync_pending) X(lane_flags) X(canon_h)       \
     X(done_tick) X(seg_flags) X(canon_tip_seed) X(canon_tick) X(nx.f) X(nx.pp_h) X(nx.pp_r) X(nx.pr_h)       \
     X(nx.pr_r) X(nx.cm_h) X(nx.cm_r) X(nx.blk_lo) X(nx.blk_hi)
 #define BFT_STATE_64(X) X(lock) X(pp) X(pend) X(cand) X(canon_tip) X(views_acc) X(nx.pp_b) X(nx.pr_d)       \
     X(nx.cm_d)
-    BFT_FN void save_state(uint32_t p) {
-        uint32_t* sv = P.save + ((uint64_t)inst_local * LY::L + lane) * SAVE_WORDS;
-#define save_p(k) (sv + (k))
-        uint32_t k = 0;
-#define BFT_SV32(f) *save_p(k++) = (uint32_t)(f);
-#define BFT_SV64(f) *save_p(k++) = (uint32_t)(f); *save_p(k++) = (uint32_t)((uint64_t)(f) >> 32);
-        BFT_STATE_32(BFT_SV32)
-        BFT_STATE_64(BFT_SV64)
-        for (int j = 0; j < NW; ++j) { BFT_SV64(prep.w[j]) BFT_SV64(comm.w[j]) }
-        for (uint32_t c = 0; c < 12; ++c) *save_p(k++) = *cache_p(c);
-        *save_p(k++) = (byz ? 1u : 0u) | (core_dead ? 2u : 0u) | (wait ? 4u : 0u) | (frozen ? 8u : 0u) |
-                       (seg_done ? 16u : 0u);
-        *save_p(k++) = (uint32_t)tick;
-        *save_p(k++) = p;
-        (void)k;                                       // k <= SAVE_COLD; the cold words are already stored
-#undef BFT_SV32
-#undef BFT_SV64
-    }
     BFT_FN void load_state(uint32_t& p) {
         const uint32_t* sv = P.save + ((uint64_t)inst_local * LY::L + lane) * SAVE_WORDS;
         uint32_t k = 0;
+#define save_p(k) (sv + (k))
 #define BFT_LD32(f) f = (decltype(f))*save_p(k++);
 #define BFT_LD64(f) { uint64_t lo_ = *save_p(k++); uint64_t hi_ = *save_p(k++); f = lo_ | (hi_ << 32); }
         BFT_STATE_32(BFT_LD32)
@@ -1182,7 +1106,6 @@ struct Sim {
         if (!resuming && P.byz_count > 0) init_byzantine();
         for (uint32_t b = lane; b < HIST_BINS; b += LY::L) *hist_slot(b) = 0;
         sync();
-        bool bailed = false;
         for (tick = tick0; tick < (int32_t)P.max_ticks; ++tick) {
             if (ballot(!seg_done).none()) break;
             bool act = running && !seg_done && !frozen;
@@ -1210,24 +1133,12 @@ struct Sim {
                 summarize(ps);
                 BFT_STAMP(1);
                 const uint32_t path = classify(ps);
-                if constexpr (FAST) {
-                    if (path == PATH_GENERAL) {               // hand the instance to the full kernel
-                        save_state(p);
-                        if (lane == 0) P.resume_flags[inst_local] = 1u;
-                        // wind down without an early exit (a `break` here costs ~25 VGPRs): nothing
-                        // is delivered, no phase or tick follows, no outputs are written
-                        bailed = true;
-                        seg_done = true;
-                        act = false;
-                    }
-                }
 #ifdef BFT_STAMPS
                 st_acc[6] += 1;                               // phases (a count, not cycles)
                 st_acc[11] += path == PATH_GENERAL ? 1 : 0;   // general-path phases
 #endif
                 // records go to LDS only if some segment of the wave takes the general path
-                // (never in FAST: its layout has no record area, and a general phase has handed over)
-                const bool pub = !FAST && (!BFT_LAZY_PUBLISH || ballot(path == PATH_GENERAL).any());
+                const bool pub = ballot(path == PATH_GENERAL).any();
                 if (pub) { publish(); sync(); }
                 else outbox_clear(nx);
                 BFT_STAMP(2);
@@ -1263,7 +1174,7 @@ struct Sim {
                 if (v != 0) wv.gadd64(P.hist + b, v);
             }
         }
-        if (me == 0 && inst_local < P.n_instances && !bailed) {
+        if (me == 0 && inst_local < P.n_instances) {
             uint32_t flags = lf | seg_flags;
             if (!frozen && canon_h < P.heights) flags |= FLAG_TIMEOUT;
             uint32_t chh = canon_h < P.heights ? canon_h : P.heights;

@@ -3,9 +3,11 @@
 // Kernels:
 //   bft_consensus_kernel  one 64-lane wave per 64/S instances (N <= 64), or one workgroup of
 //                         S = 128 / 256 lanes per instance (N <= 256); lane = validator (bft_wave.h);
-//   bft_hash_kernel       one lane per instance: Keccak-256 of every committed header, chained
-//                         through prev_hash (power-of-two N, where proposer seeds are always 0
-//                         and the consensus kernel does not need hashes);
+//   bft_consensus_fast_kernel  N = 64 with big-endian seeds: the closed-form phases (bft_fast64.h),
+//                         handing instances that need the general path to bft_consensus_resume_kernel;
+//   bft_hash_pair_kernel  one lane pair per instance: Keccak-256 of every committed header, chained
+//                         through prev_hash (big-endian seeds and power-of-two N, where proposer
+//                         seeds are always 0 and the consensus kernel does not need hashes);
 //   bft_stats_kernel      per-launch totals for the RCCL all-reduce of the benchmark.
 #include <hip/hip_runtime.h>
 
@@ -20,7 +22,7 @@
 #include "../../include/bftsim.h"
 #include "bft_common.h"
 #include "bft_wave.h"
-#include "bft_coop_hash.h"
+#include "bft_fast64.h"
 
 namespace bft {
 
@@ -157,19 +159,20 @@ __global__ __launch_bounds__(S > 64 ? S : 64, S > 64 ? 1 : BFT_WAVES_PER_SIMD) v
     }
 }
 
-// FAST kernel (N = 64, power of two): no general path; instances needing it are saved for resume
+// FAST kernel (N = 64, big-endian seeds): the closed-form phases only (bft_fast64.h); instances
+// needing the general path are saved for the resume kernel
 #ifndef BFT_FAST_WAVES_PER_SIMD
-#define BFT_FAST_WAVES_PER_SIMD 5   // 96 VGPRs + 92 B/lane of spills; measured best of 4..8 (LDS allows 8)
+#define BFT_FAST_WAVES_PER_SIMD 6   // measured best of 4..8 (profiles/r02: 4 → 3.86e8, 5 → 3.97e8, 6 → 4.17e8, 7 → 3.69e8)
 #endif
 __global__ __launch_bounds__(64, BFT_FAST_WAVES_PER_SIMD) void bft_consensus_fast_kernel(Params p) {
     extern __shared__ uint8_t lds[];
 #ifndef BFT_CONSENSUS_PRIO
 #define BFT_CONSENSUS_PRIO 2
 #endif
-    // win issue arbitration against the hash waves of the previous launch (measured +1%; the hash pass
-    // stretches into the issue gaps and still finishes within the step)
+    // win issue arbitration against the hash waves of the previous launch (the hash pass stretches into
+    // the issue gaps and still finishes within the step)
     __builtin_amdgcn_s_setprio(BFT_CONSENSUS_PRIO);
-    Sim<WaveHip, false, 64, MODE_FAST> sim(p, lds, blockIdx.x);
+    Fast64<WaveHip> sim(p, lds, blockIdx.x);
     sim.run();
 }
 // the full kernel over the instances the FAST kernel handed over, from their saved phase
@@ -205,37 +208,7 @@ static hipError_t launch_consensus(uint32_t seg, dim3 grid, size_t lds, hipStrea
     return hipGetLastError();
 }
 
-// one wave per instance: the cooperative Keccak of bft_coop_hash.h
-__global__ __launch_bounds__(64) void bft_hash_coop_kernel(Params p) {
-    __shared__ __attribute__((aligned(16))) uint8_t buf[COOP_BUF_BYTES];
-    hash_chain_wave<WaveHip>(p, blockIdx.x, buf);
-}
-
-// one lane per instance: the compact single-lane Keccak of bft_common.h
-__global__ __launch_bounds__(64) void bft_hash_lane_kernel(Params p) {
-    __shared__ __attribute__((aligned(16))) uint8_t bufs[64 * LANE_HASH_BUF];
-    uint32_t il = blockIdx.x * 64u + threadIdx.x;
-    if (il >= p.n_instances) return;
-    uint32_t inst = p.first_instance + il;
-    uint32_t ch = p.committed_height[il];
-    uint32_t prev[8];
-    for (int i = 0; i < 8; ++i)
-        prev[i] = (uint32_t)p.genesis_hash[4 * i] | ((uint32_t)p.genesis_hash[4 * i + 1] << 8) |
-                  ((uint32_t)p.genesis_hash[4 * i + 2] << 16) | ((uint32_t)p.genesis_hash[4 * i + 3] << 24);
-    uint8_t* buf = bufs + threadIdx.x * LANE_HASH_BUF;
-    for (uint32_t x = 1; x <= ch; ++x) {
-        const uint32_t* row = p.rec + ((uint64_t)il * p.rows + x) * 4;
-        uint32_t w1 = row[1];
-        uint32_t prop = w1 & 0xffffu, var = (w1 >> 16) & 1u, T = row[2];
-        uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)T + 1ull);
-        uint32_t out[8];
-        lane_block_hash(buf, prev, p.addresses + 20u * prop, p.seed, inst, x, prop, var, time, out);
-        uint32_t* dst = (uint32_t*)(p.hash + ((uint64_t)il * p.rows + x) * 32);
-        for (int i = 0; i < 8; ++i) { dst[i] = out[i]; prev[i] = out[i]; }
-    }
-}
-
-// one lane PAIR per instance (the default): the even lane holds the low 32-bit half of every
+// one lane PAIR per instance: the even lane holds the low 32-bit half of every
 // Keccak state word, the odd lane the high half. A 64-bit rotation is one v_alignbit_b32 of this
 // lane's half and the partner's (exchanged with one DPP quad_perm swap); theta parities, chi and iota
 // are half-local. Per lane and round ~125 VALU instead of ~205 for a whole state in one lane, and
@@ -420,7 +393,7 @@ struct bftsim {
     uint32_t* d_rcs = nullptr;        // RoundChangeSet tables, rcs_words(seg) per wave / workgroup
     uint32_t* d_resume = nullptr;     // FAST launches: [cap_inst] hand-over flags
     uint32_t* d_save = nullptr;       // FAST launches: [SAVE_WORDS][cap_inst * 64] saved lane state
-    int fast = 1;                     // FAST kernel + resume for N = 64 (BFTSIM_FAST=0 disables)
+    int fast = 1;                     // FAST kernel + resume for N = 64 (bftsim_set_fast(h, 0): full kernel)
     uint32_t window = 0;              // 0: full per-height rows; else ring of `window` rows
     uint64_t* d_trace = nullptr;
     uint64_t* h_trace = nullptr;
@@ -443,7 +416,6 @@ struct bftsim {
     uint32_t ring_head = 0;
     double acc_c = 0, acc_h = 0;
     uint32_t acc_n = 0;
-    int hash_mode = 0;   // 0: one lane pair per instance, 1: one wave (BFTSIM_HASH=coop), 2: one lane (=lane)
 };
 
 static int fail(bftsim* h, int code, const std::string& msg) {
@@ -547,12 +519,6 @@ int bftsim_create(const bftsim_config* cfg, int hip_device, bftsim_t** out) {
     h->genesis_seed = bft::seed_from_hash(h->genesis_hash, cfg->n, cfg->seed_byte_order == BFTSIM_SEED_LE);
     h->seg = bft::segment_size(cfg->n);
     h->hcap = cfg->heights + 64;
-    {
-        const char* hm = getenv("BFTSIM_HASH");
-        h->hash_mode = (hm && strcmp(hm, "coop") == 0) ? 1 : (hm && strcmp(hm, "lane") == 0) ? 2 : 0;
-        const char* fm = getenv("BFTSIM_FAST");
-        h->fast = (fm && strcmp(fm, "0") == 0) ? 0 : 1;
-    }
     *out = h;
     hipError_t e = hipSetDevice(hip_device);
     if (e != hipSuccess) return fail(h, BFTSIM_EHIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
@@ -633,6 +599,12 @@ int bftsim_set_window(bftsim_t* h, uint32_t window) {
     return BFTSIM_OK;
 }
 
+int bftsim_set_fast(bftsim_t* h, int on) {
+    if (!h) return BFTSIM_EINVAL;
+    h->fast = on != 0;
+    return BFTSIM_OK;
+}
+
 int bftsim_set_trace(bftsim_t* h, uint64_t* host_out, uint32_t trace_ticks) {
     if (!h) return BFTSIM_EINVAL;
     h->h_trace = host_out;
@@ -699,16 +671,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         if (h->set_busy[h->cur_set]) HIPCHECK(h, hipStreamWaitEvent(s, h->set_done[h->cur_set], 0));
         p.committed_height = h->d_ch; p.flags = h->d_flags; p.ticks = h->d_ticks; p.views = h->d_views;
         p.rec = h->d_rec; p.hash = h->d_hash;
-        if (!h->hs) {
-#ifdef BFT_HASH_LOW_PRIO
-            // the hash pass only has to finish before the next launch's hash pass: lowest stream priority
-            int lo = 0, hi = 0;
-            HIPCHECK(h, hipDeviceGetStreamPriorityRange(&lo, &hi));
-            HIPCHECK(h, hipStreamCreateWithPriority(&h->hs, hipStreamNonBlocking, lo));
-#else
-            HIPCHECK(h, hipStreamCreateWithFlags(&h->hs, hipStreamNonBlocking));
-#endif
-        }
+        if (!h->hs) HIPCHECK(h, hipStreamCreateWithFlags(&h->hs, hipStreamNonBlocking));
     }
     bftsim::LaunchEv& ev = h->ring[h->ring_head % bftsim::RING];
     if (ev.pending) {                                    // 64 launches unread: fold the oldest in
@@ -733,7 +696,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         p.save = h->d_save;
         p.save_stride = n * 64;
         HIPCHECK(h, hipMemsetAsync(h->d_resume, 0, n * 4, s));
-        hipLaunchKernelGGL(bft::bft_consensus_fast_kernel, dim3(grid), dim3(64), bft::lds_bytes_fast(), s, p);
+        hipLaunchKernelGGL(bft::bft_consensus_fast_kernel, dim3(grid), dim3(64), bft::lds_bytes_fast64(), s, p);
         HIPCHECK(h, hipGetLastError());
         hipLaunchKernelGGL(bft::bft_consensus_resume_kernel, dim3(grid), dim3(64), lds, s, p);
         HIPCHECK(h, hipGetLastError());
@@ -749,12 +712,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         hipStream_t t = pipe ? h->hs : s;
         if (pipe) HIPCHECK(h, hipStreamWaitEvent(t, ev.c1, 0));
         HIPCHECK(h, hipEventRecord(ev.h0, t));
-        if (h->hash_mode == 1)
-            hipLaunchKernelGGL(bft::bft_hash_coop_kernel, dim3((uint32_t)n), dim3(64), 0, t, p);
-        else if (h->hash_mode == 2)
-            hipLaunchKernelGGL(bft::bft_hash_lane_kernel, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, t, p);
-        else
-            hipLaunchKernelGGL(bft::bft_hash_pair_kernel, dim3((uint32_t)((n + 31) / 32)), dim3(64), 0, t, p);
+        hipLaunchKernelGGL(bft::bft_hash_pair_kernel, dim3((uint32_t)((n + 31) / 32)), dim3(64), 0, t, p);
         HIPCHECK(h, hipGetLastError());
         HIPCHECK(h, hipEventRecord(ev.h1, t));
         if (pipe) {

@@ -131,6 +131,9 @@ int bftsim_kernel_ms_sum(bftsim_t *h, double *consensus_ms, double *hash_ms, uin
  * bftsim_sync returns; bftsim_fetch/_stats_get/_fetch_summary read the last launch. Takes effect at
  * the next bftsim_prepare (buffers are re-allocated). */
 int bftsim_set_pipeline(bftsim_t *h, int on);
+/* verification switch: 0 runs N = 64 through the full kernel alone instead of the FAST kernel +
+ * resume (results are identical; the default 1 is the fast path) */
+int bftsim_set_fast(bftsim_t *h, int on);
 /* optional per-tick state digests of the next launch (debug; NULL disables) */
 int bftsim_set_trace(bftsim_t *h, uint64_t *host_out, uint32_t trace_ticks);
 /* windowed runs for long horizons (10,000 heights x 1M instances): keep only a ring

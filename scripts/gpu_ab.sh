@@ -1,17 +1,13 @@
 #!/bin/bash
-# A/B of library builds on the cfg3 bench (used through gpurun): each build runs twice
+# A/B of library builds on the cfg3 bench (through gpurun): scripts/gpu_ab.sh <suffix>... ("" = product)
 set -o pipefail
-mkdir -p gpurun_out
+mkdir -p gpurun_out/ab
 export PYTHONUNBUFFERED=1
-rm -f gpurun_out/ab.txt
-for v in "$@"; do
-  for rep in 1 2; do
-    BFTSIM_LIB=consensus-rs_amd/build/$v.so timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/ab_one.json 2>> gpurun_out/ab.err || exit 1
-    python - "$v" "$rep" >> gpurun_out/ab.txt <<'PY'
-import json, sys
-d = json.load(open("gpurun_out/ab_one.json"))
-print(sys.argv[1], "rep" + sys.argv[2], round(d["value"] / 1e6, 2), "M/s", d["roofline"]["kernel_ms"])
-PY
+for lib in "$@"; do
+  f=consensus-rs_amd/build/libbftsim${lib:+_$lib}.so
+  [ "$lib" = "prod" ] && f=consensus-rs_amd/build/libbftsim.so
+  for i in 1 2; do
+    BFTSIM_LIB=$f timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/ab/$lib.$i.json 2>> gpurun_out/ab/ab.err || exit $?
+    python -c "import json; d=json.load(open('gpurun_out/ab/$lib.$i.json')); r=d['roofline']['kernel_ms']; print('$lib', round(d['value']/1e6,1), 'M/s  consensus', round(r['bft_consensus_kernel'],3), 'ms  hash', round(r['bft_hash_kernel'],3), 'ms')"
   done
 done
-cat gpurun_out/ab.txt

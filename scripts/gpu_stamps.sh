@@ -14,11 +14,12 @@ for _ in range(2):
     sim.sync()
 out = (ctypes.c_uint64 * 12)()
 runtime.lib().bftsim_debug_stamps(out)
-names = ["t_step", "summarize", "publish+sync", "deliver?", "resolve", "mask+offset", "#phases", "loop/other", "fast_blk", "fast_pc", "general", "#general"]
-tot = sum(out[k] for k in range(12) if k not in (6, 11))
-print("phases per wave-height", out[6] / (16384 * 100.0), "general", out[11] / (16384 * 100.0))
+names = ["t_step", "classify", "event_step", "deliver_pp", "deliver_pc", "deliver_blk", "resolve", "loop/other", "#phases", "#pp", "#pc", "#blk"]
+cnt = (8, 9, 10, 11)
+tot = sum(out[k] for k in range(12) if k not in cnt)
+print("per wave-height: phases", out[8] / (16384 * 100.0), "pp", out[9] / 1638400.0, "pc", out[10] / 1638400.0, "blk", out[11] / 1638400.0)
 for k in range(12):
-    print(f"{names[k]:14s} {out[k]:16d} {100.0*out[k]/max(tot,1):6.2f}%")
+    print(f"{names[k]:14s} {out[k]:16d} {100.0*out[k]/max(tot,1):6.2f}%  {out[k]/1638400.0:9.1f} per wave-height")
 print("kernel ms", sim.kernel_ms())
 PY
 rc=$?

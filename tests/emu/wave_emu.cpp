@@ -14,7 +14,7 @@
 
 #include "../../consensus-rs_amd/csrc/bft_host.h"
 #include "../../consensus-rs_amd/csrc/bft_wave.h"
-#include "../../consensus-rs_amd/csrc/bft_coop_hash.h"
+#include "../../consensus-rs_amd/csrc/bft_fast64.h"
 
 namespace {
 
@@ -34,7 +34,6 @@ struct Sched {
     const bft::Params* P;
     uint8_t* lds;
     uint32_t wave;
-    int body;   // 0 consensus, 1 hash post-pass
     bool fast;  // FAST kernel (S == 64, power-of-two N)
 };
 thread_local Sched* g = nullptr;
@@ -117,7 +116,7 @@ template <bool NS, uint32_t S>
 void run_sim() {
     if constexpr (S == 64 && !NS) {
         if (g->fast) {                     // bft_consensus_fast_kernel
-            bft::Sim<EmuWave, false, 64, bft::MODE_FAST> sim(*g->P, g->lds, g->wave);
+            bft::Fast64<EmuWave> sim(*g->P, g->lds, g->wave);
             sim.run();
             return;
         }
@@ -153,24 +152,16 @@ void run_sim_seg(bool ns, uint32_t seg) {
 }
 
 void lane_entry(int lane) {
-    if (g->body == 1) {
-        bft::hash_chain_wave<EmuWave>(*g->P, g->wave, g->lds);
-        g->done[lane] = true;
-        g->op[lane] = 0;
-        return;
-    }
     run_sim_seg(g->P->need_seed != 0, g->P->seg);
     g->done[lane] = true;
     g->op[lane] = 0;
 }
 
-int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds, int body = 0, int nl = 64,
-             bool fast = false) {
+int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds, int nl = 64, bool fast = false) {
     static thread_local Sched s;
     g = &s;
     s.fast = fast;
     s.nl = nl;
-    s.body = body;
     s.P = &P;
     s.lds = lds.data();
     s.wave = wave;
@@ -268,7 +259,7 @@ extern "C" int emu_run_stream(const bftsim_config* cfg, uint64_t first, uint64_t
     P.rcs = rcs.data();
     for (uint32_t w = 0; w < waves; ++w) {
         memset(lds.data(), 0xcd, lds.size());
-        if (run_wave(P, w, lds, 0, seg > 64 ? (int)seg : 64)) return -1;
+        if (run_wave(P, w, lds, seg > 64 ? (int)seg : 64)) return -1;
     }
     for (uint64_t i = 0; i < n; ++i) {
         uint32_t ch = committed[i];
@@ -319,16 +310,16 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
         save.assign((size_t)n * 64 * bft::SAVE_WORDS, 0xcdcdcdcdu);
         P.resume_flags = resume.data();
         P.save = save.data();
-        std::vector<uint8_t> lds_fast(bft::lds_bytes_fast());     // the FAST kernel's exact LDS size
+        std::vector<uint8_t> lds_fast(bft::lds_bytes_fast64());   // the FAST kernel's exact LDS size
         for (uint32_t w = 0; w < waves; ++w) {
             memset(lds_fast.data(), 0xcd, lds_fast.size());
-            if (run_wave(P, w, lds_fast, 0, 64, true)) return -1;
+            if (run_wave(P, w, lds_fast, 64, true)) return -1;
         }
         P.resume_mode = 1;
     }
     for (uint32_t w = 0; w < waves; ++w) {
         memset(lds.data(), 0xcd, lds.size());
-        if (run_wave(P, w, lds, 0, seg > 64 ? (int)seg : 64)) return -1;
+        if (run_wave(P, w, lds, seg > 64 ? (int)seg : 64)) return -1;
     }
     P.resume_mode = 0;
     if (fast && getenv("BFT_EMU_FAST_REPORT")) {
@@ -336,31 +327,23 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
         for (uint64_t i = 0; i < n; ++i) nb += resume[i];
         fprintf(stderr, "emu: FAST handed over %llu of %llu instances\n", (unsigned long long)nb, (unsigned long long)n);
     }
-    // power-of-two N: the hash post-pass, as bft_hash_coop_kernel (one wave per instance,
-    // BFTSIM_HASH=coop) or bft_hash_lane_kernel (one lane per instance, default)
+    // the hash post-pass (bft_hash_pair_kernel computes the same Keccak-256 chain, two lanes per state)
     if (!P.need_seed) {
-        const char* hm = getenv("BFTSIM_HASH");
-        if (hm && strcmp(hm, "coop") == 0) {
-            std::vector<uint8_t> buf(bft::COOP_BUF_BYTES + 64);
-            for (uint64_t il = 0; il < n; ++il)
-                if (run_wave(P, (uint32_t)il, buf, 1)) return -1;
-        } else {
-            alignas(16) uint8_t buf[bft::LANE_HASH_BUF];
-            for (uint64_t il = 0; il < n; ++il) {
-                uint32_t prev[8];
-                for (int i = 0; i < 8; ++i)
-                    prev[i] = (uint32_t)gh[4 * i] | ((uint32_t)gh[4 * i + 1] << 8) | ((uint32_t)gh[4 * i + 2] << 16) |
-                              ((uint32_t)gh[4 * i + 3] << 24);
-                for (uint32_t x = 1; x <= ch[il]; ++x) {
-                    const uint32_t* row = &rec[(il * hcap + x) * 4];
-                    uint32_t prop = row[1] & 0xffffu, var = (row[1] >> 16) & 1u;
-                    uint64_t time = cfg->genesis_time + (uint64_t)cfg->block_period * ((uint64_t)row[2] + 1ull);
-                    uint32_t out[8];
-                    bft::lane_block_hash(buf, prev, cfg->addresses + 20u * prop, cfg->seed, (uint32_t)(first + il), x,
-                                         prop, var, time, out);
-                    memcpy(&hs[(il * hcap + x) * 32], out, 32);
-                    for (int i = 0; i < 8; ++i) prev[i] = out[i];
-                }
+        alignas(16) uint8_t buf[bft::LANE_HASH_BUF];
+        for (uint64_t il = 0; il < n; ++il) {
+            uint32_t prev[8];
+            for (int i = 0; i < 8; ++i)
+                prev[i] = (uint32_t)gh[4 * i] | ((uint32_t)gh[4 * i + 1] << 8) | ((uint32_t)gh[4 * i + 2] << 16) |
+                          ((uint32_t)gh[4 * i + 3] << 24);
+            for (uint32_t x = 1; x <= ch[il]; ++x) {
+                const uint32_t* row = &rec[(il * hcap + x) * 4];
+                uint32_t prop = row[1] & 0xffffu, var = (row[1] >> 16) & 1u;
+                uint64_t time = cfg->genesis_time + (uint64_t)cfg->block_period * ((uint64_t)row[2] + 1ull);
+                uint32_t out[8];
+                bft::lane_block_hash(buf, prev, cfg->addresses + 20u * prop, cfg->seed, (uint32_t)(first + il), x,
+                                     prop, var, time, out);
+                memcpy(&hs[(il * hcap + x) * 32], out, 32);
+                for (int i = 0; i < 8; ++i) prev[i] = out[i];
             }
         }
     }

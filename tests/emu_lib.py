@@ -15,7 +15,7 @@ from bftsim import _abi  # noqa: E402
 EMU_DIR = os.path.join(ROOT, "tests", "emu")
 LIB = os.path.join(EMU_DIR, "libwave_emu.so")
 SRCS = [os.path.join(EMU_DIR, "wave_emu.cpp")] + [
-    os.path.join(ROOT, "consensus-rs_amd", "csrc", f) for f in ("bft_wave.h", "bft_common.h", "bft_host.h", "bft_coop_hash.h")]
+    os.path.join(ROOT, "consensus-rs_amd", "csrc", f) for f in ("bft_wave.h", "bft_fast64.h", "bft_common.h", "bft_host.h")]
 
 _lib = None
 
@@ -23,8 +23,11 @@ _lib = None
 def build():
     if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(s) for s in SRCS):
         return
+    # build to a private name and rename: concurrent test workers never load a half-written library
+    tmp = f"{LIB}.{os.getpid()}.tmp"
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unknown-pragmas",
-                           "-o", LIB, SRCS[0]])
+                           "-o", tmp, SRCS[0]])
+    os.replace(tmp, LIB)
 
 
 def lib():

@@ -1,6 +1,6 @@
 """Randomized parity fuzz: CPU wave emulator (the kernel body) vs the oracle on random configs.
 Usage: python tests/fuzz_parity.py [seconds] [rng seed] [big]. `big` draws N in 65..256 (the
-workgroup-segment kernels). Test-only tool (not collected by pytest)."""
+workgroup-segment kernels), `n64` N = 64 (the FAST kernel and its hand-overs). Test-only tool (not collected by pytest)."""
 import random
 import sys
 import time
@@ -11,8 +11,10 @@ from bftsim.configs import BftConfig
 from parity_util import mismatches
 
 
-def random_config(rng, big=False):
-    if big:
+def random_config(rng, big=False, n64=False):
+    if n64:                              # the FAST kernel (bft_fast64.h) and its hand-overs
+        n = 64
+    elif big:
         n = rng.choice([65, 66, 80, 100, 127, 128, 129, 150, 200, 255, 256])
     else:
         n = rng.choice([1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 16, 17, 21, 31, 32, 33, 40, 63, 64])
@@ -31,9 +33,10 @@ def main():
     budget = float(sys.argv[1]) if len(sys.argv) > 1 else 60
     rng = random.Random(int(sys.argv[2]) if len(sys.argv) > 2 else 1234)
     big = len(sys.argv) > 3 and sys.argv[3] == "big"
+    n64 = len(sys.argv) > 3 and sys.argv[3] == "n64"
     t0, runs, fails = time.time(), 0, 0
     while time.time() - t0 < budget:
-        cfg = random_config(rng, big)
+        cfg = random_config(rng, big, n64)
         first = rng.randrange(1 << 20)
         n_inst = rng.choice([1, 2] if big else [1, 3, 8])
         a = O.run(cfg, first, n_inst)

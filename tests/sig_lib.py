@@ -20,7 +20,9 @@ _lib = None
 def build():
     if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(s) for s in SRCS):
         return
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unknown-pragmas", "-o", LIB, SRCS[0]])
+    tmp = f"{LIB}.{os.getpid()}.tmp"      # private name + rename: safe under concurrent test workers
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unknown-pragmas", "-o", tmp, SRCS[0]])
+    os.replace(tmp, LIB)
 
 
 def lib():

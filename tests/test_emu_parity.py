@@ -1,5 +1,6 @@
-"""The HIP kernel body (bft_wave.h, bft_coop_hash.h) run by the CPU wave emulator against the
-oracle, bit for bit: both hash post-passes, closed-form fast paths on and off, all segment sizes."""
+"""The HIP kernel bodies (bft_wave.h, bft_fast64.h) run by the CPU wave emulator against the oracle,
+bit for bit: closed-form fast paths on and off, the N = 64 FAST kernel with its hand-overs, all
+segment sizes."""
 import pytest
 
 import oracle_lib as O
@@ -53,13 +54,6 @@ def test_emulated_kernel_matches_oracle(name, mk, first, n):
     assert_same(O.run(cfg, first, n), E.run(cfg, first, n), name)
 
 
-@pytest.mark.parametrize("mode", ["coop", "lane"])
-def test_both_hash_postpasses(mode, monkeypatch):
-    monkeypatch.setenv("BFTSIM_HASH", mode)
-    cfg = cfg2(heights=15)
-    assert_same(O.run(cfg, 100, 4), E.run(cfg, 100, 4), mode)
-
-
 def test_fast_paths_off_is_identical(monkeypatch):
     cfg = BftConfig(n=8, heights=20, seed=33, drop_ppm=120_000, byz_count=2)
     fast = E.run(cfg, 0, 8)
@@ -96,7 +90,7 @@ def test_emulated_windowed_run_matches_streamed_oracle(name, mk, first, n, windo
 @pytest.mark.parametrize("name,mk", [("cfg3", lambda: cfg3(heights=8)),
                                      ("cfg4-n64", lambda: cfg4(64, heights=8))])
 def test_full_kernel_alone_n64(name, mk, monkeypatch):
-    """BFTSIM_FAST=0 on the GPU: the full kernel runs N = 64 by itself."""
+    """bftsim_set_fast(h, 0) on the GPU: the full kernel runs N = 64 by itself."""
     monkeypatch.setenv("BFT_EMU_FAST", "0")
     cfg = mk()
     assert_same(O.run(cfg, 0, 2), E.run(cfg, 0, 2), name + " full kernel")

@@ -72,7 +72,13 @@ def test_gpu_matches_oracle(name, mk, first, n):
                                        ("n64-byz21-drop5", lambda: BftConfig(n=64, heights=20, seed=15, byz_count=21,
                                                                              drop_ppm=50_000), 8)])
 def test_gpu_full_kernel_alone_n64(name, mk, n, monkeypatch):
-    """BFTSIM_FAST=0: N = 64 through the full kernel alone (no FAST kernel, no hand-over)."""
-    monkeypatch.setenv("BFTSIM_FAST", "0")
+    """bftsim_set_fast(h, 0): N = 64 through the full kernel alone (no FAST kernel, no hand-over)."""
+    from bftsim.runtime import Simulator
     cfg = mk()
-    assert_same(O.run(cfg, 0, n), gpu_run(cfg, 0, n), name + " full kernel")
+    sim = Simulator(cfg)
+    try:
+        sim.set_fast(False)
+        got = sim.run(0, n)
+    finally:
+        sim.close()
+    assert_same(O.run(cfg, 0, n), got, name + " full kernel")
