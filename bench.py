@@ -14,6 +14,11 @@ Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the roofline mode
 hashes; the rounds-to-commit and commit-latency histograms are all-reduced over RCCL and printed.
 One step takes ~11 s on one MI355X: run it with --steps 1 --warmup 0.
 
+`--workload cfg2` / `cfg4` / `drop64` measure the other consensus configurations (not the headline):
+cfg2 = 65,536 instances N=4, 10 % drops (BASELINE configs[1]); cfg4 = 16,384 instances of one N of the
+validator sweep with proposer crashes (`--n`, default 256: the workgroup-segment kernel); drop64 = 16,384
+instances N=64 f=21 with 5 % drops (most instances hand over from the FAST kernel to the resume kernel).
+
 `--workload sig` measures the real-crypto row (not the headline): one step =
 secp256k1 public-key recovery (`GossipMessage::address`, src/protocol/mod.rs:103-116) of a batch of
 262,144 signed 32-byte digests per GPU resident in HBM (libbftsig, include/bftsig.h).
@@ -57,12 +62,19 @@ HEADER_HASH_OPS = 14_976                # 2 Keccak-f[1600] x 24 rounds x 156 64-
 ALGO_BYTES_PER_VIEW = 48
 
 
-def pmc_traffic():
-    """HBM bytes per dispatch per kernel from the newest committed PMC summary
-    (profiles/<round>/pmc_summary.json, written by scripts/pmc_summary.py from rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes of this same bench command)."""
+def _pmc_files(workload: str):
+    """The committed PMC summaries of a workload, oldest first: profiles/<round>/pmc_summary.json for the
+    headline (cfg3), profiles/<round>/<workload>/pmc_summary.json for the others."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")))
+    sub = "" if workload == "cfg3" else workload
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", "*", sub, "pmc_summary.json")))
+
+
+def pmc_traffic(workload: str = "cfg3"):
+    """HBM bytes per dispatch per kernel from the newest committed PMC summary of this workload
+    (written by scripts/pmc_summary.py from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
+    same bench command)."""
+    files = _pmc_files(workload)
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -73,11 +85,10 @@ def pmc_traffic():
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2   # wave64 VALU instructions/s: one per 2 cycles per SIMD (SIMD-32)
 
 
-def pmc_issue():
-    """Per dispatch VALU / SALU wave-instructions of the FAST consensus kernel from the newest PMC
-    summary (SQ_INSTS_VALU, SQ_INSTS_SALU of scripts/gpu_profile.sh's SQ pass), or None."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")))
+def pmc_issue(workload: str = "cfg3"):
+    """Per dispatch VALU / SALU wave-instructions of the consensus kernel from the newest PMC
+    summary of this workload (SQ_INSTS_VALU, SQ_INSTS_SALU of scripts/gpu_profile.sh's SQ pass), or None."""
+    files = _pmc_files(workload)
     if not files:
         return None
     k = json.load(open(files[-1])).get("kernels", {})
@@ -85,6 +96,17 @@ def pmc_issue():
     if "SQ_INSTS_VALU" not in e:
         return None
     return {"valu": e["SQ_INSTS_VALU"], "salu": e.get("SQ_INSTS_SALU")}
+
+
+def cfg_desc(cfg) -> str:
+    d = [f"N={cfg.n}"]
+    if cfg.byz_count:
+        d.append(f"f={cfg.byz_count} equivocating")
+    if cfg.drop_ppm:
+        d.append(f"{cfg.drop_ppm / 1e4:g}% drop")
+    if cfg.proposer_crash_ppm:
+        d.append(f"proposer crash p={cfg.proposer_crash_ppm / 1e6:g}")
+    return ", ".join(d)
 
 
 def usable_cpus() -> int:
@@ -141,7 +163,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=("cfg3", "cfg5", "sig", "wire", "msgpath"), default="cfg3")
+    ap.add_argument("--workload", choices=("cfg3", "cfg2", "cfg4", "drop64", "cfg5", "sig", "wire", "msgpath"),
+                    default="cfg3")
+    ap.add_argument("--n", type=int, default=256, help="cfg4: validators per instance")
     ap.add_argument("--instances", type=int, default=None, help="instances per GPU")
     ap.add_argument("--heights", type=int, default=None)
     ap.add_argument("--window", type=int, default=256, help="cfg5: canonical rows kept per instance")
@@ -164,16 +188,17 @@ def main():
 
     import torch
     import torch.distributed as dist
-    from bftsim.configs import cfg3, cfg5
+    from bftsim.configs import BftConfig, cfg2, cfg3, cfg4, cfg5
     from bftsim.distributed import all_reduce_stats
     from bftsim.runtime import Simulator
     c5 = args.workload == "cfg5"
+    wl = args.workload
     if args.instances is None:
-        args.instances = 131_072 if c5 else 16_384
+        args.instances = {"cfg5": 131_072, "cfg2": 65_536}.get(wl, 16_384)
     if args.heights is None:
         args.heights = 10_000 if c5 else 100
     if args.cpu_sample is None:
-        args.cpu_sample = 512 if c5 else 16_384
+        args.cpu_sample = {"cfg5": 512, "cfg2": 16_384, "cfg4": 1024 if args.n > 64 else 8192}.get(wl, 16_384)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -184,7 +209,16 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    cfg = cfg5(heights=args.heights) if c5 else cfg3(heights=args.heights)
+    if wl == "cfg5":
+        cfg = cfg5(heights=args.heights)
+    elif wl == "cfg2":
+        cfg = cfg2(heights=args.heights)
+    elif wl == "cfg4":
+        cfg = cfg4(args.n, heights=args.heights)
+    elif wl == "drop64":
+        cfg = BftConfig(n=64, heights=args.heights, seed=15, byz_count=21, drop_ppm=50_000, name="drop64")
+    else:
+        cfg = cfg3(heights=args.heights)
     if args.seed_order == "le":
         import dataclasses
         cfg = dataclasses.replace(cfg, seed_byte_order=1, name=cfg.name + "-le")
@@ -242,7 +276,7 @@ def main():
         # dominant kernel by device time
         c_ops = consensus_ops_per_view(cfg.n) * views_rank
         h_ops = HEADER_HASH_OPS * st["committed_heights"]
-        if c5 or cfg.seed_byte_order:     # windowed runs / LE seeds hash inside the consensus kernel
+        if c5 or cfg.seed_byte_order or (cfg.n & (cfg.n - 1)):   # block hashes inside the consensus kernel
             c_ops, h_ops = c_ops + h_ops, 0
         if cms >= hms:
             dom, ops, ms = "bft_consensus_kernel", c_ops, cms
@@ -250,7 +284,7 @@ def main():
             dom, ops, ms = "bft_hash_kernel", h_ops, hms
         achieved = ops / (ms / 1e3) / 1e12
         peak = VALU_PEAK / 1e12
-        traffic, traffic_src = pmc_traffic()
+        traffic, traffic_src = pmc_traffic(wl)
         algo_bytes = ALGO_BYTES_PER_VIEW * views_rank
         def trim(h):
             h = list(h)
@@ -258,7 +292,8 @@ def main():
                 h.pop()
             return h
         out = {
-            "metric": METRIC_CFG5 if c5 else METRIC,
+            "metric": METRIC if wl == "cfg3" else METRIC_CFG5 if c5 else (
+                f"{wl} instance-rounds/sec (whole node), {cfg_desc(cfg)}; bit-exact"),
             "value": value,
             "unit": "instance-rounds/s",
             "n_gpus": world,
@@ -273,8 +308,8 @@ def main():
             "config": {
                 "workload": (f"cfg5: {I} instances per GPU, N=7, 5% drop, {args.heights} heights, "
                              f"window {args.window}") if c5 else
-                            (f"cfg3: {I} instances per GPU, N=64, f=21 equivocating, "
-                             f"{args.heights} heights" + (", little-endian U128 seeds" if cfg.seed_byte_order else "")),
+                            (f"{wl}: {I} instances per GPU, {cfg_desc(cfg)}, {args.heights} heights" +
+                             (", little-endian U128 seeds" if cfg.seed_byte_order else "")),
                 "instances_per_gpu": I, "n_validators": cfg.n, "byzantine": cfg.byz_count,
                 "instances_total": args.instances if args.scaling == "strong" else args.instances * world,
                 "seed_byte_order": "le" if cfg.seed_byte_order else "be",
@@ -292,10 +327,10 @@ def main():
                 "traffic": (traffic or {}).get(dom),
                 # what the hardware issues, beside the algorithmic model: VALU wave-instructions of
                 # the profiled launch (PMC) per second of this run's kernel time vs the issue peak
-                "issue": (lambda q: None if q is None or c5 or dom != "bft_consensus_kernel" else {
+                "issue": (lambda q: None if q is None or dom != "bft_consensus_kernel" else {
                     "valu_wave_instr_per_launch": q["valu"], "salu_wave_instr_per_launch": q["salu"],
                     "valu_per_s": q["valu"] / (ms / 1e3), "valu_peak_per_s": VALU_ISSUE_PEAK,
-                    "valu_frac": q["valu"] / (ms / 1e3) / VALU_ISSUE_PEAK})(pmc_issue()),
+                    "valu_frac": q["valu"] / (ms / 1e3) / VALU_ISSUE_PEAK})(pmc_issue(wl)),
                 "traffic_source": traffic_src,
                 "hbm": {"algorithmic_bytes": algo_bytes, "achieved_GBps": algo_bytes / (ms / 1e3) / 1e9,
                         "peak_GBps": HBM_PEAK / 1e9, "frac": algo_bytes / (ms / 1e3) / HBM_PEAK},

@@ -32,7 +32,11 @@ struct F64Layout {
     static constexpr uint32_t CACHE_WORDS = 8;                 // 4 kinds (PP, PR, CM, old CM) x 2
     static constexpr uint32_t RING_OFF = CACHE_OFF + CACHE_WORDS * 64 * 4;   // 64 canonical rows x 16 B
     static constexpr uint32_t LAT_OFF = RING_OFF + 64 * 16;    // commit-latency histogram (65 words)
-    static constexpr uint32_t BYTES = LAT_OFF + 65 * 4 + 4;
+    // cold per-lane state (SoA [word][lane]): sync_pending, rc_last_tick, pend's time tick, the outbox
+    // Preprepare's time tick, the lane's result flags — off the registers of the hot loop
+    static constexpr uint32_t LANE_OFF = LAT_OFF + 65 * 4 + 4;
+    static constexpr uint32_t W_SYNC = 0, W_RCLT = 1, W_PENDT = 2, W_PPT = 3, W_LFL = 4, LANE_WORDS = 5;
+    static constexpr uint32_t BYTES = LANE_OFF + LANE_WORDS * 64 * 4;
 };
 constexpr uint32_t lds_bytes_fast64() { return F64Layout::BYTES; }
 
@@ -41,7 +45,7 @@ struct Fast64 {
     static constexpr uint32_t N = 64, Q = 42;   // floor(2N/3) (validator.rs:149-154)
     // lane flag bits
     static constexpr uint32_t L_ST = 7u, L_WAIT = 8u, L_LOCK = 16u, L_BYZ = 32u, L_RUN = 64u, L_DEAD = 128u,
-                              L_PENDV = 256u, L_CMT = 512u;
+                              L_PENDV = 256u, L_CMT = 512u, L_PROP = 1024u;   // L_PROP: proposer is set (= 0)
     enum : uint32_t { P_GENERAL = 0, P_BLK = 1, P_PC = 2, P_PP = 3, P_NONE = 4 };
 
     const Params& P;
@@ -59,12 +63,11 @@ struct Fast64 {
     // per lane (Core + RoundState + chain tip + miner + timers + outbox)
     uint32_t fl;                       // L_* bits; state in bits 0..2
     uint32_t h;
-    uint64_t pp, prep, comm;
-    uint32_t pend_T, cand_T, proposer, last;
-    int32_t last_T, timer_tick, rc_last_tick, wake_tick;
-    uint32_t mint_height, miner_queue, sync_pending;
-    uint32_t nxf, nx_ppT, nx_blo, nx_bhi;
-    uint32_t lane_flags;
+    uint64_t pp, prep, comm;            // MessageManage sender sets (protocol/mod.rs:176-209)
+    uint32_t cand_T, last;
+    int32_t last_T, timer_tick, wake_tick;
+    uint32_t mint_height, miner_queue;
+    uint32_t nxf, nx_blo, nx_bhi;
 #ifdef BFT_STAMPS
     uint64_t st_acc[12];
     uint64_t st_t;
@@ -89,11 +92,11 @@ struct Fast64 {
         canon_tip = 0; views_acc = 0; byz_mask = 0;
         tick = 0;
         h = 0; pp = BLK_NONE; prep = comm = 0;
-        pend_T = cand_T = 0; proposer = 0xffffffffu; last = 0;
-        last_T = -1; timer_tick = -1; rc_last_tick = 0; wake_tick = -1;
-        mint_height = 0; miner_queue = 0; sync_pending = 0;
-        nxf = 0; nx_ppT = 0; nx_blo = nx_bhi = 0;
-        lane_flags = 0;
+        cand_T = 0; last = 0;
+        last_T = -1; timer_tick = -1; wake_tick = -1;
+        mint_height = 0; miner_queue = 0;
+        for (uint32_t k = 0; k < F64Layout::LANE_WORDS; ++k) *lane_p(k) = 0;
+        nxf = 0; nx_blo = nx_bhi = 0;
         for (uint32_t k = 0; k < F64Layout::CACHE_WORDS; ++k) *cache_p(k) = 0;
         off_inst = offset_inst_part(p.seed, inst);
         off_tick = 0;
@@ -108,6 +111,8 @@ struct Fast64 {
         BFT_OPAQUE_SGPR(hi);
         return (uint64_t)lo | ((uint64_t)hi << 32);
     }
+    BFT_FN uint32_t* lane_p(uint32_t w) const { return (uint32_t*)(lds + F64Layout::LANE_OFF) + w * 64u + me; }
+    BFT_FN uint32_t proposer() const { return has(L_PROP) ? 0u : 0xffffffffu; }
     BFT_FN uint32_t st() const { return fl & L_ST; }
     BFT_FN void set_st(uint32_t s) { fl = (fl & ~L_ST) | s; }
     BFT_FN bool has(uint32_t b) const { return (fl & b) != 0; }
@@ -153,14 +158,14 @@ struct Fast64 {
         const bool upd = c && !(cd != 0 && ch == vh && cd == d32);   // cache miss: the message goes out
         if (upd) { cp[0] = vh; cp[64] = d32; }
         const bool dup = upd && (nxf & flag) != 0;                     // a second one of its kind this phase
-        lane_flags |= dup ? FLAG_OUTBOX : 0u;
+        if (dup) *lane_p(F64Layout::W_LFL) |= FLAG_OUTBOX;
         const bool put = upd && !dup;
         nxf |= put ? (flag | (has(L_BYZ) ? wflag : 0u)) : 0u;
         return put;
     }
     BFT_FN void out_preprepare_p(bool c) {                       // view (h, 0), own candidate; equivocates iff Byzantine
         const bool put = send_kind(c, 0, h, cand(), F_PP, F_PP_EQ);
-        nx_ppT = put ? cand_T : nx_ppT;
+        if (put) *lane_p(F64Layout::W_PPT) = cand_T;
     }
     BFT_FN void out_prepare_p(bool c) { send_kind(c, 1, h, pp, F_PR, F_PR_W); }   // (h, 0, pp)
     BFT_FN void out_commit_p(bool c) { send_kind(c, 2, h, pp, F_CM, F_CM_W); }
@@ -176,13 +181,13 @@ struct Fast64 {
         const uint32_t d32 = blk_d32(d);
         if (cp[64] != 0 && cp[0] == vh && cp[64] == d32) return;
         cp[0] = vh; cp[64] = d32;
-        if (nxf & F_OCM) { lane_flags |= FLAG_OUTBOX; return; }
+        if (nxf & F_OCM) { *lane_p(F64Layout::W_LFL) |= FLAG_OUTBOX; return; }
         nxf |= F_OCM | (has(L_BYZ) ? F_OCM_W : 0u);
         uint32_t* s = save_p() + SAVE_COLD;
         s[0] = vh; s[1] = 0; s[2] = (uint32_t)d; s[3] = (uint32_t)(d >> 32);
     }
     BFT_FN void out_round_change(uint32_t vh, uint32_t vr) {
-        if (nxf & F_RC) { lane_flags |= FLAG_OUTBOX; return; }
+        if (nxf & F_RC) { *lane_p(F64Layout::W_LFL) |= FLAG_OUTBOX; return; }
         nxf |= F_RC;
         uint32_t* s = save_p() + SAVE_COLD;
         s[4] = vh; s[5] = vr;
@@ -267,13 +272,13 @@ struct Fast64 {
         h = c ? last + 1 : h;
         fl = c ? ((fl & ~(L_ST | L_WAIT | L_LOCK | L_PENDV)) | ST_ACCEPT_REQUEST) : fl;
         pp = c ? BLK_NONE : pp;
-        prep = c ? 0ull : prep;
+        prep = c ? 0ull : prep;                                  // MessageManage::new
         comm = c ? 0ull : comm;
-        proposer = c ? 0u : proposer;                            // (seed 0 + round 0) mod 64
+        fl |= c ? L_PROP : 0u;                                   // proposer = (seed 0 + round 0) mod 64
         timer_tick = c ? tick + 1 : timer_tick;                  // new_round_change_timer
     }
     BFT_FN void send_preprepare_cand_p(bool c) {                 // preprepare.rs:30-43, req = candidate
-        const bool s = c && h == mint_height && proposer == me;
+        const bool s = c && h == mint_height && has(L_PROP) && me == 0;
         if (ballot(s) != 0) {                                    // the proposer (validator 0) proposes
             bool cr = false;
             if (P.crash_on) cr = proposer_crashed(seed(), P.crash_thr32, 1u, inst, h, 0);
@@ -285,7 +290,7 @@ struct Fast64 {
         start_new_zero_round_p(c);
         const bool pv = c && h == mint_height;                   // accept the own candidate
         fl |= pv ? L_PENDV : 0u;
-        pend_T = pv ? cand_T : pend_T;
+        if (pv) *lane_p(F64Layout::W_PENDT) = cand_T;
         send_preprepare_cand_p(pv);
     }
     BFT_FN void miner_mine_p(bool c) {                           // minner/mod.rs:95-143
@@ -306,8 +311,8 @@ struct Fast64 {
     }
     BFT_FN void new_round_change_timer() { timer_tick = tick + 1; }
     BFT_FN void send_round_change(uint32_t round) {              // round_change.rs:38-63 (cold)
-        if (rc_last_tick == tick) { new_round_change_timer(); return; }
-        rc_last_tick = tick;
+        if ((int32_t)*lane_p(F64Layout::W_RCLT) == tick) { new_round_change_timer(); return; }
+        *lane_p(F64Layout::W_RCLT) = (uint32_t)tick;
         if (0u < round) { fl |= L_WAIT; new_round_change_timer(); }   // catchup_round (core.rs:555-565)
         out_round_change(h, round);
     }
@@ -321,10 +326,11 @@ struct Fast64 {
         wake_tick = w ? -1 : wake_tick;
         if (ballot(w) != 0) handle_new_header_event_p(w);
         if (ballot(run && wake_tick < 0 && miner_queue != 0) != 0) miner_step_p();
-        const bool sp = run && sync_pending != 0;
+        const uint32_t spv = *lane_p(F64Layout::W_SYNC);
+        const bool sp = run && spv != 0;
         if (ballot(sp) != 0) {
-            if (sp && last < sync_pending) out_sync(last + 1);
-            sync_pending = sp ? 0u : sync_pending;
+            if (sp && last < spv) out_sync(last + 1);
+            if (sp) *lane_p(F64Layout::W_SYNC) = 0;
         }
         const bool tm = run && !has(L_DEAD) && timer_tick == tick;   // TimerEvent (core.rs:207-225)
         if (ballot(tm) != 0) {
@@ -357,7 +363,7 @@ struct Fast64 {
                 }
             }
         }
-        go = go && proposer == src;                              // else NotFromProposer
+        go = go && has(L_PROP) && src == 0;                      // else NotFromProposer
         const uint32_t bh = blk_h(b);
         const bool bad = go && (bh == 0 || bh - 1 > last);       // Backend::verify: unknown ancestor
         const bool acc = go && !bad && st() == ST_ACCEPT_REQUEST;
@@ -414,8 +420,15 @@ struct Fast64 {
         const int rp = check_message_class(MT_PREPARE, c.pr_h, h, s0);
         const int rm = check_message_class(MT_COMMIT, c.cm_h, h, s0);
         // FutureBlockMessage → the delayed sync check (core.rs:58-69)
-        sync_pending = (prd != 0 && rp == CM_FUTURE_BLOCK && c.pr_h > sync_pending) ? c.pr_h : sync_pending;
-        sync_pending = (cmd != 0 && rm == CM_FUTURE_BLOCK && c.cm_h > sync_pending) ? c.cm_h : sync_pending;
+        const bool fpr = prd != 0 && rp == CM_FUTURE_BLOCK, fcm = cmd != 0 && rm == CM_FUTURE_BLOCK;
+        if (ballot(fpr || fcm) != 0) {
+            if (fpr || fcm) {
+                uint32_t v = *lane_p(F64Layout::W_SYNC);
+                v = (fpr && c.pr_h > v) ? c.pr_h : v;
+                v = (fcm && c.cm_h > v) ? c.cm_h : v;
+                *lane_p(F64Layout::W_SYNC) = v;
+            }
+        }
         const uint64_t PRacc = (rp == CM_OK && c.pr_h == h) ? prd : 0ull;
         const uint64_t CMacc = (rm == CM_OK && c.cm_h == h) ? (cmd & class_match_k(c.kcm, c.v1, c.cm_cls, pp)) : 0ull;
         // Order-free evaluation first. The delivery order (rotation by `off`) only matters when the
@@ -508,12 +521,12 @@ struct Fast64 {
         flush_rows();
         uint32_t* s = save_p();
         const uint64_t lock = has(L_LOCK) ? pp : BLK_NONE;
-        const uint64_t pend = has(L_PENDV) ? blk_make(h, me, 0, pend_T) : BLK_NONE;
+        const uint64_t pend = has(L_PENDV) ? blk_make(h, me, 0, *lane_p(F64Layout::W_PENDT)) : BLK_NONE;
         const uint64_t cd = mint_height ? cand() : BLK_NONE;
-        const uint64_t ppb = blk_make(h, me, 0, nx_ppT);
-        const uint32_t w32[29] = {h, 0u, st(), 0u, proposer, last, 0u, (uint32_t)last_T, (uint32_t)timer_tick,
-                                  (uint32_t)rc_last_tick, (uint32_t)wake_tick, mint_height, miner_queue,
-                                  sync_pending, lane_flags, canon_h, done_tick, seg_flags, 0u, canon_tick, nxf,
+        const uint64_t ppb = blk_make(h, me, 0, *lane_p(F64Layout::W_PPT));
+        const uint32_t w32[29] = {h, 0u, st(), 0u, proposer(), last, 0u, (uint32_t)last_T, (uint32_t)timer_tick,
+                                  *lane_p(F64Layout::W_RCLT), (uint32_t)wake_tick, mint_height, miner_queue,
+                                  *lane_p(F64Layout::W_SYNC), *lane_p(F64Layout::W_LFL), canon_h, done_tick, seg_flags, 0u, canon_tick, nxf,
                                   h, 0u, h, 0u, h, 0u, nx_blo, nx_bhi};
         uint32_t k = 0;
         for (uint32_t i = 0; i < 29; ++i) s[k++] = w32[i];
@@ -575,7 +588,7 @@ struct Fast64 {
             F64_STAMP(7);
             // the T-step, only when some running validator has a tick event
             if (ballot(has(L_RUN) && (tick == 0 || wake_tick == tick || (wake_tick < 0 && miner_queue != 0) ||
-                                      sync_pending != 0 || (!has(L_DEAD) && timer_tick == tick))) != 0) {
+                                      *lane_p(F64Layout::W_SYNC) != 0 || (!has(L_DEAD) && timer_tick == tick))) != 0) {
                 t_step();
             }
             F64_STAMP(0);
@@ -601,7 +614,7 @@ struct Fast64 {
                         path = P_PP;
                         j = ctz64(kpp);
                         pp_h = uni(rl(h, j));
-                        pp_T = uni(rl(nx_ppT, j));
+                        pp_T = uni(rl(*lane_p(F64Layout::W_PPT), j));
                         pp_eq = uni(rl(nxf & F_PP_EQ, j));
                     }
                 } else if ((kpr | kcm) == 0) {
@@ -690,7 +703,7 @@ struct Fast64 {
             }
             if (me == 0 && views_acc != 0) wv.gadd64(P.hist, views_acc);
         }
-        uint32_t lf = lane_flags;
+        uint32_t lf = *lane_p(F64Layout::W_LFL);
         for (uint32_t m = 1; m < 64u; m <<= 1) lf |= wv.shfl_xor(lf, (int)m);
         if (me == 0 && inst_local < P.n_instances && !bailed) {
             uint32_t flags = lf | seg_flags;

@@ -1,14 +1,17 @@
 #!/bin/bash
-# Copy the summaries of a scripts/gpu_profile.sh run (gpurun_out/prof) into profiles/<round>/ (tracked).
+# Copy the summaries of scripts/gpu_profile.sh runs (gpurun_out/prof/<workload>) into profiles/<round>/
+# (tracked): the headline (cfg3) at profiles/<round>/, every other workload at profiles/<round>/<workload>/.
+# usage: scripts/save_profile.sh <round> <workload>...
 set -e
-R=${1:-r01}
-D=profiles/$R
-mkdir -p $D/pmc
-cp gpurun_out/prof/stats/run_kernel_stats.csv $D/kernel_stats.csv
-cp gpurun_out/prof/stats/run_kernel_trace.csv $D/kernel_trace.csv
-cp gpurun_out/prof/pmc_summary.json $D/pmc_summary.json
-for p in fetch write sq; do cp gpurun_out/prof/$p/run_counter_collection.csv $D/pmc/${p}_counter_collection.csv; done
-cp gpurun_out/bench.json $D/bench.json
-cp gpurun_out/host_cpu.txt $D/host_cpu.txt
-[ -f gpurun_out/gpu_parity.log ] && tail -3 gpurun_out/gpu_parity.log > $D/gpu_parity_tail.txt || true
-echo "saved to $D"
+RND=$1; shift
+for W in "$@"; do
+  S=gpurun_out/prof/$W
+  [ "$W" = cfg3 ] && D=profiles/$RND || D=profiles/$RND/$W
+  mkdir -p $D/pmc
+  cp $S/stats/run_kernel_stats.csv $D/kernel_stats.csv
+  cp $S/pmc_summary.json $D/pmc_summary.json
+  for p in fetch write sq; do cp $S/$p/run_counter_collection.csv $D/pmc/${p}_counter_collection.csv; done
+  cp $S/bench.json $D/bench.json
+  cp $S/host_cpu.txt $D/host_cpu.txt
+  echo "saved $W to $D"
+done
