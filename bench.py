@@ -110,7 +110,16 @@ def cfg_desc(cfg) -> str:
 
 
 def usable_cpus() -> int:
-    return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    """CPUs this process may use: the affinity mask, capped by the cgroup CPU quota (a container
+    limited to 16 CPUs of a 256-CPU host runs 256 threads slower than 16)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def cpu_baseline(cfg, sample: int, threads: int, name: str = "cfg3"):
@@ -135,9 +144,11 @@ def cpu_baseline(cfg, sample: int, threads: int, name: str = "cfg3"):
     out = dict(value=views / secs, unit="instance-rounds/s", cores=threads, kind="port",
                sample=f"{sample} {name} instances ({views} instance-rounds) on {threads} threads, "
                       f"{secs:.1f} s", host=host_cpu())
-    if threads != 16:
-        v16, s16 = timed(sample, 16)
-        out["threads_16"] = dict(value=v16 / s16, sample=f"{sample} instances on 16 threads, {s16:.1f} s")
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else threads
+    if aff > threads:                         # the affinity mask, oversubscribing the quota
+        va, sa = timed(sample, aff)
+        out["affinity_threads"] = dict(value=va / sa, threads=aff,
+                                       sample=f"{sample} instances on {aff} threads, {sa:.1f} s")
     if name != "cfg5":                        # also the single-thread rate
         s1 = max(1, sample // 64)
         v1, t1 = timed(s1, 1)
@@ -173,6 +184,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each step's block-hash pass on the launch stream (no overlap across steps)")
+    ap.add_argument("--pipeline-depth", type=int, default=None,
+                    help="row-table sets in the launch ring (bftsim_set_pipeline); default 3, and 6 at <= 2,048 "
+                         "instances per GPU where the hash chains' latency, not the GPU, bounds a launch")
     ap.add_argument("--seed-order", choices=("be", "le"), default="be",
                     help="U128 byte order of randon_seed (validator.rs:39-48; include/bftsim.h BFTSIM_SEED_*)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
@@ -224,13 +238,15 @@ def main():
         cfg = dataclasses.replace(cfg, seed_byte_order=1, name=cfg.name + "-le")
     sim = Simulator(cfg, device=local)
     pipelined = not c5 and not args.no_pipeline
-    sim.set_pipeline(pipelined)
     if args.scaling == "strong":
         from bftsim.distributed import strong_shard
         first, I = strong_shard(rank, world, args.instances)
     else:
         I = args.instances
         first = rank * I
+    if args.pipeline_depth is None:
+        args.pipeline_depth = 6 if I <= 2048 else 3     # profiles/r02/curve: best per shard size
+    sim.set_pipeline(pipelined, args.pipeline_depth)
     if c5:
         sim.set_window(args.window)
     sim.prepare(I)
@@ -314,7 +330,7 @@ def main():
                 "instances_total": args.instances if args.scaling == "strong" else args.instances * world,
                 "seed_byte_order": "le" if cfg.seed_byte_order else "be",
                 "heights": args.heights, "parallelism": f"instance-sharded x{world}",
-                "pipelined": pipelined,
+                "pipelined": pipelined, "pipeline_depth": args.pipeline_depth if pipelined else 0,
                 "instance_rounds_per_step": views_all,
                 "committed_heights_per_step": heights_all,
                 "safety_violations": safety_all, "timeouts": timeout_all,

@@ -182,9 +182,10 @@ class Simulator:
         """Verification switch: False runs N = 64 through the full kernel alone (identical results)."""
         _check(self.h, lib().bftsim_set_fast(self.h, 1 if on else 0), "bftsim_set_fast")
 
-    def set_pipeline(self, on: bool):
-        """Batch throughput mode: hash pass of launch k overlaps the consensus of launch k+1."""
-        _check(self.h, lib().bftsim_set_pipeline(self.h, 1 if on else 0), "bftsim_set_pipeline")
+    def set_pipeline(self, on, depth: int = 2):
+        """Batch throughput mode: a ring of `depth` row-table sets; the hash pass of each launch overlaps
+        the following launches (include/bftsim.h bftsim_set_pipeline)."""
+        _check(self.h, lib().bftsim_set_pipeline(self.h, depth if on else 0), "bftsim_set_pipeline")
 
     def stats(self):
         s = _abi.CStats()

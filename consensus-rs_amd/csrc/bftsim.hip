@@ -402,14 +402,19 @@ struct bftsim {
     uint64_t last_n = 0, last_first = 0;
     hipStream_t last_stream = nullptr;
     // pipelined launches (bftsim_set_pipeline): two row-table sets used alternately, the hash pass of
-    // launch k on its own stream `hs`, overlapping the consensus kernel of launch k+1
-    int pipeline = 0;
-    hipStream_t hs = nullptr;
-    uint32_t* alt_ch = nullptr; uint32_t* alt_flags = nullptr; uint32_t* alt_ticks = nullptr;
-    uint64_t* alt_views = nullptr; uint32_t* alt_rec = nullptr; uint8_t* alt_hash = nullptr;
-    hipEvent_t set_done[2] = {nullptr, nullptr};    // hash pass of the last launch that used set 0 / 1
-    bool set_busy[2] = {false, false};
-    uint32_t cur_set = 0;
+    // launch k on the set's own stream, overlapping the consensus kernels of the following launches
+    // (and, with more than two sets, the hash passes of other launches: bftsim_set_pipeline)
+    static constexpr uint32_t MAX_SETS = 8;
+    struct RowSet {
+        uint32_t* ch = nullptr; uint32_t* flags = nullptr; uint32_t* ticks = nullptr; uint64_t* views = nullptr;
+        uint32_t* rec = nullptr; uint8_t* hash = nullptr;
+        hipStream_t hs = nullptr;     // the set's hash stream
+        hipEvent_t done = nullptr;    // hash pass of the last launch that used the set
+        bool busy = false;
+    } sets[MAX_SETS];
+    int pipeline = 0;                 // number of row-table sets (0: no pipelining)
+    uint32_t n_sets = 0, cur_set = 0;
+    hipStream_t hs = nullptr;         // the hash stream of the last pipelined launch
     // per-launch kernel timing: a ring of event quadruples, read by bftsim_kernel_ms_sum
     static constexpr uint32_t RING = 64;
     struct LaunchEv { hipEvent_t c0, c1, h0, h1; bool has_hash, pending; } ring[RING] = {};
@@ -429,16 +434,25 @@ static int fail(bftsim* h, int code, const std::string& msg) {
     } while (0)
 
 static void free_bufs(bftsim* h) {
-    (void)hipFree(h->d_ch); (void)hipFree(h->d_flags); (void)hipFree(h->d_ticks); (void)hipFree(h->d_views);
-    (void)hipFree(h->d_rec); (void)hipFree(h->d_hash); (void)hipFree(h->d_trace); (void)hipFree(h->d_tips);
-    (void)hipFree(h->d_rcs);
+    // the per-height row tables are owned by the sets (set 0 = the unpipelined tables); d_ch .. d_hash
+    // only point at the set of the last launch
+    if (h->n_sets == 0) {
+        (void)hipFree(h->d_ch); (void)hipFree(h->d_flags); (void)hipFree(h->d_ticks); (void)hipFree(h->d_views);
+        (void)hipFree(h->d_rec); (void)hipFree(h->d_hash);
+    }
+    for (uint32_t k = 0; k < h->n_sets; ++k) {
+        bftsim::RowSet& r = h->sets[k];
+        (void)hipFree(r.ch); (void)hipFree(r.flags); (void)hipFree(r.ticks); (void)hipFree(r.views);
+        (void)hipFree(r.rec); (void)hipFree(r.hash);
+        r.ch = r.flags = r.ticks = nullptr; r.views = nullptr; r.rec = nullptr; r.hash = nullptr;
+    }
+    (void)hipFree(h->d_trace); (void)hipFree(h->d_tips); (void)hipFree(h->d_rcs);
     h->d_rcs = nullptr;
     (void)hipFree(h->d_resume); (void)hipFree(h->d_save);
     h->d_resume = nullptr; h->d_save = nullptr;
-    (void)hipFree(h->alt_ch); (void)hipFree(h->alt_flags); (void)hipFree(h->alt_ticks); (void)hipFree(h->alt_views);
-    (void)hipFree(h->alt_rec); (void)hipFree(h->alt_hash);
-    h->alt_ch = h->alt_flags = h->alt_ticks = nullptr; h->alt_views = nullptr; h->alt_rec = nullptr; h->alt_hash = nullptr;
-    h->set_busy[0] = h->set_busy[1] = false;
+    for (uint32_t k = 0; k < bftsim::MAX_SETS; ++k) h->sets[k].busy = false;
+    h->n_sets = 0;
+    h->cur_set = 0;
     h->d_ch = h->d_flags = h->d_ticks = nullptr; h->d_views = nullptr;
     h->d_rec = nullptr; h->d_hash = nullptr; h->d_trace = nullptr; h->d_tips = nullptr;
     h->cap_inst = 0;
@@ -450,7 +464,8 @@ static void free_bufs(bftsim* h) {
 static int sync_all(bftsim* h) {
     HIPCHECK(h, hipSetDevice(h->device));
     HIPCHECK(h, hipStreamSynchronize(h->last_stream));
-    if (h->hs) HIPCHECK(h, hipStreamSynchronize(h->hs));
+    for (uint32_t k = 0; k < bftsim::MAX_SETS; ++k)
+        if (h->sets[k].hs) HIPCHECK(h, hipStreamSynchronize(h->sets[k].hs));
     return BFTSIM_OK;
 }
 
@@ -532,7 +547,8 @@ int bftsim_create(const bftsim_config* cfg, int hip_device, bftsim_t** out) {
         HIPCHECK(h, hipEventCreate(&h->ring[i].c0)); HIPCHECK(h, hipEventCreate(&h->ring[i].c1));
         HIPCHECK(h, hipEventCreate(&h->ring[i].h0)); HIPCHECK(h, hipEventCreate(&h->ring[i].h1));
     }
-    for (int i = 0; i < 2; ++i) HIPCHECK(h, hipEventCreateWithFlags(&h->set_done[i], hipEventDisableTiming));
+    for (uint32_t i = 0; i < bftsim::MAX_SETS; ++i)
+        HIPCHECK(h, hipEventCreateWithFlags(&h->sets[i].done, hipEventDisableTiming));
     return BFTSIM_OK;
 }
 
@@ -547,8 +563,10 @@ void bftsim_destroy(bftsim_t* h) {
         if (h->ring[i].h0) (void)hipEventDestroy(h->ring[i].h0);
         if (h->ring[i].h1) (void)hipEventDestroy(h->ring[i].h1);
     }
-    for (int i = 0; i < 2; ++i) if (h->set_done[i]) (void)hipEventDestroy(h->set_done[i]);
-    if (h->hs) (void)hipStreamDestroy(h->hs);
+    for (uint32_t i = 0; i < bftsim::MAX_SETS; ++i) {
+        if (h->sets[i].done) (void)hipEventDestroy(h->sets[i].done);
+        if (h->sets[i].hs) (void)hipStreamDestroy(h->sets[i].hs);
+    }
     delete h;
 }
 
@@ -574,13 +592,18 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         HIPCHECK(h, hipMalloc(&h->d_resume, n * 4));
         HIPCHECK(h, hipMalloc(&h->d_save, (uint64_t)bft::SAVE_WORDS * n * 64 * 4));
     }
-    if (h->pipeline) {
-        HIPCHECK(h, hipMalloc(&h->alt_ch, n * 4));
-        HIPCHECK(h, hipMalloc(&h->alt_flags, n * 4));
-        HIPCHECK(h, hipMalloc(&h->alt_ticks, n * 4));
-        HIPCHECK(h, hipMalloc(&h->alt_views, n * 8));
-        HIPCHECK(h, hipMalloc(&h->alt_rec, n * h->hcap * 16));
-        HIPCHECK(h, hipMalloc(&h->alt_hash, n * h->hcap * 32));
+    h->sets[0].ch = h->d_ch; h->sets[0].flags = h->d_flags; h->sets[0].ticks = h->d_ticks;
+    h->sets[0].views = h->d_views; h->sets[0].rec = h->d_rec; h->sets[0].hash = h->d_hash;
+    h->n_sets = 1;
+    for (uint32_t k = 1; k < (uint32_t)h->pipeline; ++k) {
+        bftsim::RowSet& r = h->sets[k];
+        HIPCHECK(h, hipMalloc(&r.ch, n * 4));
+        HIPCHECK(h, hipMalloc(&r.flags, n * 4));
+        HIPCHECK(h, hipMalloc(&r.ticks, n * 4));
+        HIPCHECK(h, hipMalloc(&r.views, n * 8));
+        HIPCHECK(h, hipMalloc(&r.rec, n * h->hcap * 16));
+        HIPCHECK(h, hipMalloc(&r.hash, n * h->hcap * 32));
+        h->n_sets = k + 1;
     }
     h->cap_inst = n;
     h->n_req = n;
@@ -662,16 +685,19 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         g_stamp_waves = waves;
     }
 #endif
-    const bool pipe = h->pipeline && !p.need_seed && h->alt_rec;
+    const bool pipe = h->pipeline >= 2 && !p.need_seed && h->n_sets >= 2;
     if (pipe) {
-        // alternate row-table sets: the hash pass of launch k-1 may still be reading the other one
-        std::swap(h->d_ch, h->alt_ch); std::swap(h->d_flags, h->alt_flags); std::swap(h->d_ticks, h->alt_ticks);
-        std::swap(h->d_views, h->alt_views); std::swap(h->d_rec, h->alt_rec); std::swap(h->d_hash, h->alt_hash);
-        h->cur_set ^= 1u;
-        if (h->set_busy[h->cur_set]) HIPCHECK(h, hipStreamWaitEvent(s, h->set_done[h->cur_set], 0));
+        // the next row-table set in the ring: the hash pass of the launch that used it last may still be
+        // reading it
+        h->cur_set = (h->cur_set + 1) % h->n_sets;
+        bftsim::RowSet& r = h->sets[h->cur_set];
+        if (r.busy) HIPCHECK(h, hipStreamWaitEvent(s, r.done, 0));
+        h->d_ch = r.ch; h->d_flags = r.flags; h->d_ticks = r.ticks; h->d_views = r.views;
+        h->d_rec = r.rec; h->d_hash = r.hash;
         p.committed_height = h->d_ch; p.flags = h->d_flags; p.ticks = h->d_ticks; p.views = h->d_views;
         p.rec = h->d_rec; p.hash = h->d_hash;
-        if (!h->hs) HIPCHECK(h, hipStreamCreateWithFlags(&h->hs, hipStreamNonBlocking));
+        if (!r.hs) HIPCHECK(h, hipStreamCreateWithFlags(&r.hs, hipStreamNonBlocking));
+        h->hs = r.hs;
     }
     bftsim::LaunchEv& ev = h->ring[h->ring_head % bftsim::RING];
     if (ev.pending) {                                    // 64 launches unread: fold the oldest in
@@ -709,15 +735,15 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     ev.has_hash = !p.need_seed;
     ev.pending = true;
     if (!p.need_seed) {
-        hipStream_t t = pipe ? h->hs : s;
+        hipStream_t t = pipe ? h->sets[h->cur_set].hs : s;
         if (pipe) HIPCHECK(h, hipStreamWaitEvent(t, ev.c1, 0));
         HIPCHECK(h, hipEventRecord(ev.h0, t));
         hipLaunchKernelGGL(bft::bft_hash_pair_kernel, dim3((uint32_t)((n + 31) / 32)), dim3(64), 0, t, p);
         HIPCHECK(h, hipGetLastError());
         HIPCHECK(h, hipEventRecord(ev.h1, t));
         if (pipe) {
-            HIPCHECK(h, hipEventRecord(h->set_done[h->cur_set], t));
-            h->set_busy[h->cur_set] = true;
+            HIPCHECK(h, hipEventRecord(h->sets[h->cur_set].done, t));
+            h->sets[h->cur_set].busy = true;
         }
     }
     h->last_n = n;
@@ -728,10 +754,12 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
 
 int bftsim_set_pipeline(bftsim_t* h, int on) {
     if (!h) return BFTSIM_EINVAL;
-    if ((on != 0) == (h->pipeline != 0)) return BFTSIM_OK;
+    if (on < 0 || on > (int)bftsim::MAX_SETS) return fail(h, BFTSIM_EINVAL, "pipeline depth must be 0..8");
+    const int depth = on == 0 ? 0 : on == 1 ? 2 : on;
+    if (depth == h->pipeline) return BFTSIM_OK;
     int rc = h->last_stream || h->hs ? sync_all(h) : BFTSIM_OK;
     if (rc) return rc;
-    h->pipeline = on != 0;
+    h->pipeline = depth;
     (void)hipSetDevice(h->device);
     free_bufs(h);                                   // re-sized (one or two sets) by the next prepare
     return BFTSIM_OK;

@@ -125,11 +125,13 @@ int bftsim_last_kernel_ms(bftsim_t *h, float *consensus_ms, float *hash_ms);
 /* summed per-kernel device times (ms) of every launch since the previous call, without blocking
  * between launches (waits only for the launches being summed) */
 int bftsim_kernel_ms_sum(bftsim_t *h, double *consensus_ms, double *hash_ms, uint32_t *launches);
-/* pipelined launches (power-of-two N, the batch throughput mode of the benchmark): two sets of
- * per-height row tables used alternately, and the block-hash pass of launch k on a second stream,
- * where it overlaps the consensus kernel of launch k+1. Results of a launch are complete once
- * bftsim_sync returns; bftsim_fetch/_stats_get/_fetch_summary read the last launch. Takes effect at
- * the next bftsim_prepare (buffers are re-allocated). */
+/* pipelined launches (big-endian seeds and power-of-two N, the batch throughput mode of the
+ * benchmark): a ring of `on` per-height row-table sets (on = 1 means 2; 0 disables) used in turn, and
+ * the block-hash pass of each launch on its set's own stream, where it overlaps the consensus kernels
+ * of the following launches and, with three or more sets, the hash passes of other launches (a
+ * hash chain is sequential in height, so small batches are bound by its latency, not by the GPU).
+ * Results of a launch are complete once bftsim_sync returns; bftsim_fetch/_stats_get/_fetch_summary
+ * read the last launch. Takes effect at the next bftsim_prepare (buffers are re-allocated). */
 int bftsim_set_pipeline(bftsim_t *h, int on);
 /* verification switch: 0 runs N = 64 through the full kernel alone instead of the FAST kernel +
  * resume (results are identical; the default 1 is the fast path) */

@@ -1,5 +1,5 @@
-"""GPU: the pipelined launch mode of the benchmark (bftsim_set_pipeline) — alternating row-table
-sets, the block-hash pass of launch k on a second stream overlapping the consensus of launch k+1 —
+"""GPU: the pipelined launch mode of the benchmark (bftsim_set_pipeline) — a ring of row-table sets,
+the block-hash pass of each launch on its set's stream overlapping the following launches —
 gives the oracle's results for every launch, and the per-launch HIP-event timings are all read."""
 import numpy as np
 import pytest
@@ -16,15 +16,16 @@ def _sim(cfg):
     return Simulator(cfg)
 
 
-def test_pipelined_launches_match_oracle():
+@pytest.mark.parametrize("depth", [2, 3, 4])
+def test_pipelined_launches_match_oracle(depth):
     cfg = cfg3(heights=30)
     n = 64
     sim = _sim(cfg)
     try:
-        sim.set_pipeline(True)
+        sim.set_pipeline(True, depth)
         sim.prepare(n)
         sim.kernel_ms_sum()
-        for k in range(5):                       # odd count: the last launch used the second set
+        for k in range(5):                       # the ring of sets wraps around
             sim.launch(k * n)
         sim.sync()
         got = sim.fetch()
