@@ -66,6 +66,7 @@ struct Params {
     uint32_t seed_le;                 // BFTSIM_SEED_LE: randon_seed reads U128 little-endian (bftsim.h)
     uint32_t backlog_replay;          // BFTSIM_BACKLOG_REPLAY (SPEC.md §10)
     uint32_t pad3;
+    uint32_t* backlog;                // replay mode: per wave / workgroup [S slots][5 words][L lanes]
 };
 
 // flags (same bits as the oracle)

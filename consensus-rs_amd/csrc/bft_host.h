@@ -89,7 +89,7 @@ inline Params params_from_config(const bftsim_config& c, uint32_t seg, uint32_t 
     p.first_instance = (uint32_t)first;
     p.n_instances = (uint32_t)n;
     p.genesis_seed = genesis_seed;
-    p.fast = 1;
+    p.fast = p.backlog_replay ? 0u : 1u;             // replay mode: one message at a time (SPEC.md §10)
     p.q = (2u * c.n) / 3u;
     p.nmask = (c.n & (c.n - 1)) == 0 ? c.n - 1 : 0;
     return p;

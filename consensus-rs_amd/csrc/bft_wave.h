@@ -74,7 +74,7 @@ template <uint32_t S>
 struct Layout {
     static constexpr uint32_t L = S > 64 ? S : 64;
     static constexpr int NW = S > 64 ? (int)(S / 64) : 1;
-    static constexpr int K = S > 64 ? 4 : 8;          // RoundChangeSet rounds kept per validator
+    static constexpr int K = 16;                      // RoundChangeSet rounds kept per validator
     static constexpr uint32_t CMT_STRIDE = 8;          // words per lane of the commit hand-off
     static constexpr uint32_t REC_OFF = 0;
     static constexpr uint32_t RC_OFF = REC_OFF + L * (uint32_t)REC_WORDS * 4;
@@ -82,6 +82,7 @@ struct Layout {
     static constexpr uint32_t CACHE_OFF = RC_OFF;
     static constexpr uint32_t HIST_OFF = CACHE_OFF + 12u * L * 4u;
     static constexpr uint32_t RCS_WORDS = (uint32_t)K * (1u + 2u * NW) * L;    // global, per wave
+    static constexpr uint32_t BL_WORDS = S * 5u * L;  // replay mode: backlog slots, global, per wave
     static constexpr uint32_t SEG_OFF = HIST_OFF + 528;
     static_assert(L * CMT_STRIDE <= L * REC_WORDS, "commit hand-off must fit in the record area");
     static_assert(HIST_BINS * 4 <= 528, "histogram area");
@@ -94,6 +95,11 @@ struct Layout {
 };
 BFT_FN uint32_t rcs_words(uint32_t seg) {
     return seg == 256 ? Layout<256>::RCS_WORDS : seg == 128 ? Layout<128>::RCS_WORDS : Layout<64>::RCS_WORDS;
+}
+BFT_FN uint32_t backlog_words(uint32_t seg) {      // per wave (S <= 64) or workgroup
+    return seg == 256 ? Layout<256>::BL_WORDS : seg == 128 ? Layout<128>::BL_WORDS : seg == 64 ? Layout<64>::BL_WORDS
+         : seg == 32 ? Layout<32>::BL_WORDS : seg == 16 ? Layout<16>::BL_WORDS : seg == 8 ? Layout<8>::BL_WORDS
+         : Layout<4>::BL_WORDS;
 }
 BFT_FN uint32_t lds_bytes(uint32_t seg, bool need_seed) {
     return seg == 256 ? Layout<256>::bytes(need_seed) : seg == 128 ? Layout<128>::bytes(need_seed)
@@ -157,6 +163,7 @@ struct Sim {
     uint64_t commit_blk;
     uint32_t lane_flags;
     uint32_t* rcs_base;      // this wave's RoundChangeSet table (global)
+    uint32_t* bl_base;       // this wave's backlog slots (global, replay mode)
 #ifdef BFT_STAMPS
     uint64_t st_acc[12];
     uint64_t st_t;
@@ -202,6 +209,7 @@ struct Sim {
         lane_flags = 0;
         off_inst = offset_inst_part(p.seed, inst);
         rcs_base = p.rcs + (uint64_t)wave_global * LY::RCS_WORDS;
+        bl_base = p.backlog ? p.backlog + (uint64_t)wave_global * LY::BL_WORDS : nullptr;
         off_tick = 0;
     }
 
@@ -535,7 +543,11 @@ struct Sim {
 
     BFT_FN void handle_prepare(uint32_t src, uint32_t vh, uint32_t vr, uint64_t d, bool wild) {   // prepare.rs:48-66
         int res = check_message(2, vh);
-        if (res != 0) { if (res == 2) note_future_block(vh); return; }
+        if (res != 0) {
+            if (res == CM_FUTURE_BLOCK) note_future_block(vh);
+            else if (res == CM_FUTURE_MSG) backlog_store(src, MT_PREPARE, vh, vr, d, wild);
+            return;
+        }
         if (vh != h || vr != r) return;
         prep.set(src);
         if (blk_valid(lock) && digest_match(d, wild, lock)) { lock_hash(); st = ST_PREPARED; send_commit(); }
@@ -544,7 +556,11 @@ struct Sim {
 
     BFT_FN void handle_commit(uint32_t src, uint32_t vh, uint32_t vr, uint64_t d, bool wild) {    // commit.rs:63-111
         int res = check_message(3, vh);
-        if (res != 0) { if (res == 2) note_future_block(vh); return; }
+        if (res != 0) {
+            if (res == CM_FUTURE_BLOCK) note_future_block(vh);
+            else if (res == CM_FUTURE_MSG) backlog_store(src, MT_COMMIT, vh, vr, d, wild);
+            return;
+        }
         if (!digest_match(d, wild, pp) || vh != h || vr != r) return;
         comm.set(src);
         if (comm.popc() > qval() && st < ST_COMMITTED) { lock_hash(); core_commit(); }
@@ -558,6 +574,38 @@ struct Sim {
         if ((uint32_t)n >= qval() + 1u && wait && r < mr) {
             send_round_change(mr);
             start_new_round(mr);
+        } else if (wait && r < mr) {                     // FutureRoundMessage (round_change.rs:93-96)
+            backlog_store(src, MT_ROUND_CHANGE, vh, mr, 0, false);
+        }
+    }
+
+    // ---------------------------------------------------------------- backlog replay (SPEC.md §10)
+    // BackLogActor (back_log.rs:38-65): per sender the first FutureMessage / FutureRoundMessage is kept.
+    // The reference never re-delivers it (outside replay mode nothing is stored: dropped). Slot of
+    // sender s: words [s][k][lane], k = {valid | code << 1 | wild << 4, height, round, digest lo, hi}.
+    BFT_FN uint32_t* bl_p(uint32_t s, uint32_t k) const { return bl_base + (s * 5u + k) * LY::L + lane; }
+    BFT_FN void backlog_store(uint32_t src, int code, uint32_t vh, uint32_t vr, uint64_t d, bool wild) {
+        if (!P.backlog_replay) return;
+        if (*bl_p(src, 0) & 1u) return;                  // or_insert_with: the first message stays
+        *bl_p(src, 0) = 1u | ((uint32_t)code << 1) | (wild ? 16u : 0u);
+        *bl_p(src, 1) = vh; *bl_p(src, 2) = vr;
+        *bl_p(src, 3) = (uint32_t)d; *bl_p(src, 4) = (uint32_t)(d >> 32);
+    }
+    // the stored messages in ascending sender order, each slot emptied and handled as a BackLogEvent
+    // (core.rs:197-204); one that is again a Future(Round)Message is stored again
+    BFT_FN void replay_backlog() {
+        const uint32_t n = nval();
+        for (uint32_t s = 0; s < n; ++s) {
+            const uint32_t hd = *bl_p(s, 0);
+            if (!(hd & 1u)) continue;
+            const uint32_t vh = *bl_p(s, 1), vr = *bl_p(s, 2);
+            const uint64_t d = (uint64_t)*bl_p(s, 3) | ((uint64_t)*bl_p(s, 4) << 32);
+            *bl_p(s, 0) = 0;
+            if (core_dead) return;
+            const int code = (int)((hd >> 1) & 7u);
+            if (code == MT_PREPARE) handle_prepare(s, vh, vr, d, (hd & 16u) != 0);
+            else if (code == MT_COMMIT) handle_commit(s, vh, vr, d, (hd & 16u) != 0);
+            else handle_round_change(s, vh, vr);
         }
     }
 
@@ -612,6 +660,7 @@ struct Sim {
             sync_pending = 0;
         }
         if (!core_dead && timer_tick == tick) { timer_tick = -1; handle_timer_event(); }
+        if (P.backlog_replay) replay_backlog();          // SPEC.md §10
     }
 
     // segment collectives: ballots as sender bitmaps; reductions (butterfly inside a wave
@@ -1039,6 +1088,7 @@ struct Sim {
             return;
         }
         // general path: every delivered non-empty sender, in rotated order, one at a time
+        if (P.backlog_replay) replay_backlog();          // the stored messages first (SPEC.md §10)
         M any = ps.k_pp | ps.k_pr | ps.k_cm | ps.k_ocm | ps.k_rc | ps.k_sync | ps.k_blk;
         M c = rot(mk & any, off);
         while (c.any()) {
@@ -1112,6 +1162,7 @@ struct Sim {
             off_tick = offset_tick_part(off_inst, (uint32_t)tick);
             BFT_STAMP(7);
             if (act && !resuming) t_step();
+            if (P.backlog_replay && !resuming) resolve_commits();   // replayed commits of the T-step
             BFT_STAMP(0);
             const uint32_t pstart = resuming ? p0 : 0u;
             resuming = false;

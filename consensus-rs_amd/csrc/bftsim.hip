@@ -391,6 +391,8 @@ struct bftsim {
     uint64_t* d_hist = nullptr;       // [HIST_BINS] of the last launch
     uint8_t* d_tips = nullptr;        // [cap_inst * 32]
     uint32_t* d_rcs = nullptr;        // RoundChangeSet tables, rcs_words(seg) per wave / workgroup
+    uint32_t* d_backlog = nullptr;    // replay mode: backlog slots, backlog_words(seg) per wave / workgroup
+    uint64_t backlog_bytes = 0;
     uint32_t* d_resume = nullptr;     // FAST launches: [cap_inst] hand-over flags
     uint32_t* d_save = nullptr;       // FAST launches: [SAVE_WORDS][cap_inst * 64] saved lane state
     int fast = 1;                     // FAST kernel + resume for N = 64 (bftsim_set_fast(h, 0): full kernel)
@@ -448,6 +450,9 @@ static void free_bufs(bftsim* h) {
     }
     (void)hipFree(h->d_trace); (void)hipFree(h->d_tips); (void)hipFree(h->d_rcs);
     h->d_rcs = nullptr;
+    (void)hipFree(h->d_backlog);
+    h->d_backlog = nullptr;
+    h->backlog_bytes = 0;
     (void)hipFree(h->d_resume); (void)hipFree(h->d_save);
     h->d_resume = nullptr; h->d_save = nullptr;
     for (uint32_t k = 0; k < bftsim::MAX_SETS; ++k) h->sets[k].busy = false;
@@ -587,6 +592,10 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg;
         uint64_t blocks = (n + per_block - 1) / per_block;
         HIPCHECK(h, hipMalloc(&h->d_rcs, blocks * bft::rcs_words(h->seg) * 4));
+        if (h->cfg.backlog_mode == BFTSIM_BACKLOG_REPLAY) {
+            h->backlog_bytes = blocks * bft::backlog_words(h->seg) * 4;
+            HIPCHECK(h, hipMalloc(&h->d_backlog, h->backlog_bytes));
+        }
     }
     if (h->seg == 64 && h->cfg.n == 64) {          // FAST kernel hand-over buffers
         HIPCHECK(h, hipMalloc(&h->d_resume, n * 4));
@@ -649,6 +658,7 @@ static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
     p.trace_ticks = h->trace_ticks;
     p.hist = h->d_hist;
     p.rcs = h->d_rcs;
+    p.backlog = h->d_backlog;
     if (h->window) {
         p.window_mask = h->window - 1;
         p.rows = h->window;
@@ -711,10 +721,11 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     h->ring_head += 1;
     HIPCHECK(h, hipMemsetAsync(h->d_rec, 0, n * h->hcap * 16, s));
     HIPCHECK(h, hipMemsetAsync(h->d_hist, 0, bft::HIST_BINS * sizeof(uint64_t), s));
+    if (h->d_backlog) HIPCHECK(h, hipMemsetAsync(h->d_backlog, 0, h->backlog_bytes, s));
     uint32_t per_block = h->seg > 64 ? 1u : 64u / h->seg;      // instances per workgroup
     uint32_t grid = (uint32_t)((n + per_block - 1) / per_block);
     size_t lds = bft::lds_bytes(h->seg, p.need_seed != 0);
-    const bool fast = h->fast && h->d_save && !p.need_seed && !h->h_trace && h->seg == 64;
+    const bool fast = h->fast && p.fast && h->d_save && !p.need_seed && !h->h_trace && h->seg == 64;
     HIPCHECK(h, hipEventRecord(ev.c0, s));
     if (fast) {
         // FAST kernel over every instance, then the full kernel over the ones it handed over

@@ -333,6 +333,9 @@ typedef struct {
 } outbox;
 
 typedef struct { uint32_t round; bits set; } rc_entry;
+
+/* a stored FutureMessage / FutureRoundMessage (backlog replay mode, SPEC.md §10) */
+typedef struct { uint8_t valid, code, wild; uint32_t vh, vr; blk d; } bl_entry;
 #define RCS_MAX 64
 
 typedef struct {
@@ -361,6 +364,7 @@ typedef struct {
     uint32_t s_cm_h, s_cm_r; blk s_cm_d; int s_cm_valid;
     uint32_t s_ocm_h, s_ocm_r; blk s_ocm_d; int s_ocm_valid;
     outbox next, cur;
+    bl_entry *bl;             /* [n] per-sender backlog slots (backlog replay mode only) */
 } val;
 
 typedef struct {
@@ -714,10 +718,24 @@ static void handle_preprepare(world *w, val *v, uint32_t src, const outbox *m) {
     }
 }
 
+/* BackLogActor::handle (back_log.rs:38-65): the first message per sender is kept (or_insert_with);
+ * reached from handle_check_message on FutureMessage / FutureRoundMessage (core.rs:353-358). The
+ * reference never re-delivers it (process_back_log only iterates), so outside replay mode it is dropped. */
+static void backlog_store(world *w, val *v, uint32_t src, int code, uint32_t vh, uint32_t vr, blk d, int wild) {
+    if (!w->cfg->backlog_mode) return;
+    bl_entry *e = &v->bl[src];
+    if (e->valid) return;
+    e->valid = 1; e->code = (uint8_t)code; e->wild = (uint8_t)wild; e->vh = vh; e->vr = vr; e->d = d;
+}
+
 /* HandlePrepare::handle (prepare.rs:48-66) */
 static void handle_prepare(world *w, val *v, uint32_t src, const outbox *m) {
     int res = check_message(v, MT_PREPARE, m->pr_h);
-    if (res != E_OK) { if (res == E_FUTURE_BLOCK) note_future_block(v, m->pr_h); return; }
+    if (res != E_OK) {
+        if (res == E_FUTURE_BLOCK) note_future_block(v, m->pr_h);
+        else if (res == E_FUTURE_MSG) backlog_store(w, v, src, MT_PREPARE, m->pr_h, m->pr_r, m->pr_d, m->pr_wild);
+        return;
+    }
     if (m->pr_h != v->h || m->pr_r != v->r) return;                     /* InconsistentSubject */
     bits_set(&v->prep, src);                                            /* accept */
     if (v->lock.valid && digest_match(m->pr_d, m->pr_wild, v->lock)) {
@@ -735,7 +753,11 @@ static void handle_prepare(world *w, val *v, uint32_t src, const outbox *m) {
 /* HandleCommit::handle + verify_commit (commit.rs:63-111) */
 static void handle_commit_msg(world *w, val *v, uint32_t src, uint32_t vh, uint32_t vr, blk d, int wild) {
     int res = check_message(v, MT_COMMIT, vh);
-    if (res != E_OK) { if (res == E_FUTURE_BLOCK) note_future_block(v, vh); return; }
+    if (res != E_OK) {
+        if (res == E_FUTURE_BLOCK) note_future_block(v, vh);
+        else if (res == E_FUTURE_MSG) backlog_store(w, v, src, MT_COMMIT, vh, vr, d, wild);
+        return;
+    }
     assert(v->pp.valid);                                                /* subject().unwrap() */
     if (!digest_match(d, wild, v->pp) || vh != v->h || vr != v->r) return;
     bits_set(&v->comm, src);
@@ -746,10 +768,9 @@ static void handle_commit_msg(world *w, val *v, uint32_t src, uint32_t vh, uint3
 }
 
 /* HandleRoundChange::handle (round_change.rs:65-98) */
-static void handle_round_change(world *w, val *v, uint32_t src, const outbox *m) {
-    int res = check_message(v, MT_ROUND_CHANGE, m->rc_h);
-    if (res != E_OK) { if (res == E_FUTURE_BLOCK) note_future_block(v, m->rc_h); return; }
-    uint32_t mr = m->rc_r;
+static void handle_round_change_v(world *w, val *v, uint32_t src, uint32_t vh, uint32_t mr) {
+    int res = check_message(v, MT_ROUND_CHANGE, vh);
+    if (res != E_OK) { if (res == E_FUTURE_BLOCK) note_future_block(v, vh); return; }
     if (v->r > mr && mr > 0) {
         send_round_change(w, v, mr);
         return;
@@ -760,7 +781,35 @@ static void handle_round_change(world *w, val *v, uint32_t src, const outbox *m)
         start_new_round(w, v, mr);
         return;
     }
-    /* else FutureRoundMessage → backlog, never re-delivered (back_log.rs:38-91) */
+    if (v->wait && v->r < mr)   /* FutureRoundMessage (round_change.rs:93-96) → backlog */
+        backlog_store(w, v, src, MT_ROUND_CHANGE, vh, mr, NONE_BLK, 0);
+}
+static void handle_round_change(world *w, val *v, uint32_t src, const outbox *m) {
+    handle_round_change_v(w, v, src, m->rc_h, m->rc_r);
+}
+
+/* Backlog replay (SPEC.md §10): the stored messages in ascending sender order, each slot emptied and
+ * the message handled as a BackLogEvent (core.rs:197-204 → handle_check_message); one that is again a
+ * FutureMessage / FutureRoundMessage is stored again. */
+static void backlog_replay(world *w, val *v) {
+    for (uint32_t s = 0; s < w->n; ++s) {
+        bl_entry *e = &v->bl[s];
+        if (!e->valid) continue;
+        bl_entry m = *e;
+        e->valid = 0;
+        if (v->core_dead) return;
+        if (m.code == MT_PREPARE) {
+            outbox o;
+            memset(&o, 0, sizeof o);
+            o.has_pr = 1; o.pr_h = m.vh; o.pr_r = m.vr; o.pr_d = m.d; o.pr_wild = m.wild;
+            handle_prepare(w, v, s, &o);
+        } else if (m.code == MT_COMMIT) {
+            handle_commit_msg(w, v, s, m.vh, m.vr, m.d, m.wild);
+        } else {
+            handle_round_change_v(w, v, s, m.vh, m.vr);
+        }
+        if (w->frozen) return;
+    }
 }
 
 /* handle_msg_middle Block branch (core.rs:75-82) */
@@ -809,6 +858,10 @@ static void deliver_phase(world *w, uint32_t phase) {
         if (!v->running) continue;
         miner_step(w, v);                               /* event step */
         if (w->frozen) return;
+        if (w->cfg->backlog_mode) {                     /* backlog replay (SPEC.md §10) */
+            backlog_replay(w, v);
+            if (w->frozen) return;
+        }
         uint64_t mk[4];
         orc_deliver_mask(w->cfg, w->inst, (uint32_t)w->tick, phase, r, mk);
         bits dm;
@@ -871,6 +924,10 @@ static void run_tick(world *w) {
         if (!v->core_dead && v->timer_tick == w->tick) {
             v->timer_tick = -1;
             handle_timer_event(w, v);
+        }
+        if (w->cfg->backlog_mode) {                     /* SPEC.md §10 */
+            backlog_replay(w, v);
+            if (w->frozen) break;
         }
     }
     for (uint32_t p = 0;; ++p) {
@@ -940,6 +997,9 @@ static int run_instance_ex(const orc_config *cfg, uint32_t inst, const orc_resul
     w->n = n;
     w->q = orc_two_thirds_majority(n);
     w->v = (val *)calloc(n, sizeof(val));
+    bl_entry *bl_all = cfg->backlog_mode ? (bl_entry *)calloc((size_t)n * n, sizeof(bl_entry)) : NULL;
+    if (bl_all)
+        for (uint32_t i = 0; i < n; ++i) w->v[i].bl = bl_all + (size_t)i * n;
     w->canon_cap = cfg->heights + 64;
     w->canon = (canon_entry *)calloc(w->canon_cap + 1, sizeof(canon_entry));
     /* genesis (core/genesis.rs:24-59) */
@@ -1004,6 +1064,7 @@ static int run_instance_ex(const orc_config *cfg, uint32_t inst, const orc_resul
         res->views[idx] = views;
     }
     if (st) stream_summary(cfg, w, done_tick, st, idx, hist);
+    free(bl_all);
     free(w->v);
     free(w->canon);
     free(R);

@@ -257,6 +257,8 @@ extern "C" int emu_run_stream(const bftsim_config* cfg, uint64_t first, uint64_t
     std::vector<uint8_t> lds(bft::lds_bytes(seg, true));
     std::vector<uint32_t> rcs((size_t)waves * bft::rcs_words(seg), 0xcdcdcdcdu);
     P.rcs = rcs.data();
+    std::vector<uint32_t> backlog(P.backlog_replay ? (size_t)waves * bft::backlog_words(seg) : 0, 0);
+    P.backlog = P.backlog_replay ? backlog.data() : nullptr;
     for (uint32_t w = 0; w < waves; ++w) {
         memset(lds.data(), 0xcd, lds.size());
         if (run_wave(P, w, lds, seg > 64 ? (int)seg : 64)) return -1;
@@ -300,10 +302,12 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
     std::vector<uint8_t> lds(bft::lds_bytes(seg, P.need_seed != 0));
     std::vector<uint32_t> rcs((size_t)waves * bft::rcs_words(seg), 0xcdcdcdcdu);
     P.rcs = rcs.data();
+    std::vector<uint32_t> backlog(P.backlog_replay ? (size_t)waves * bft::backlog_words(seg) : 0, 0);
+    P.backlog = P.backlog_replay ? backlog.data() : nullptr;
     // as libbftsim: N = 64 runs the FAST kernel, then the full kernel resumes the instances it handed
     // over (BFT_EMU_FAST=0: the full kernel alone)
     const char* ef = getenv("BFT_EMU_FAST");
-    const bool fast = seg == 64 && cfg->n == 64 && !P.need_seed && !trace && !(ef && strcmp(ef, "0") == 0);
+    const bool fast = seg == 64 && cfg->n == 64 && P.fast && !P.need_seed && !trace && !(ef && strcmp(ef, "0") == 0);
     std::vector<uint32_t> resume, save;
     if (fast) {
         resume.assign(n, 0);

@@ -1,6 +1,7 @@
 """Randomized parity fuzz: CPU wave emulator (the kernel body) vs the oracle on random configs.
 Usage: python tests/fuzz_parity.py [seconds] [rng seed] [big]. `big` draws N in 65..256 (the
-workgroup-segment kernels), `n64` N = 64 (the FAST kernel and its hand-overs). Test-only tool (not collected by pytest)."""
+workgroup-segment kernels), `n64` N = 64 (the FAST kernel and its hand-overs); a fourth argument
+`replay` runs every config in backlog replay mode (SPEC.md §10). Test-only tool (not collected by pytest)."""
 import random
 import sys
 import time
@@ -11,7 +12,7 @@ from bftsim.configs import BftConfig
 from parity_util import mismatches
 
 
-def random_config(rng, big=False, n64=False):
+def random_config(rng, big=False, n64=False, replay=False):
     if n64:                              # the FAST kernel (bft_fast64.h) and its hand-overs
         n = 64
     elif big:
@@ -26,7 +27,8 @@ def random_config(rng, big=False, n64=False):
     heights = rng.choice([5, 20, 40])
     return BftConfig(n=n, heights=heights, seed=rng.randrange(1 << 40), byz_count=byz,
                      drop_ppm=drop, proposer_crash_ppm=crash, phase_cap=cap, silent=silent,
-                     max_ticks=heights * 4 + 16, name=f"n{n}-b{byz}-d{drop}-c{crash}-cap{cap}-s{len(silent)}")
+                     max_ticks=heights * 4 + 16, backlog_mode=1 if replay else 0,
+                     name=f"n{n}-b{byz}-d{drop}-c{crash}-cap{cap}-s{len(silent)}{'-replay' if replay else ''}")
 
 
 def main():
@@ -34,9 +36,10 @@ def main():
     rng = random.Random(int(sys.argv[2]) if len(sys.argv) > 2 else 1234)
     big = len(sys.argv) > 3 and sys.argv[3] == "big"
     n64 = len(sys.argv) > 3 and sys.argv[3] == "n64"
+    replay = "replay" in sys.argv[3:]
     t0, runs, fails = time.time(), 0, 0
     while time.time() - t0 < budget:
-        cfg = random_config(rng, big, n64)
+        cfg = random_config(rng, big, n64, replay)
         first = rng.randrange(1 << 20)
         n_inst = rng.choice([1, 2] if big else [1, 3, 8])
         a = O.run(cfg, first, n_inst)
@@ -45,7 +48,7 @@ def main():
         runs += 1
         if bad:
             fails += 1
-            print("MISMATCH", cfg, first, n_inst, bad, flush=True)
+            print("MISMATCH", cfg.name, cfg.seed, first, n_inst, bad, flush=True)
     print(f"fuzz: {runs} configs, {fails} mismatches", flush=True)
     sys.exit(1 if fails else 0)
 

@@ -13,6 +13,11 @@ def _le(cfg):
     import dataclasses
     return dataclasses.replace(cfg, seed_byte_order=1, name=cfg.name + "-le")
 
+
+def _replay(cfg):
+    import dataclasses
+    return dataclasses.replace(cfg, backlog_mode=1, name=cfg.name + "-replay")
+
 CASES = [
     ("cfg1-n5", lambda: cfg1(True, heights=40), 0, 1),
     ("cfg2", lambda: cfg2(heights=25), 0, 16),
@@ -45,6 +50,16 @@ CASES = [
     ("cfg3-le", lambda: _le(cfg3(heights=8)), 0, 2),
     ("cfg4-n64-le", lambda: _le(cfg4(64, heights=10)), 0, 2),
     ("cfg4-n128-le", lambda: _le(cfg4(128, heights=6)), 0, 1),
+    # backlog replay mode (bftsim.h BFTSIM_BACKLOG_REPLAY, SPEC.md §10): every phase one message at a time
+    ("cfg2-replay", lambda: _replay(cfg2(heights=30)), 0, 16),
+    ("n4-drop30-replay", lambda: _replay(BftConfig(n=4, heights=25, seed=7, drop_ppm=300_000)), 0, 8),
+    ("n7-byz2-drop-replay", lambda: _replay(BftConfig(n=7, heights=25, seed=8, byz_count=2,
+                                                      drop_ppm=200_000)), 0, 8),
+    ("n16-crash-drop-replay", lambda: _replay(BftConfig(n=16, heights=15, seed=3, drop_ppm=200_000,
+                                                        proposer_crash_ppm=300_000)), 0, 4),
+    ("n64-drop10-replay", lambda: _replay(BftConfig(n=64, heights=10, seed=5, drop_ppm=100_000)), 0, 2),
+    ("n100-drop-replay", lambda: _replay(BftConfig(n=100, heights=8, seed=6, drop_ppm=200_000)), 0, 1),
+    ("cfg2-le-replay", lambda: _replay(_le(cfg2(heights=20))), 0, 8),
 ]
 
 
@@ -70,6 +85,7 @@ STREAM_CASES = [
     ("cfg4-n100", lambda: cfg4(100, heights=8), 0, 1, 64),
     ("n7-crash-drop-w128", lambda: BftConfig(n=7, heights=200, seed=41, drop_ppm=150_000,
                                              proposer_crash_ppm=300_000), 0, 8, 128),
+    ("cfg2-replay-w64", lambda: _replay(cfg2(heights=150)), 0, 8, 64),
 ]
 
 

@@ -15,6 +15,11 @@ def _le(cfg):
     return dataclasses.replace(cfg, seed_byte_order=1, name=cfg.name + "-le")
 
 
+def _replay(cfg):
+    import dataclasses
+    return dataclasses.replace(cfg, backlog_mode=1, name=cfg.name + "-replay")
+
+
 def gpu_run(cfg, first, n, trace_ticks=0):
     from bftsim.runtime import Simulator
     sim = Simulator(cfg)
@@ -56,6 +61,17 @@ CASES = [
     ("cfg4-n64-le", lambda: _le(cfg4(64, heights=60)), 0, 24),
     ("cfg4-n7-le", lambda: _le(cfg4(7, heights=60)), 0, 24),
     ("cfg4-n256-le", lambda: _le(cfg4(256, heights=30)), 0, 4),
+    # backlog replay mode (BFTSIM_BACKLOG_REPLAY, SPEC.md §10): the general path with the backlog table
+    ("cfg2-replay", lambda: _replay(cfg2()), 0, 256),
+    ("cfg5-replay", lambda: _replay(cfg5(heights=200)), 0, 64),
+    ("n4-drop30-replay", lambda: _replay(BftConfig(n=4, heights=40, seed=7, drop_ppm=300_000)), 0, 64),
+    ("n7-byz2-drop-replay", lambda: _replay(BftConfig(n=7, heights=40, seed=8, byz_count=2,
+                                                      drop_ppm=200_000)), 0, 32),
+    ("cfg4-n16-replay", lambda: _replay(cfg4(16, heights=40)), 0, 16),
+    ("n64-drop10-replay", lambda: _replay(BftConfig(n=64, heights=20, seed=5, drop_ppm=100_000)), 0, 8),
+    ("cfg3-replay", lambda: _replay(cfg3(heights=30)), 0, 8),
+    ("n100-drop-replay", lambda: _replay(BftConfig(n=100, heights=20, seed=6, drop_ppm=200_000)), 0, 4),
+    ("n256-drop-replay", lambda: _replay(BftConfig(n=256, heights=10, seed=6, drop_ppm=100_000)), 0, 2),
 ] + [(f"cfg4-n{n}", (lambda n=n: cfg4(n, heights=60)), 0, 24)
      for n in (4, 7, 10, 16, 31, 32, 33, 63, 64, 65, 100, 128, 200, 256)]
 
