@@ -14,7 +14,8 @@ Prints ONE JSON line (rank 0). See DESIGN.md §Measurement for the roofline mode
 hashes; the rounds-to-commit and commit-latency histograms are all-reduced over RCCL and printed.
 One step takes ~11 s on one MI355X: run it with --steps 1 --warmup 0.
 
-`--workload cfg2` / `cfg4` / `drop64` measure the other consensus configurations (not the headline):
+`--workload cfg2` / `cfg4` / `drop64` measure the other consensus configurations (not the headline;
+`--byz 1` / `--byz 2` turn cfg2 / cfg5 into their Byzantine variants, SPEC.md §6):
 cfg2 = 65,536 instances N=4, 10 % drops (BASELINE configs[1]); cfg4 = 16,384 instances of one N of the
 validator sweep with proposer crashes (`--n`, default 256: the workgroup-segment kernel); drop64 = 16,384
 instances N=64 f=21 with 5 % drops (most instances hand over from the FAST kernel to the resume kernel).
@@ -187,6 +188,9 @@ def main():
     ap.add_argument("--pipeline-depth", type=int, default=None,
                     help="row-table sets in the launch ring (bftsim_set_pipeline); default 3, and 6 at <= 2,048 "
                          "instances per GPU where the hash chains' latency, not the GPU, bounds a launch")
+    ap.add_argument("--byz", type=int, default=None,
+                    help="cfg2 / cfg5: run the tolerated f as this many equivocating validators (SPEC.md §6: "
+                         "cfg2-byz = 1, cfg5-byz = 2)")
     ap.add_argument("--seed-order", choices=("be", "le"), default="be",
                     help="U128 byte order of randon_seed (validator.rs:39-48; include/bftsim.h BFTSIM_SEED_*)")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
@@ -224,9 +228,9 @@ def main():
     torch.cuda.set_device(dev)
 
     if wl == "cfg5":
-        cfg = cfg5(heights=args.heights)
+        cfg = cfg5(heights=args.heights, byz=args.byz or 0)
     elif wl == "cfg2":
-        cfg = cfg2(heights=args.heights)
+        cfg = cfg2(heights=args.heights, byz=args.byz or 0)
     elif wl == "cfg4":
         cfg = cfg4(args.n, heights=args.heights)
     elif wl == "drop64":
@@ -308,7 +312,7 @@ def main():
                 h.pop()
             return h
         out = {
-            "metric": METRIC if wl == "cfg3" else METRIC_CFG5 if c5 else (
+            "metric": METRIC if wl == "cfg3" else METRIC_CFG5 if c5 and not cfg.byz_count else (
                 f"{wl} instance-rounds/sec (whole node), {cfg_desc(cfg)}; bit-exact"),
             "value": value,
             "unit": "instance-rounds/s",
@@ -322,7 +326,7 @@ def main():
             "dtype": "u64",
             "data": "synthetic (seeded Philox schedule, SPEC.md)",
             "config": {
-                "workload": (f"cfg5: {I} instances per GPU, N=7, 5% drop, {args.heights} heights, "
+                "workload": (f"{cfg.name}: {I} instances per GPU, {cfg_desc(cfg)}, {args.heights} heights, "
                              f"window {args.window}") if c5 else
                             (f"{wl}: {I} instances per GPU, {cfg_desc(cfg)}, {args.heights} heights" +
                              (", little-endian U128 seeds" if cfg.seed_byte_order else "")),

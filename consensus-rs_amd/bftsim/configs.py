@@ -107,9 +107,11 @@ def cfg1(n5: bool = True, heights: int = 100, seed: int = 1) -> BftConfig:
                      name="cfg1-n5" if n5 else "cfg1-n4")
 
 
-def cfg2(heights: int = 100) -> BftConfig:
-    """65,536 instances, N=4 f=1, 10% message drop (BASELINE.json configs[1])."""
-    return BftConfig(n=4, heights=heights, seed=2, drop_ppm=100_000, name="cfg2")
+def cfg2(heights: int = 100, byz: int = 0) -> BftConfig:
+    """65,536 instances, N=4 f=1, 10% message drop (BASELINE.json configs[1]). f is the tolerance
+    ⌊(N−1)/3⌋ here (SPEC.md §6); byz=1 runs that f as an equivocating validator ("cfg2-byz")."""
+    return BftConfig(n=4, heights=heights, seed=2, drop_ppm=100_000, byz_count=byz,
+                     name="cfg2-byz" if byz else "cfg2")
 
 
 def cfg3(heights: int = 100) -> BftConfig:
@@ -122,9 +124,11 @@ def cfg4(n: int, heights: int = 100) -> BftConfig:
     return BftConfig(n=n, heights=heights, seed=4, proposer_crash_ppm=300_000, name=f"cfg4-n{n}")
 
 
-def cfg5(heights: int = 10_000) -> BftConfig:
-    """1M instances, N=7 (tolerates f=2), 5% drop, long horizon; all validators honest."""
-    return BftConfig(n=7, heights=heights, seed=5, drop_ppm=50_000, name="cfg5")
+def cfg5(heights: int = 10_000, byz: int = 0) -> BftConfig:
+    """1M instances, N=7 (tolerates f=2), 5% drop, long horizon; all validators honest. byz=2 runs
+    the tolerated f as equivocating validators ("cfg5-byz")."""
+    return BftConfig(n=7, heights=heights, seed=5, drop_ppm=50_000, byz_count=byz,
+                     name="cfg5-byz" if byz else "cfg5")
 
 
 INSTANCES = {"cfg1": 1, "cfg2": 65_536, "cfg3": 16_384, "cfg4": 16_384, "cfg5": 1_048_576}

@@ -25,6 +25,8 @@ CASES = [
     ("cfg4-n10", lambda: cfg4(10, heights=25), 3, 8),
     ("cfg4-n33", lambda: cfg4(33, heights=15), 3, 2),
     ("cfg5", lambda: cfg5(heights=40), 0, 8),
+    ("cfg2-byz", lambda: cfg2(heights=25, byz=1), 0, 16),
+    ("cfg5-byz", lambda: cfg5(heights=40, byz=2), 0, 8),
     ("n7-byz3-drop", lambda: BftConfig(n=7, heights=25, seed=9, byz_count=3, drop_ppm=100_000), 0, 8),
     ("n4-cap2-drop30", lambda: BftConfig(n=4, heights=25, seed=12, drop_ppm=300_000, phase_cap=2), 0, 16),
     ("n16-crash-drop", lambda: BftConfig(n=16, heights=15, seed=21, drop_ppm=150_000,

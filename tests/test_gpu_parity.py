@@ -37,6 +37,9 @@ CASES = [
     ("cfg3", lambda: cfg3(), 0, 48),
     ("cfg3-tail", lambda: cfg3(), 16_300, 16),
     ("cfg5", lambda: cfg5(heights=300), 0, 64),
+    # the tolerated f of cfg2 / cfg5 run as equivocating validators (SPEC.md §6)
+    ("cfg2-byz", lambda: cfg2(byz=1), 0, 256),
+    ("cfg5-byz", lambda: cfg5(heights=300, byz=2), 0, 64),
     ("n4-byz2-unsafe", lambda: BftConfig(n=4, heights=40, seed=9, byz_count=2), 0, 64),
     ("n64-byz32-fork", lambda: BftConfig(n=64, heights=20, seed=31, byz_count=32), 0, 32),
     ("n64-byz40-drop5-fork", lambda: BftConfig(n=64, heights=20, seed=31, byz_count=40, drop_ppm=50_000), 0, 16),
