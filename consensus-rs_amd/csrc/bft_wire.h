@@ -234,7 +234,10 @@ BFT_FN bool decode_body(M& m, Decoded& d) {
     uint32_t glen;
     if (!rd_arr(m, glen)) return false;
     Arr<M> g{&m, glen, false};
-    if (!rd_arr(g, n) || n != 5) return false;
+    // signature and commit_seal are #[serde(default)] (protocol/mod.rs:48-51): serde's derived
+    // sequence visitor accepts the array without them (3 or 4 elements) and fills None
+    uint32_t gfields;
+    if (!rd_arr(g, gfields) || gfields < 3 || gfields > 5) return false;
     if (!rd_unit_variant(g, idx) || idx < 1 || idx > 3) return false;     // Prepare, Commit, RoundChange
     d.code = idx + 1u;
     if (!rd_uint(g, d.create_time)) return false;
@@ -245,8 +248,9 @@ BFT_FN bool decode_body(M& m, Decoded& d) {
     if (!rd_uint(s, d.round) || !rd_uint(s, d.height)) return false;
     if (!rd_bytes_fixed(s, 32, d.digest)) return false;
     if (s.left != 0) return false;
-    if (!rd_opt_bytes(g, 65, d.sig, d.has_sig)) return false;
-    if (!rd_opt_bytes(g, 65, d.seal, d.has_seal)) return false;
+    d.has_sig = d.has_seal = 0;
+    if (gfields >= 4 && !rd_opt_bytes(g, 65, d.sig, d.has_sig)) return false;
+    if (gfields >= 5 && !rd_opt_bytes(g, 65, d.seal, d.has_seal)) return false;
     if (g.left != 0 || g.bad) return false;
     return m.i == m.n;
 }

@@ -6,10 +6,8 @@
 // a pack pass copies the slots into the contiguous stream (lanes write consecutive bytes). The two
 // Keccak-256 digests run lane-per-message over the GossipMessage / sign-payload slots. Decoding is
 // lane-per-frame through the streaming decoder of bft_wire.h (plain byte loads: a 16-byte or 4-byte
-// register window measured 1.6-1.9x slower — the per-byte window test diverges the loads).
-// BFTWIRE_DECODE=wave selects a wave-per-frame decoder (frame in LDS, every nested byte array
-// un-expanded by all lanes with a scanned byte automaton): bit-identical, but ~64x the instruction
-// issue per message, measured 2.2x slower end to end — kept for A/B.
+// register window measured 1.6-1.9x slower — the per-byte window test diverges the loads; an
+// LDS-staged and a wave-per-frame decoder measured 1.25x and 2.2x slower and were removed).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -229,225 +227,6 @@ __global__ __launch_bounds__(64) void wire_decode_kernel(const uint8_t* stream, 
     ok[i] = good ? 1 : 0;
 }
 
-// BFTWIRE_DECODE=lds (A/B): one wave per 64 consecutive frames; their contiguous byte range is first
-// staged in LDS with coalesced 16-byte loads, then each lane parses its frame from LDS. Bit-identical,
-// but measured 1.25x slower than the global-memory lane decoder: the 40 KB buffer allows 4 waves per
-// CU, too few to hide the parse's dependent-read chains. A range larger than the buffer falls back to
-// global reads.
-constexpr uint32_t DEC_LDS = 40960;
-__global__ __launch_bounds__(64) void wire_decode_lds_kernel(const uint8_t* stream, const uint64_t* off, uint64_t n,
-                                                             bftwire_batch out, uint8_t* has_sig, uint8_t* has_seal,
-                                                             uint8_t* ok) {
-    __shared__ __attribute__((aligned(16))) uint8_t buf[DEC_LDS];
-    const uint64_t i0 = (uint64_t)blockIdx.x * 64u;
-    const uint64_t i = i0 + threadIdx.x;
-    const uint64_t iend = i0 + 64u < n ? i0 + 64u : n;
-    const uint64_t lo = off[i0], hi = off[iend];
-    const uint64_t base = lo & ~(uint64_t)15;
-    const bool staged = hi - base <= DEC_LDS;                 // block-uniform
-    if (staged) {
-        for (uint64_t j = 16u * threadIdx.x; base + j < hi; j += 64u * 16u)
-            *(uint4*)(buf + j) = *(const uint4*)(stream + base + j);
-        __syncthreads();
-    }
-    if (i >= n) return;
-    const uint64_t o = off[i], len = off[i + 1] - o;
-    Decoded d;
-    const uint8_t* f = staged ? buf + (o - base) : stream + o;
-    const bool good = len <= MAX_FRAME && decode_frame(f, (uint32_t)len, d);
-    out.code[i] = good ? (uint8_t)d.code : 0;
-    out.round[i] = good ? d.round : 0;
-    out.height[i] = good ? d.height : 0;
-    out.create_time[i] = good ? d.create_time : 0;
-    out.ttl[i] = good ? d.ttl : 0;
-    out.raw_time[i] = good ? d.raw_time : 0;
-    for (int k = 0; k < 32; ++k) out.digest[32u * i + k] = good ? d.digest[k] : 0;
-    for (int k = 0; k < 65; ++k) out.signature[65u * i + k] = (good && d.has_sig) ? d.sig[k] : 0;
-    for (int k = 0; k < 65; ++k) out.commit_seal[65u * i + k] = (good && d.has_seal) ? d.seal[k] : 0;
-    has_sig[i] = good && d.has_sig ? 1 : 0;
-    has_seal[i] = good && d.has_seal ? 1 : 0;
-    ok[i] = good ? 1 : 0;
-}
-
-// ---------------------------------------------------------------- wave-cooperative decode
-// The elements of a MessagePack array of uint8 are 1 (fixint), 2 (0xcc), 3 (0xcd), 5 (0xce) or 9 (0xcf)
-// bytes; which byte starts an element depends on every byte before it. Each lane takes one byte
-// and its transition function over the states {0: at an element start, k: k bytes of the element
-// left, 9: error}, packed as 10 nibbles; an inclusive Hillis-Steele scan of function composition
-// (6 shuffle steps) gives every lane its entry state. A lane whose exit state is 0 ends an element
-// and emits its byte (the value byte; the padding bytes of a wide encoding must be zero, as the
-// serial decoder's `v > 255` check requires).
-constexpr uint32_t ST_ERR = 9u;
-__device__ inline uint64_t fn_of_byte(uint32_t b) {
-    const uint32_t s0 = b < 0x80u ? 0u : b == 0xccu ? 1u : b == 0xcdu ? 2u : b == 0xceu ? 4u : b == 0xcfu ? 8u : ST_ERR;
-    // f(0) = s0, f(k) = k - 1 (k = 1..8), f(9) = 9
-    return 0x9765432100ull | s0;     // nibble k: f(k); f(1..8) = 0..7, f(9) = 9
-}
-__device__ inline uint32_t fn_at(uint64_t f, uint32_t s) { return (uint32_t)(f >> (4u * s)) & 15u; }
-__device__ inline uint64_t fn_then(uint64_t first, uint64_t second) {      // second o first
-    uint64_t r = 0;
-#pragma unroll
-    for (uint32_t s = 0; s < 10; ++s) r |= (uint64_t)fn_at(second, fn_at(first, s)) << (4u * s);
-    return r;
-}
-__device__ inline uint64_t shfl_up64(uint64_t v, uint32_t d) {
-    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, 64), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, 64);
-    return (uint64_t)lo | ((uint64_t)hi << 32);
-}
-// `count` elements from src[pos, end) into dst; returns the position after them, or ~0u if malformed
-__device__ inline uint32_t wave_unexpand(const uint8_t* src, uint32_t end, uint32_t pos, uint32_t count, uint8_t* dst) {
-    const uint32_t lane = __lane_id();
-    uint32_t done = 0, state = 0;
-    while (done < count) {
-        if (pos >= end) return ~0u;
-        const uint32_t q = pos + lane;
-        const bool in = q < end;
-        const uint32_t b = in ? src[q] : 0u;
-        uint64_t f = in ? fn_of_byte(b) : 0x9999999999ull;
-        uint64_t F = f;
-#pragma unroll
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint64_t o = shfl_up64(F, d);
-            if (lane >= d) F = fn_then(o, F);
-        }
-        const uint64_t Fprev = shfl_up64(F, 1);
-        const uint32_t s_in = lane == 0 ? state : fn_at(Fprev, state);
-        const uint32_t s_out = fn_at(f, s_in);
-        const bool emit = in && s_out == 0u;
-        const bool bad = in && (s_out == ST_ERR || (s_in >= 2u && s_in <= 8u && b != 0u));
-        const uint64_t em = __ballot(emit);
-        const uint32_t need = count - done;
-        // lanes up to the need-th emitting lane belong to this array
-        uint32_t last = 63u;
-        if ((uint32_t)__popcll(em) >= need) {
-            uint64_t m = em;
-            for (uint32_t k = 1; k < need; ++k) m &= m - 1;            // drop the first need-1 set bits
-            last = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-        }
-        const bool mine = lane <= last;
-        if (__ballot(mine && bad)) return ~0u;
-        if (emit && mine) dst[done + (uint32_t)__popcll(em & ((1ull << lane) - 1ull))] = (uint8_t)b;
-        const uint32_t took = (uint32_t)__popcll(em & (last == 63u ? ~0ull : ((2ull << last) - 1ull)));
-        state = (uint32_t)__shfl((int)s_out, (int)last, 64);
-        if (last == 63u && !__shfl((int)in, 63, 64)) return ~0u;      // ran past the end of the buffer
-        done += took;
-        pos += last + 1u;
-    }
-    wsync();
-    return state == 0u ? pos : ~0u;
-}
-
-struct DecScalars {
-    uint32_t ok, code, peer_none;
-    uint64_t ctime, round, height, ttl, rtime;
-    uint32_t has_sig, has_seal;
-};
-
-__global__ __launch_bounds__(64 * WAVES) void wire_decode_wave_kernel(const uint8_t* stream, const uint64_t* off,
-                                                                    uint64_t n, bftwire_batch out, uint8_t* has_sig,
-                                                                    uint8_t* has_seal, uint8_t* ok) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[WAVES * LDS_WAVE];
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint64_t i = (uint64_t)blockIdx.x * WAVES + wave;
-    if (i >= n) return;
-    uint8_t* F = lds + wave * LDS_WAVE + LDS_F;
-    uint8_t* G = lds + wave * LDS_WAVE + LDS_G;
-    uint8_t* S = lds + wave * LDS_WAVE + LDS_S;
-    uint8_t* SIG = lds + wave * LDS_WAVE + LDS_SP;          // signature, seal at +80
-    uint8_t* SEAL = SIG + 80;
-    const uint64_t o = off[i], len64 = off[i + 1] - o;
-    bool good = len64 >= 4 && len64 <= MAX_FRAME;
-    const uint32_t len = good ? (uint32_t)len64 : 0u;
-    for (uint32_t j = lane; j < len; j += 64u) F[j] = stream[o + j];
-    wsync();
-    // RawMessage header, serially (lane 0): size, [[Consensus, ttl, time, peer], payload
-    uint32_t v0 = 0, v1 = 0, v2 = 0;
-    DecScalars sc{};
-    if (lane == 0 && good) {
-        const uint32_t body = ((uint32_t)F[0] << 24) | ((uint32_t)F[1] << 16) | ((uint32_t)F[2] << 8) | F[3];
-        Mem m{F, len, 4};
-        uint32_t nn, idx, t;
-        bool g = body == len - 4u && rd_arr(m, nn) && nn == 2 && rd_arr(m, nn) && nn == 4 && rd_unit_variant(m, idx) &&
-                 idx == P2P_CONSENSUS && rd_uint(m, sc.ttl) && rd_uint(m, sc.rtime) && m.get(t);
-        if (g && t != 0xc0) {                                  // peer_id: Some (decoded, not returned)
-            g = rd_arr_tag(m, t, nn) && nn <= MAX_PEER;
-            for (uint32_t k = 0; g && k < nn; ++k) { uint64_t v; g = rd_uint(m, v) && v <= 255; }
-        }
-        uint32_t glen = 0;
-        g = g && rd_arr(m, glen) && glen <= MAX_G;
-        v0 = g ? 1u : 0u; v1 = m.i; v2 = glen;
-    }
-    good = __shfl((int)v0, 0, 64) != 0;
-    uint32_t p = (uint32_t)__shfl((int)v1, 0, 64), glen = (uint32_t)__shfl((int)v2, 0, 64);
-    if (good) good = wave_unexpand(F, len, p, glen, G) == len;
-    // GossipMessage header: [[code, []], create_time, msg array
-    if (lane == 0 && good) {
-        Mem m{G, glen, 0};
-        uint32_t nn = 0, idx = 0, slen = 0;
-        bool g = rd_arr(m, nn) && nn == 5 && rd_unit_variant(m, idx) && idx >= 1 && idx <= 3 && rd_uint(m, sc.ctime) &&
-                 rd_arr(m, slen) && slen <= MAX_S;
-        sc.code = idx + 1u;
-        v0 = g ? 1u : 0u; v1 = m.i; v2 = slen;
-    }
-    if (good) {
-        good = __shfl((int)v0, 0, 64) != 0;
-        p = (uint32_t)__shfl((int)v1, 0, 64);
-        const uint32_t slen = (uint32_t)__shfl((int)v2, 0, 64);
-        if (good) {
-            p = wave_unexpand(G, glen, p, slen, S);
-            good = p != ~0u;
-        }
-        // signature, commit_seal: nil or [65 elements]
-        uint8_t* dsts[2] = {SIG, SEAL};
-        uint32_t present[2] = {0, 0};
-        for (int k = 0; k < 2 && good; ++k) {
-            const uint32_t t = G[p < glen ? p : 0];
-            if (p >= glen) { good = false; break; }
-            if (t == 0xc0) { p += 1; continue; }
-            uint32_t hl = (t & 0xf0u) == 0x90u ? 1u : t == 0xdcu ? 3u : t == 0xddu ? 5u : 0u;
-            uint32_t nn = hl == 1u ? (t & 15u) : hl == 3u && p + 2 < glen ? ((uint32_t)G[p + 1] << 8) | G[p + 2]
-                        : hl == 5u && p + 4 < glen ? ((uint32_t)G[p + 1] << 24) | ((uint32_t)G[p + 2] << 16) |
-                                                      ((uint32_t)G[p + 3] << 8) | G[p + 4] : 0u;
-            if (hl == 0u || nn != 65u) { good = false; break; }
-            p = wave_unexpand(G, glen, p + hl, 65u, dsts[k]);
-            good = p != ~0u;
-            present[k] = 1;
-        }
-        good = good && p == glen;
-        sc.has_sig = present[0];
-        sc.has_seal = present[1];
-        // Subject: [[round, height], digest]
-        if (good) {
-            if (lane == 0) {
-                Mem m{S, slen, 0};
-                uint32_t nn, dl = 0;
-                bool g = rd_arr(m, nn) && nn == 2 && rd_arr(m, nn) && nn == 2 && rd_uint(m, sc.round) &&
-                         rd_uint(m, sc.height) && rd_arr(m, dl) && dl == 32;
-                v0 = g ? 1u : 0u; v1 = m.i;
-            }
-            good = __shfl((int)v0, 0, 64) != 0;
-            if (good) good = wave_unexpand(S, slen, (uint32_t)__shfl((int)v1, 0, 64), 32u, F) == slen;   // digest -> F
-        }
-    }
-    // outputs (F now holds the digest)
-    if (lane < 32) out.digest[32u * i + lane] = good ? F[lane] : 0;
-    for (uint32_t k = lane; k < 65u; k += 64u) {
-        out.signature[65u * i + k] = (good && sc.has_sig) ? SIG[k] : 0;
-        out.commit_seal[65u * i + k] = (good && sc.has_seal) ? SEAL[k] : 0;
-    }
-    if (lane == 0) {
-        out.code[i] = good ? (uint8_t)sc.code : 0;
-        out.round[i] = good ? sc.round : 0;
-        out.height[i] = good ? sc.height : 0;
-        out.create_time[i] = good ? sc.ctime : 0;
-        out.ttl[i] = good ? sc.ttl : 0;
-        out.raw_time[i] = good ? sc.rtime : 0;
-        has_sig[i] = good && sc.has_sig ? 1 : 0;
-        has_seal[i] = good && sc.has_seal ? 1 : 0;
-        ok[i] = good ? 1 : 0;
-    }
-}
-
 }  // namespace wire
 }  // namespace bft
 
@@ -460,7 +239,6 @@ struct bftwire {
     uint32_t *glen = nullptr, *splen = nullptr;
     void* scan_tmp = nullptr;
     size_t scan_bytes = 0;
-    int decode_mode = 0;           // 0 global lanes, 1 LDS-staged lanes, 2 wave-cooperative
     std::string err;
 };
 
@@ -505,8 +283,6 @@ int bftwire_create(int hip_device, bftwire_t** out) {
     if (!out) return -1;
     bftwire* h = new bftwire();
     h->device = hip_device;
-    const char* dm = getenv("BFTWIRE_DECODE");
-    h->decode_mode = (dm && strcmp(dm, "lds") == 0) ? 1 : (dm && strcmp(dm, "wave") == 0) ? 2 : 0;
     *out = h;
     WCHECK(h, hipSetDevice(hip_device));
     return 0;
@@ -564,15 +340,9 @@ int bftwire_decode(bftwire_t* h, const uint8_t* stream, const uint64_t* frame_of
         !out->digest || !out->create_time || !out->signature || !out->commit_seal || !out->ttl || !out->raw_time)
         return wfail(h, -1, "bftwire_decode: null buffer");
     WCHECK(h, hipSetDevice(h->device));
-    if (h->decode_mode == 0)       // product: lane per frame straight from global memory
-        hipLaunchKernelGGL(wire_decode_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream_,
-                           stream, frame_off, n, *out, has_sig, has_seal, ok);
-    else if (h->decode_mode == 1)  // BFTWIRE_DECODE=lds: frames staged in LDS first (A/B)
-        hipLaunchKernelGGL(wire_decode_lds_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream_,
-                           stream, frame_off, n, *out, has_sig, has_seal, ok);
-    else                           // BFTWIRE_DECODE=wave: the wave-cooperative decoder (A/B)
-        hipLaunchKernelGGL(wire_decode_wave_kernel, dim3((unsigned)((n + WAVES - 1) / WAVES)), dim3(64 * WAVES), 0,
-                           (hipStream_t)stream_, stream, frame_off, n, *out, has_sig, has_seal, ok);
+    // lane per frame straight from global memory
+    hipLaunchKernelGGL(wire_decode_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream_,
+                       stream, frame_off, n, *out, has_sig, has_seal, ok);
     WCHECK(h, hipGetLastError());
     return 0;
 }

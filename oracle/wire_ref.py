@@ -59,7 +59,9 @@ def decode(fr: bytes) -> dict | None:
         if uv != [P2P_CONSENSUS, []]:
             return None
         g = msgpack.unpackb(bytes(payload))
-        cv, ctime, msg, sig, seal = g
+        if not 3 <= len(g) <= 5:                 # signature / commit_seal are #[serde(default)]
+            return None
+        cv, ctime, msg, sig, seal = list(g) + [None] * (5 - len(g))
         if cv[1] != [] or not 1 <= cv[0] <= 3:
             return None
         (rnd, height), digest = msgpack.unpackb(bytes(msg))

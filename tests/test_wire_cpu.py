@@ -7,6 +7,8 @@ import re
 import struct
 import sys
 
+import msgpack
+
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -76,6 +78,27 @@ def test_malformed_frames_rejected():
     assert W.decode(pp) is None and R.decode(pp) is None
     for cut in range(4, len(f), 17):                                 # every truncation is rejected, never crashes
         assert W.decode(struct.pack(">I", cut - 4) + f[4:cut]) is None
+
+
+def test_short_gossip_arrays_default_to_none():
+    # GossipMessage.signature / commit_seal are #[serde(default)] (protocol/mod.rs:48-51): a 3- or
+    # 4-element array decodes with None for the missing options; 2 or 6 elements are rejected
+    rng = random.Random(6)
+    m = random_message(rng, peer=False)
+    m["code"] = 3
+    sub = R.subject(m["round"], m["height"], m["digest"])
+    for k in (3, 4):
+        g = msgpack.packb([[m["code"] - 1, []], m["create_time"], list(sub), list(m["signature"])][:k])
+        f = R.frame(g, ttl=m["ttl"], create_time=m["raw_time"])
+        want, got = R.decode(f), W.decode(f)
+        assert want is not None and want["commit_seal"] is None
+        assert (want["signature"] is None) == (k == 3)
+        assert got is not None and got["digest"] == want["digest"] and got["round"] == want["round"]
+        assert got["signature"] == want["signature"] and got["commit_seal"] is None
+    for k in (2, 6):
+        g = msgpack.packb(([[m["code"] - 1, []], m["create_time"], list(sub), None, None, None])[:k])
+        f = R.frame(g, ttl=m["ttl"], create_time=m["raw_time"])
+        assert R.decode(f) is None and W.decode(f) is None
 
 
 def test_split_frames_matches_codec_loop():
