@@ -265,7 +265,16 @@ def main():
         sim.launch(first, stream)
         torch.cuda.synchronize(dev)
     st = sim.stats()
-    tot = all_reduce_stats(st, device=dev)   # one int64 all-reduce (RCCL over xGMI)
+    # node-wide statistics: one RCCL all-reduce inside libbftsim (bftsim_stats_allreduce, over xGMI);
+    # torch.distributed's all-reduce of the same counts only if librccl cannot be opened
+    try:
+        from bftsim.distributed import capi_comm_init
+        capi_comm_init(sim, rank, world)
+        tot = sim.stats_allreduce()
+        reduce_via = "libbftsim bftsim_stats_allreduce (RCCL)"
+    except Exception as e:                 # noqa: BLE001 — reported in the JSON line
+        tot = all_reduce_stats(st, device=dev)
+        reduce_via = f"torch.distributed (bftsim_stats_allreduce failed: {e})"
     views_all, heights_all = tot["views"], tot["committed_heights"]
     safety_all, timeout_all = tot["flagged"][0], tot["flagged"][4]
 
@@ -336,6 +345,7 @@ def main():
                 "heights": args.heights, "parallelism": f"instance-sharded x{world}",
                 "pipelined": pipelined, "pipeline_depth": args.pipeline_depth if pipelined else 0,
                 "instance_rounds_per_step": views_all,
+                "stats_allreduce": reduce_via,
                 "committed_heights_per_step": heights_all,
                 "safety_violations": safety_all, "timeouts": timeout_all,
                 "rounds_to_commit_hist": trim(tot["round_hist"]),

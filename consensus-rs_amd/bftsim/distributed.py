@@ -45,6 +45,16 @@ def all_reduce_stats(st: Dict, device=None) -> Dict:
     return out
 
 
+def capi_comm_init(sim, rank: int, world: int):
+    """Join `sim` to the node's RCCL communicator of libbftsim (bftsim_comm_init): rank 0 makes the id,
+    the default torch.distributed group carries it to the other ranks (any channel would do)."""
+    import torch.distributed as dist
+    uid = [sim.comm_unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0)
+    sim.comm_init(world, rank, uid[0])
+
+
 def stats_from_result(r) -> Dict:
     """The bftsim_stats of a result dict (host arrays), as bft_stats_kernel computes it."""
     ch = r["committed_height"]

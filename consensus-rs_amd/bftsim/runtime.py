@@ -38,6 +38,9 @@ def lib():
         L.bftsim_sync.argtypes = [ctypes.c_void_p]
         L.bftsim_fetch.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.CResult)]
         L.bftsim_stats_get.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.CStats)]
+        L.bftsim_stats_allreduce.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.CStats)]
+        L.bftsim_comm_unique_id.argtypes = [ctypes.c_void_p]
+        L.bftsim_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
         L.bftsim_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
                                             ctypes.POINTER(ctypes.c_float)]
         L.bftsim_kernel_ms_sum.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
@@ -187,9 +190,32 @@ class Simulator:
         the following launches (include/bftsim.h bftsim_set_pipeline)."""
         _check(self.h, lib().bftsim_set_pipeline(self.h, depth if on else 0), "bftsim_set_pipeline")
 
-    def stats(self):
-        s = _abi.CStats()
-        _check(self.h, lib().bftsim_stats_get(self.h, ctypes.byref(s)), "bftsim_stats_get")
+    @staticmethod
+    def _stats_dict(s):
         return dict(instances=s.instances, committed_heights=s.committed_heights, views=s.views,
                     ticks=s.ticks, flagged=list(s.flagged), round_hist=list(s.round_hist),
                     latency_hist=list(s.latency_hist))
+
+    def stats(self):
+        s = _abi.CStats()
+        _check(self.h, lib().bftsim_stats_get(self.h, ctypes.byref(s)), "bftsim_stats_get")
+        return self._stats_dict(s)
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """rank 0: the 128-byte RCCL id every rank passes to comm_init (include/bftsim.h)"""
+        buf = ctypes.create_string_buffer(128)
+        rc = lib().bftsim_comm_unique_id(buf)
+        if rc != 0:
+            raise BftsimError(f"bftsim_comm_unique_id failed ({rc})")
+        return buf.raw
+
+    def comm_init(self, world: int, rank: int, unique_id: bytes):
+        assert len(unique_id) == 128
+        _check(self.h, lib().bftsim_comm_init(self.h, world, rank, unique_id), "bftsim_comm_init")
+
+    def stats_allreduce(self):
+        """bftsim_stats of the last launch summed over every rank: one RCCL all-reduce in libbftsim"""
+        s = _abi.CStats()
+        _check(self.h, lib().bftsim_stats_allreduce(self.h, ctypes.byref(s)), "bftsim_stats_allreduce")
+        return self._stats_dict(s)

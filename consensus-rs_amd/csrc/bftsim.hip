@@ -15,6 +15,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>                 // types only: librccl is opened at bftsim_comm_init (dlopen)
+
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -389,6 +393,8 @@ struct bftsim {
     uint8_t* d_hash = nullptr;
     unsigned long long* d_stats = nullptr;
     uint64_t* d_hist = nullptr;       // [HIST_BINS] of the last launch
+    uint64_t* d_red = nullptr;        // bftsim_stats image reduced by bftsim_stats_allreduce
+    ncclComm_t comm = nullptr;        // bftsim_comm_init: one rank of a multi-GPU run (RCCL over xGMI)
     uint8_t* d_tips = nullptr;        // [cap_inst * 32]
     uint32_t* d_rcs = nullptr;        // RoundChangeSet tables, rcs_words(seg) per wave / workgroup
     uint32_t* d_backlog = nullptr;    // replay mode: backlog slots, backlog_words(seg) per wave / workgroup
@@ -479,6 +485,43 @@ static uint64_t* g_stamps = nullptr;
 static uint64_t g_stamp_waves = 0;
 #endif
 
+// ------------------------------------------------------------------------------ RCCL (multi-GPU)
+// The one collective of the path: the run statistics of every rank summed over RCCL.
+// librccl is opened on first use (the soname torch also loads, so one copy serves the process);
+// the library itself stays loadable without it.
+namespace {
+struct Rccl {
+    ncclResult_t (*get_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                               hipStream_t) = nullptr;
+    ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+    const char* (*err)(ncclResult_t) = nullptr;
+    bool ok = false;
+    std::string why;
+};
+Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!lib) lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!lib) { r.why = std::string("dlopen librccl.so.1: ") + dlerror(); return; }
+        r.get_id = (decltype(r.get_id))dlsym(lib, "ncclGetUniqueId");
+        r.init_rank = (decltype(r.init_rank))dlsym(lib, "ncclCommInitRank");
+        r.all_reduce = (decltype(r.all_reduce))dlsym(lib, "ncclAllReduce");
+        r.destroy = (decltype(r.destroy))dlsym(lib, "ncclCommDestroy");
+        r.err = (decltype(r.err))dlsym(lib, "ncclGetErrorString");
+        r.ok = r.get_id && r.init_rank && r.all_reduce && r.destroy && r.err;
+        if (!r.ok) r.why = "librccl.so.1 lacks an entry point";
+    });
+    return r;
+}
+void comm_destroy(ncclComm_t c) {
+    if (rccl().ok) (void)rccl().destroy(c);
+}
+}  // namespace
+
 extern "C" {
 
 #ifdef BFT_STAMPS
@@ -562,6 +605,8 @@ void bftsim_destroy(bftsim_t* h) {
     (void)hipSetDevice(h->device);
     free_bufs(h);
     (void)hipFree(h->d_addr); (void)hipFree(h->d_ghash); (void)hipFree(h->d_stats); (void)hipFree(h->d_hist);
+    (void)hipFree(h->d_red);
+    if (h->comm) comm_destroy(h->comm);
     for (uint32_t i = 0; i < bftsim::RING; ++i) {
         if (h->ring[i].c0) (void)hipEventDestroy(h->ring[i].c0);
         if (h->ring[i].c1) (void)hipEventDestroy(h->ring[i].c1);
@@ -904,6 +949,56 @@ int bftsim_fetch_summary(bftsim_t* h, uint64_t* committed_height, uint32_t* flag
     if (ticks) HIPCHECK(h, hipMemcpy(ticks, h->d_ticks, n * 4, hipMemcpyDeviceToHost));
     if (views) HIPCHECK(h, hipMemcpy(views, h->d_views, n * 8, hipMemcpyDeviceToHost));
     if (tip_hash) HIPCHECK(h, hipMemcpy(tip_hash, h->d_tips, n * 32, hipMemcpyDeviceToHost));
+    return BFTSIM_OK;
+}
+
+int bftsim_comm_unique_id(uint8_t out[128]) {
+    static_assert(sizeof(ncclUniqueId) == 128, "NCCL_UNIQUE_ID_BYTES");
+    if (!out) return BFTSIM_EINVAL;
+    Rccl& r = rccl();
+    if (!r.ok) return BFTSIM_EUNSUPPORTED;
+    ncclUniqueId id;
+    if (r.get_id(&id) != ncclSuccess) return BFTSIM_EHIP;
+    memcpy(out, &id, 128);
+    return BFTSIM_OK;
+}
+
+int bftsim_comm_init(bftsim_t* h, int world_size, int rank, const uint8_t unique_id[128]) {
+    if (!h || !unique_id || world_size < 1 || rank < 0 || rank >= world_size)
+        return fail(h, BFTSIM_EINVAL, "bftsim_comm_init: bad world / rank");
+    Rccl& r = rccl();
+    if (!r.ok) return fail(h, BFTSIM_EUNSUPPORTED, r.why);
+    HIPCHECK(h, hipSetDevice(h->device));
+    if (h->comm) { comm_destroy(h->comm); h->comm = nullptr; }
+    ncclUniqueId id;
+    memcpy(&id, unique_id, 128);
+    ncclResult_t e = r.init_rank(&h->comm, world_size, id, rank);
+    if (e != ncclSuccess) { h->comm = nullptr; return fail(h, BFTSIM_EHIP, std::string("ncclCommInitRank: ") + r.err(e)); }
+    if (!h->d_red) HIPCHECK(h, hipMalloc(&h->d_red, sizeof(bftsim_stats)));
+    return BFTSIM_OK;
+}
+
+// bftsim_stats of the last launch of every rank, summed (every field is a count): the device image of
+// the local statistics, one ncclAllReduce(sum, uint64) over xGMI on the launch stream, one copy back
+int bftsim_stats_allreduce(bftsim_t* h, bftsim_stats* out) {
+    if (!h || !out) return BFTSIM_EINVAL;
+    if (!h->comm) return fail(h, BFTSIM_EINVAL, "bftsim_comm_init not called");
+    if (h->last_n == 0 || !h->d_ch) return fail(h, BFTSIM_EINVAL, "nothing launched");
+    static_assert(sizeof(bftsim_stats) == (11 + bft::HIST_BINS) * 8, "bftsim_stats: a flat array of uint64 counts");
+    HIPCHECK(h, hipSetDevice(h->device));
+    bft::Params p = make_params(h, h->last_first, h->last_n);
+    hipStream_t s = h->last_stream;
+    HIPCHECK(h, hipMemsetAsync(h->d_stats, 0, 16 * 8, s));
+    uint32_t g = (uint32_t)((h->last_n + 255) / 256);
+    hipLaunchKernelGGL(bft::bft_stats_kernel, dim3(g), dim3(256), 0, s, p, h->d_stats);
+    HIPCHECK(h, hipGetLastError());
+    HIPCHECK(h, hipMemcpyAsync(h->d_red, h->d_stats, 11 * 8, hipMemcpyDeviceToDevice, s));
+    HIPCHECK(h, hipMemcpyAsync(h->d_red + 11, h->d_hist, bft::HIST_BINS * 8, hipMemcpyDeviceToDevice, s));
+    Rccl& r = rccl();
+    ncclResult_t e = r.all_reduce(h->d_red, h->d_red, sizeof(bftsim_stats) / 8, ncclUint64, ncclSum, h->comm, s);
+    if (e != ncclSuccess) return fail(h, BFTSIM_EHIP, std::string("ncclAllReduce: ") + r.err(e));
+    HIPCHECK(h, hipMemcpyAsync(out, h->d_red, sizeof(bftsim_stats), hipMemcpyDeviceToHost, s));
+    HIPCHECK(h, hipStreamSynchronize(s));
     return BFTSIM_OK;
 }
 

@@ -120,6 +120,16 @@ int bftsim_launch(bftsim_t *h, uint64_t first_instance, void *hip_stream);   /* 
 int bftsim_sync(bftsim_t *h);
 int bftsim_fetch(bftsim_t *h, bftsim_result *out);
 int bftsim_stats_get(bftsim_t *h, bftsim_stats *out);   /* device reduction + copy */
+/* multi-GPU (one process per GPU): the instances shard over the ranks with no data-path
+ * collective; the statistics of every rank are summed by one RCCL all-reduce over xGMI. Rank 0 makes
+ * the 128-byte id (ncclGetUniqueId) and the host hands it to every rank (any channel); each rank
+ * then joins with its handle. Replaces the per-node Engine of create_bft_engine
+ * (src/consensus/consensus.rs:42-60) with one engine per device and a node-wide statistic.
+ * BFTSIM_EUNSUPPORTED when librccl.so.1 cannot be opened. */
+int bftsim_comm_unique_id(uint8_t unique_id[128]);
+int bftsim_comm_init(bftsim_t *h, int world_size, int rank, const uint8_t unique_id[128]);
+/* bftsim_stats of the last launch summed over every rank (collective: every rank calls it) */
+int bftsim_stats_allreduce(bftsim_t *h, bftsim_stats *out);
 /* per-kernel device time of the last launch, from HIP events on the launch stream (ms) */
 int bftsim_last_kernel_ms(bftsim_t *h, float *consensus_ms, float *hash_ms);
 /* summed per-kernel device times (ms) of every launch since the previous call, without blocking
