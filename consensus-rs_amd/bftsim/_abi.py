@@ -34,6 +34,12 @@ class CStats(ctypes.Structure):
                 ("latency_hist", ctypes.c_uint64 * 65)]
 
 
+class CCryptoReport(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint64) for k in (
+        "messages", "seals", "forged", "recovered_as_sender", "mismatches", "seal_errors", "signatures",
+        "recoveries", "log_overflows")]
+
+
 def to_cconfig(cfg: BftConfig):
     """Returns (struct, keepalive) — keep the second object alive while the struct is used."""
     c = CConfig()

@@ -40,6 +40,9 @@ def lib():
         L.bftsim_stats_get.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.CStats)]
         L.bftsim_stats_allreduce.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.CStats)]
         L.bftsim_comm_unique_id.argtypes = [ctypes.c_void_p]
+        L.bftsim_set_crypto.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32]
+        L.bftsim_crypto_verify.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.CCryptoReport), ctypes.c_void_p,
+                                           ctypes.c_void_p]
         L.bftsim_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
         L.bftsim_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
                                             ctypes.POINTER(ctypes.c_float)]
@@ -64,6 +67,13 @@ def lib():
         L.bftsim_export_headers.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         _lib = L
     return _lib
+
+
+def keccak256(data: bytes) -> bytes:
+    """Keccak-256 (`hash`, cryptocurrency-kit) through libbftsim (host code, no GPU needed)."""
+    out = ctypes.create_string_buffer(32)
+    lib().bftsim_keccak256(data, len(data), out)
+    return out.raw
 
 
 def _check(h, rc, what):
@@ -103,6 +113,7 @@ class Simulator:
             _check(self.h, lib().bftsim_set_trace(self.h, tr.ctypes.data, trace_ticks), "set_trace")
         try:
             _check(self.h, lib().bftsim_run(self.h, first, n, ctypes.byref(r)), "bftsim_run")
+            self.n_prepared = n
         finally:
             if trace_ticks:
                 lib().bftsim_set_trace(self.h, None, 0)
@@ -200,6 +211,30 @@ class Simulator:
         s = _abi.CStats()
         _check(self.h, lib().bftsim_stats_get(self.h, ctypes.byref(s)), "bftsim_stats_get")
         return self._stats_dict(s)
+
+    def set_crypto(self, secrets, forged=(), log_cap: int = 0):
+        """Real-crypto mode (include/bftsim.h bftsim_set_crypto, SPEC.md §11): `secrets` = one 32-byte
+        key per validator in the sorted validator order (None turns the mode off); `forged` = indices
+        that sign with a key that is not theirs. Applies at the next prepare."""
+        if secrets is None:
+            _check(self.h, lib().bftsim_set_crypto(self.h, None, None, 0), "bftsim_set_crypto")
+            return
+        assert len(secrets) == self.cfg.n and all(len(k) == 32 for k in secrets)
+        fb = bytes(1 if v in set(forged) else 0 for v in range(self.cfg.n))
+        _check(self.h, lib().bftsim_set_crypto(self.h, b"".join(secrets), fb, log_cap), "bftsim_set_crypto")
+
+    def crypto_verify(self):
+        """The batched sign / recover pass over the last launch's messages: report dict, per-instance
+        checksum [n, 32] (XOR of keccak(signature || seal)) and message counts [n]."""
+        n = self.n_prepared
+        rep = _abi.CCryptoReport()
+        ck = np.zeros((n, 32), np.uint8)
+        cnt = np.zeros(n, np.uint32)
+        _check(self.h, lib().bftsim_crypto_verify(self.h, ctypes.byref(rep), ck.ctypes.data, cnt.ctypes.data),
+               "bftsim_crypto_verify")
+        out = {k: getattr(rep, k) for k, _ in _abi.CCryptoReport._fields_}
+        out["checksum"], out["inst_messages"] = ck, cnt
+        return out
 
     @staticmethod
     def comm_unique_id() -> bytes:

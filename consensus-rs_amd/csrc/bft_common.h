@@ -67,7 +67,18 @@ struct Params {
     uint32_t backlog_replay;          // BFTSIM_BACKLOG_REPLAY (SPEC.md §10)
     uint32_t pad3;
     uint32_t* backlog;                // replay mode: per wave / workgroup [S slots][5 words][L lanes]
+    // real-crypto mode (SPEC.md §11): every consensus message broadcast is logged for the batched
+    // sign / recover pass; a forged sender's messages reach no receiver
+    uint32_t* mlog;                   // [n_inst][mlog_cap][MLOG_WORDS] (nullptr: mode off)
+    uint32_t* mlog_n;                 // [n_inst] messages logged (may exceed mlog_cap: overflow)
+    uint32_t mlog_cap;
+    uint32_t pad4;
+    uint64_t forged[4];               // validators signing with a key that is not theirs
 };
+// one logged broadcast: {tick, phase | code << 8 | sender << 16, height, round, block id lo, hi,
+// flags (MLOG_*), 0}; code = MessageType 1..4 (Preprepare .. RoundChange)
+constexpr uint32_t MLOG_WORDS = 8;
+constexpr uint32_t MLOG_FORGED = 1u, MLOG_WILD = 2u, MLOG_EQUIV = 4u, MLOG_OLD = 8u;
 
 // flags (same bits as the oracle)
 constexpr uint32_t FLAG_SAFETY = 1u, FLAG_PHASE_CAP = 2u, FLAG_CORE_PANIC = 4u, FLAG_OUTBOX = 8u,

@@ -164,6 +164,7 @@ struct Sim {
     uint32_t lane_flags;
     uint32_t* rcs_base;      // this wave's RoundChangeSet table (global)
     uint32_t* bl_base;       // this wave's backlog slots (global, replay mode)
+    uint32_t mlog_cnt;       // real-crypto mode: messages logged so far by this instance (segment-uniform)
 #ifdef BFT_STAMPS
     uint64_t st_acc[12];
     uint64_t st_t;
@@ -206,6 +207,7 @@ struct Sim {
         for (uint32_t k = 0; k < 12; ++k) *cache_p(k) = 0;
         outbox_init(nx);
         commit_x = 0; commit_round = 0; commit_seed = 0; commit_blk = 0;
+        mlog_cnt = 0;
         lane_flags = 0;
         off_inst = offset_inst_part(p.seed, inst);
         rcs_base = p.rcs + (uint64_t)wave_global * LY::RCS_WORDS;
@@ -607,6 +609,45 @@ struct Sim {
             else if (code == MT_COMMIT) handle_commit(s, vh, vr, d, (hd & 16u) != 0);
             else handle_round_change(s, vh, vr);
         }
+    }
+
+    // ---------------------------------------------------------------- real-crypto mode (SPEC.md §11)
+    // At the start of a phase every sender's consensus messages (the outbox kinds that are
+    // GossipMessages: Preprepare, Prepare, old-block Commit, Commit, RoundChange) are broadcast, i.e.
+    // signed (core.rs:425-429). They are logged in (sender, kind) order for the batched sign / recover
+    // pass; a forged sender's signature recovers a non-validator, so handle_message (core.rs:314-322)
+    // drops them at every receiver, the sender included: they leave the outbox here.
+    static constexpr uint32_t F_CONS = F_PP | F_PP_EQ | F_PR | F_PR_W | F_CM | F_CM_W | F_OCM | F_OCM_W | F_RC;
+    BFT_FN void mlog_put(uint32_t idx, uint32_t code, uint32_t h_, uint32_t r_, uint64_t b, uint32_t fl,
+                         uint32_t phase) {
+        if (idx >= P.mlog_cap) return;                // counted, not stored: overflow (bftsim_crypto_verify)
+        uint32_t* e = P.mlog + ((uint64_t)inst_local * P.mlog_cap + idx) * MLOG_WORDS;
+        e[0] = (uint32_t)tick; e[1] = phase | (code << 8) | (me << 16); e[2] = h_; e[3] = r_;
+        e[4] = (uint32_t)b; e[5] = (uint32_t)(b >> 32); e[6] = fl; e[7] = 0;
+    }
+    BFT_FN void crypto_log(bool act, uint32_t phase) {
+        const uint32_t f = act ? nx.f : 0u;
+        const uint32_t nk = ((f & F_PP) ? 1u : 0u) + ((f & F_PR) ? 1u : 0u) + ((f & F_OCM) ? 1u : 0u) +
+                            ((f & F_CM) ? 1u : 0u) + ((f & F_RC) ? 1u : 0u);
+        // this lane's first slot: the messages of the lower senders of the segment (3 ballots of nk's bits)
+        const M below = seg_mask & M::low(lane);
+        uint32_t pre = 0, tot = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 3; ++b) {
+            const M bb = ballot(((nk >> b) & 1u) != 0);
+            pre += (bb & below).popc() << b;
+            tot += (bb & seg_mask).popc() << b;
+        }
+        uint32_t idx = mlog_cnt + pre;
+        const bool forged = is_val && ((P.forged[(me >> 6) & 3u] >> (me & 63u)) & 1ull);
+        const uint32_t ff = forged ? MLOG_FORGED : 0u;
+        if (f & F_PP) mlog_put(idx++, MT_PREPREPARE, nx.pp_h, nx.pp_r, nx.pp_b, ff | ((f & F_PP_EQ) ? MLOG_EQUIV : 0u), phase);
+        if (f & F_PR) mlog_put(idx++, MT_PREPARE, nx.pr_h, nx.pr_r, nx.pr_d, ff | ((f & F_PR_W) ? MLOG_WILD : 0u), phase);
+        if (f & F_OCM) mlog_put(idx++, MT_COMMIT, nx.ocm_h, nx.ocm_r, nx.ocm_d, ff | MLOG_OLD | ((f & F_OCM_W) ? MLOG_WILD : 0u), phase);
+        if (f & F_CM) mlog_put(idx++, MT_COMMIT, nx.cm_h, nx.cm_r, nx.cm_d, ff | ((f & F_CM_W) ? MLOG_WILD : 0u), phase);
+        if (f & F_RC) mlog_put(idx++, MT_ROUND_CHANGE, nx.rc_h, nx.rc_r, 0, ff, phase);
+        mlog_cnt += tot;
+        if (forged) nx.f &= ~F_CONS;
     }
 
     // ---------------------------------------------------------------- phase machinery
@@ -1171,6 +1212,7 @@ struct Sim {
                 M bal = ballot(pend_l);
                 if (bal.none()) break;
                 bool seg_pending = (bal & seg_mask).any();
+                if (P.mlog) crypto_log(act && !frozen, p);      // real-crypto mode (SPEC.md §11)
                 if (p >= P.phase_cap) {
                     // messages still in flight are dropped (SPEC.md §2)
                     M inflight = ballot(act && nx.f != 0);
@@ -1234,6 +1276,7 @@ struct Sim {
             P.flags[inst_local] = flags;
             P.ticks[inst_local] = done_tick;
             P.views[inst_local] = views;
+            if (P.mlog) P.mlog_n[inst_local] = mlog_cnt;
         }
     }
 };

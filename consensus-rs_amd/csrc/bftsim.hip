@@ -27,6 +27,7 @@
 #include "bft_common.h"
 #include "bft_wave.h"
 #include "bft_fast64.h"
+#include "bft_crypto.h"
 
 namespace bft {
 
@@ -366,6 +367,181 @@ __global__ __launch_bounds__(256) void bft_tip_kernel(Params p, uint8_t* tips) {
     for (int i = 0; i < 32; ++i) tips[(uint64_t)il * 32 + i] = src[i];
 }
 
+
+// ------------------------------------------------------------------------------ real-crypto mode
+// The batched sign / recover pass over a launch's broadcast log (SPEC.md §11; bftsim_crypto_verify).
+struct CryptoArgs {
+    const uint32_t* mlog;
+    const uint32_t* mlog_n;
+    uint32_t cap;
+    uint32_t n_val;
+    const uint64_t* moff;             // [n_inst] first dense message index of each instance
+    uint64_t forged[4];
+    // dense, per message
+    uint64_t* mref;                   // instance * cap + slot
+    uint8_t* raw;                     // Subject digest (block hash, zeros for RoundChange)
+    uint32_t* key;                    // signing key: sender, or n_val + sender (forged key)
+    uint32_t* msg_k;                  // commit seal index
+    uint8_t* sign_dig;
+    uint8_t* sigs;
+    uint8_t* rec_addr;
+    uint8_t* rec_ok;
+    // dense, per commit
+    uint32_t* ncm;
+    uint8_t* seal_dig;
+    uint8_t* seal_raw;
+    uint32_t* seal_key;
+    uint8_t* seals;
+    uint8_t* seal_ok;
+    // results
+    uint32_t* inst_ck;                // [n_inst][8] XOR of keccak(signature || seal)
+    unsigned long long* counts;       // [8] messages, commits, forged, recovered-as-sender, mismatches, seal errors
+};
+
+// parent hash of the block at height x as the run left it: the canonical row x-1 (genesis at 1); a
+// height above the committed chain + 1 has no known parent and uses 0^32 (SPEC.md §11)
+__device__ inline void crypto_parent(const Params& p, uint32_t il, uint32_t x, uint32_t prev[8]) {
+    const uint32_t ch = p.committed_height[il];
+    if (x <= 1) {
+        for (int i = 0; i < 8; ++i)
+            prev[i] = (uint32_t)p.genesis_hash[4 * i] | ((uint32_t)p.genesis_hash[4 * i + 1] << 8) |
+                      ((uint32_t)p.genesis_hash[4 * i + 2] << 16) | ((uint32_t)p.genesis_hash[4 * i + 3] << 24);
+    } else if (x - 1 <= ch) {
+        const uint32_t* ph = (const uint32_t*)(p.hash + ((uint64_t)il * p.rows + (x - 1)) * 32);
+        for (int i = 0; i < 8; ++i) prev[i] = ph[i];
+    } else {
+        for (int i = 0; i < 8; ++i) prev[i] = 0;
+    }
+}
+// Subject digest of a logged block id: the canonical row's hash when the block is the committed one
+// at its height, else the hash of its header over crypto_parent
+__device__ inline void crypto_block_digest(const Params& p, uint32_t il, uint64_t b, uint8_t* hbuf, uint8_t out[32]) {
+    const uint32_t x = blk_h(b), prop = blk_prop(b), var = blk_var(b);
+    if (!blk_valid(b) || x == 0) { for (int i = 0; i < 32; ++i) out[i] = 0; return; }
+    if (x <= p.committed_height[il]) {
+        const uint32_t* row = p.rec + ((uint64_t)il * p.rows + x) * 4;
+        if ((row[1] & 0xffffu) == prop && ((row[1] >> 16) & 1u) == var) {
+            const uint8_t* hs = p.hash + ((uint64_t)il * p.rows + x) * 32;
+            for (int i = 0; i < 32; ++i) out[i] = hs[i];
+            return;
+        }
+    }
+    uint32_t prev[8], w[8];
+    crypto_parent(p, il, x, prev);
+    const uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)blk_T(b) + 1ull);
+    lane_block_hash(hbuf, prev, p.addresses + 20u * prop, p.seed, p.first_instance + il, x, prop, var, time, w);
+    for (int i = 0; i < 32; ++i) out[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+}
+
+// pass 1 (workgroup per instance): digests, signing keys, the commits' seal digests
+__global__ __launch_bounds__(64) void bft_crypto_prep_kernel(Params p, CryptoArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t hb[64 * LANE_HASH_BUF];
+    __shared__ uint8_t kb[64 * 136];
+    uint8_t* hbuf = hb + threadIdx.x * LANE_HASH_BUF;
+    uint8_t* kbuf = kb + threadIdx.x * 136;
+    const uint32_t il = blockIdx.x;
+    const uint32_t cnt = a.mlog_n[il] < a.cap ? a.mlog_n[il] : a.cap;
+    for (uint32_t j = threadIdx.x; j < cnt; j += 64u) {
+        const uint32_t* e = a.mlog + ((uint64_t)il * a.cap + j) * MLOG_WORDS;
+        const uint64_t m = a.moff[il] + j;
+        const uint32_t code = (e[1] >> 8) & 0xffu, sender = e[1] >> 16;
+        const bool forged = (e[6] & MLOG_FORGED) != 0;
+        uint8_t d[32];
+        if (code == MT_ROUND_CHANGE) { for (int i = 0; i < 32; ++i) d[i] = 0; }     // EMPTY_HASH (round_change.rs:55-58)
+        else crypto_block_digest(p, il, (uint64_t)e[4] | ((uint64_t)e[5] << 32), hbuf, d);
+        for (int i = 0; i < 32; ++i) a.raw[m * 32 + i] = d[i];
+        const uint32_t key = sender + (forged ? a.n_val : 0u);
+        a.key[m] = key;
+        a.mref[m] = (uint64_t)il * a.cap + j;
+        if (code == MT_COMMIT) {
+            const uint32_t k = atomicAdd(a.ncm, 1u);
+            a.msg_k[m] = k;
+            a.seal_key[k] = key;
+            uint8_t sd[32];
+            crypto::seal_digest(kbuf, d, sd);
+            for (int i = 0; i < 32; ++i) { a.seal_dig[(uint64_t)k * 32 + i] = sd[i]; a.seal_raw[(uint64_t)k * 32 + i] = d[i]; }
+        }
+    }
+}
+
+// pass 2 (lane per message): the sign digest of the GossipMessage (signature None, the seal of a Commit)
+__global__ __launch_bounds__(64) void bft_crypto_digest_kernel(Params p, CryptoArgs a, uint64_t M) {
+    __shared__ __attribute__((aligned(16))) uint8_t hb[64 * LANE_HASH_BUF];
+    __shared__ uint8_t kb[64 * 136];
+    const uint64_t m = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (m >= M) return;
+    uint8_t* hbuf = hb + threadIdx.x * LANE_HASH_BUF;
+    uint8_t* kbuf = kb + threadIdx.x * 136;
+    const uint64_t ref = a.mref[m];
+    const uint32_t il = (uint32_t)(ref / a.cap);
+    const uint32_t* e = a.mlog + ref * MLOG_WORDS;
+    const uint32_t code = (e[1] >> 8) & 0xffu, tick = e[0];
+    const uint32_t h_ = e[2], r_ = e[3];
+    // create_time: RoundChange carries the wall clock in ms (round_change.rs:61), the others 0
+    const uint64_t ctime = code == MT_ROUND_CHANGE
+                               ? 1000ull * (p.genesis_time + (uint64_t)p.block_period * (uint64_t)tick) : 0ull;
+    const uint8_t* seal = code == MT_COMMIT ? a.seals + (uint64_t)a.msg_k[m] * 65 : nullptr;
+    uint8_t out[32];
+    if (code == MT_PREPREPARE) {
+        const uint64_t b = (uint64_t)e[4] | ((uint64_t)e[5] << 32);
+        const uint32_t x = blk_h(b), prop = blk_prop(b), var = blk_var(b);
+        uint32_t prev[8];
+        crypto_parent(p, il, x, prev);
+        const uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)blk_T(b) + 1ull);
+        const uint32_t hlen = header_raw((uint64_t*)hbuf, prev, p.addresses + 20u * prop, p.seed, p.first_instance + il,
+                                         x, prop, var, time);
+        crypto::sign_digest(kbuf, code, ctime, r_, h_, nullptr, hbuf, hlen, nullptr, out);
+    } else {
+        crypto::sign_digest(kbuf, code, ctime, r_, h_, a.raw + m * 32, nullptr, 0, seal, out);
+    }
+    for (int i = 0; i < 32; ++i) a.sign_dig[m * 32 + i] = out[i];
+}
+
+// pass 3 (lane per message): the receivers' checks (handle_message, core.rs:314-322: the recovered
+// address must be a validator; verify_commit, commit.rs:94-100: the seal must recover) against what the
+// simulation assumed (forged senders dropped, everyone else accepted), and the per-instance checksum
+__global__ __launch_bounds__(64) void bft_crypto_check_kernel(Params p, CryptoArgs a, uint64_t M) {
+    __shared__ uint8_t kb[64 * 136];
+    const uint64_t m = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (m >= M) return;
+    uint8_t* kbuf = kb + threadIdx.x * 136;
+    const uint64_t ref = a.mref[m];
+    const uint32_t il = (uint32_t)(ref / a.cap);
+    const uint32_t* e = a.mlog + ref * MLOG_WORDS;
+    const uint32_t code = (e[1] >> 8) & 0xffu, sender = e[1] >> 16;
+    const bool forged = (e[6] & MLOG_FORGED) != 0;
+    const uint8_t* ra = a.rec_addr + m * 20;
+    bool member = false, as_sender = false;
+    if (a.rec_ok[m]) {
+        for (uint32_t v = 0; v < a.n_val; ++v) {
+            bool eq = true;
+            for (int i = 0; i < 20 && eq; ++i) eq = ra[i] == p.addresses[20u * v + i];
+            if (eq) { member = true; as_sender = as_sender || v == sender; }
+        }
+    }
+    bool seal_err = false;
+    const uint8_t* seal = nullptr;
+    if (code == MT_COMMIT) {
+        const uint32_t k = a.msg_k[m];
+        seal = a.seals + (uint64_t)k * 65;
+        seal_err = !a.seal_ok[k];
+    }
+    const bool mismatch = forged ? member : !as_sender;
+    uint8_t t[32];
+    crypto::sig_term(kbuf, a.sigs + m * 65, seal, t);
+    for (int w = 0; w < 8; ++w) {
+        const uint32_t v = (uint32_t)t[4 * w] | ((uint32_t)t[4 * w + 1] << 8) | ((uint32_t)t[4 * w + 2] << 16) |
+                           ((uint32_t)t[4 * w + 3] << 24);
+        atomicXor(a.inst_ck + (uint64_t)il * 8 + w, v);
+    }
+    atomicAdd(a.counts + 0, 1ull);
+    if (code == MT_COMMIT) atomicAdd(a.counts + 1, 1ull);
+    if (forged) atomicAdd(a.counts + 2, 1ull);
+    if (as_sender) atomicAdd(a.counts + 3, 1ull);
+    if (mismatch) atomicAdd(a.counts + 4, 1ull);
+    if (seal_err) atomicAdd(a.counts + 5, 1ull);
+}
+
 }  // namespace bft
 
 #include "bft_host.h"
@@ -395,6 +571,14 @@ struct bftsim {
     uint64_t* d_hist = nullptr;       // [HIST_BINS] of the last launch
     uint64_t* d_red = nullptr;        // bftsim_stats image reduced by bftsim_stats_allreduce
     ncclComm_t comm = nullptr;        // bftsim_comm_init: one rank of a multi-GPU run (RCCL over xGMI)
+    // real-crypto mode (bftsim_set_crypto, SPEC.md §11)
+    bool crypto = false;
+    uint64_t forged[4] = {0, 0, 0, 0};
+    uint32_t mlog_cap = 0;
+    uint32_t* d_mlog = nullptr;       // [cap_inst][mlog_cap][MLOG_WORDS]
+    uint32_t* d_mlog_n = nullptr;     // [cap_inst]
+    uint8_t* d_keys = nullptr;        // [2N][32]: the validators' secrets, then their forged keys
+    void* sig = nullptr;              // libbftsig handle (bftsig_t*)
     uint8_t* d_tips = nullptr;        // [cap_inst * 32]
     uint32_t* d_rcs = nullptr;        // RoundChangeSet tables, rcs_words(seg) per wave / workgroup
     uint32_t* d_backlog = nullptr;    // replay mode: backlog slots, backlog_words(seg) per wave / workgroup
@@ -458,6 +642,8 @@ static void free_bufs(bftsim* h) {
     h->d_rcs = nullptr;
     (void)hipFree(h->d_backlog);
     h->d_backlog = nullptr;
+    (void)hipFree(h->d_mlog); (void)hipFree(h->d_mlog_n);
+    h->d_mlog = nullptr; h->d_mlog_n = nullptr;
     h->backlog_bytes = 0;
     (void)hipFree(h->d_resume); (void)hipFree(h->d_save);
     h->d_resume = nullptr; h->d_save = nullptr;
@@ -519,6 +705,43 @@ Rccl& rccl() {
 }
 void comm_destroy(ncclComm_t c) {
     if (rccl().ok) (void)rccl().destroy(c);
+}
+
+// libbftsig (include/bftsig.h), next to this library: the batched secp256k1 of real-crypto mode
+struct SigApi {
+    int (*create)(int, void**) = nullptr;
+    void (*destroy)(void*) = nullptr;
+    const char* (*last_error)(const void*) = nullptr;
+    int (*secret_to_address)(void*, const uint8_t*, uint64_t, uint8_t*, uint8_t*, uint8_t*, void*) = nullptr;
+    int (*sign)(void*, const uint8_t*, const uint32_t*, const uint8_t*, uint64_t, uint8_t*, uint8_t*, void*) = nullptr;
+    int (*recover)(void*, const uint8_t*, const uint8_t*, uint64_t, uint8_t*, uint8_t*, uint8_t*, void*) = nullptr;
+    bool ok = false;
+    std::string why;
+};
+void sig_api_anchor() {}
+SigApi& sig_api() {
+    static SigApi a;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        Dl_info di;
+        std::string path = "libbftsig.so";
+        if (dladdr((void*)&sig_api_anchor, &di) && di.dli_fname) {
+            std::string self = di.dli_fname;
+            size_t k = self.rfind('/');
+            if (k != std::string::npos) path = self.substr(0, k + 1) + "libbftsig.so";
+        }
+        void* lib = dlopen(path.c_str(), RTLD_NOW | RTLD_GLOBAL);
+        if (!lib) { a.why = std::string("dlopen ") + path + ": " + dlerror(); return; }
+        a.create = (decltype(a.create))dlsym(lib, "bftsig_create");
+        a.destroy = (decltype(a.destroy))dlsym(lib, "bftsig_destroy");
+        a.last_error = (decltype(a.last_error))dlsym(lib, "bftsig_last_error");
+        a.secret_to_address = (decltype(a.secret_to_address))dlsym(lib, "bftsig_secret_to_address");
+        a.sign = (decltype(a.sign))dlsym(lib, "bftsig_sign");
+        a.recover = (decltype(a.recover))dlsym(lib, "bftsig_recover");
+        a.ok = a.create && a.destroy && a.last_error && a.secret_to_address && a.sign && a.recover;
+        if (!a.ok) a.why = path + " lacks an entry point";
+    });
+    return a;
 }
 }  // namespace
 
@@ -606,7 +829,9 @@ void bftsim_destroy(bftsim_t* h) {
     free_bufs(h);
     (void)hipFree(h->d_addr); (void)hipFree(h->d_ghash); (void)hipFree(h->d_stats); (void)hipFree(h->d_hist);
     (void)hipFree(h->d_red);
+    (void)hipFree(h->d_keys);
     if (h->comm) comm_destroy(h->comm);
+    if (h->sig) sig_api().destroy(h->sig);
     for (uint32_t i = 0; i < bftsim::RING; ++i) {
         if (h->ring[i].c0) (void)hipEventDestroy(h->ring[i].c0);
         if (h->ring[i].c1) (void)hipEventDestroy(h->ring[i].c1);
@@ -637,6 +862,10 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg;
         uint64_t blocks = (n + per_block - 1) / per_block;
         HIPCHECK(h, hipMalloc(&h->d_rcs, blocks * bft::rcs_words(h->seg) * 4));
+        if (h->crypto) {
+            HIPCHECK(h, hipMalloc(&h->d_mlog, n * (uint64_t)h->mlog_cap * bft::MLOG_WORDS * 4));
+            HIPCHECK(h, hipMalloc(&h->d_mlog_n, n * 4));
+        }
         if (h->cfg.backlog_mode == BFTSIM_BACKLOG_REPLAY) {
             h->backlog_bytes = blocks * bft::backlog_words(h->seg) * 4;
             HIPCHECK(h, hipMalloc(&h->d_backlog, h->backlog_bytes));
@@ -704,6 +933,12 @@ static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
     p.hist = h->d_hist;
     p.rcs = h->d_rcs;
     p.backlog = h->d_backlog;
+    if (h->crypto && h->d_mlog) {
+        p.mlog = h->d_mlog;
+        p.mlog_n = h->d_mlog_n;
+        p.mlog_cap = h->mlog_cap;
+        for (int k = 0; k < 4; ++k) p.forged[k] = h->forged[k];
+    }
     if (h->window) {
         p.window_mask = h->window - 1;
         p.rows = h->window;
@@ -770,7 +1005,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     uint32_t per_block = h->seg > 64 ? 1u : 64u / h->seg;      // instances per workgroup
     uint32_t grid = (uint32_t)((n + per_block - 1) / per_block);
     size_t lds = bft::lds_bytes(h->seg, p.need_seed != 0);
-    const bool fast = h->fast && p.fast && h->d_save && !p.need_seed && !h->h_trace && h->seg == 64;
+    const bool fast = h->fast && p.fast && !p.mlog && h->d_save && !p.need_seed && !h->h_trace && h->seg == 64;
     HIPCHECK(h, hipEventRecord(ev.c0, s));
     if (fast) {
         // FAST kernel over every instance, then the full kernel over the ones it handed over
@@ -999,6 +1234,142 @@ int bftsim_stats_allreduce(bftsim_t* h, bftsim_stats* out) {
     if (e != ncclSuccess) return fail(h, BFTSIM_EHIP, std::string("ncclAllReduce: ") + r.err(e));
     HIPCHECK(h, hipMemcpyAsync(out, h->d_red, sizeof(bftsim_stats), hipMemcpyDeviceToHost, s));
     HIPCHECK(h, hipStreamSynchronize(s));
+    return BFTSIM_OK;
+}
+
+int bftsim_set_crypto(bftsim_t* h, const uint8_t* secrets32, const uint8_t* forged, uint32_t log_cap) {
+    if (!h) return BFTSIM_EINVAL;
+    const uint32_t n = h->cfg.n;
+    if (!secrets32) {                                  // off
+        h->crypto = false;
+        free_bufs(h);
+        return BFTSIM_OK;
+    }
+    if (h->window) return fail(h, BFTSIM_EINVAL, "real-crypto mode needs the per-height rows (window 0)");
+    SigApi& a = sig_api();
+    if (!a.ok) return fail(h, BFTSIM_EUNSUPPORTED, a.why);
+    HIPCHECK(h, hipSetDevice(h->device));
+    if (!h->sig && a.create(h->device, &h->sig) != 0) return fail(h, BFTSIM_EHIP, "bftsig_create failed");
+    // the forged key of validator v: keccak(secret_v), a valid key that is not a validator's
+    std::vector<uint8_t> keys((size_t)2 * n * 32);
+    memcpy(keys.data(), secrets32, (size_t)n * 32);
+    for (uint32_t v = 0; v < n; ++v) host_keccak(secrets32 + 32u * v, 32, keys.data() + (size_t)(n + v) * 32);
+    if (!h->d_keys) HIPCHECK(h, hipMalloc(&h->d_keys, (size_t)2 * 256 * 32));
+    HIPCHECK(h, hipMemcpy(h->d_keys, keys.data(), keys.size(), hipMemcpyHostToDevice));
+    // every secret must derive the validator address of its index (the sorted validator set)
+    uint8_t *d_addr = nullptr, *d_ok = nullptr;
+    HIPCHECK(h, hipMalloc(&d_addr, (size_t)n * 20));
+    HIPCHECK(h, hipMalloc(&d_ok, n));
+    int rc = a.secret_to_address(h->sig, h->d_keys, n, nullptr, d_addr, d_ok, nullptr);
+    std::vector<uint8_t> addr((size_t)n * 20), ok(n);
+    hipError_t e = rc == 0 ? hipDeviceSynchronize() : hipSuccess;
+    if (rc == 0 && e == hipSuccess) e = hipMemcpy(addr.data(), d_addr, addr.size(), hipMemcpyDeviceToHost);
+    if (rc == 0 && e == hipSuccess) e = hipMemcpy(ok.data(), d_ok, n, hipMemcpyDeviceToHost);
+    (void)hipFree(d_addr); (void)hipFree(d_ok);
+    if (rc != 0) return fail(h, BFTSIM_EHIP, std::string("bftsig_secret_to_address: ") + a.last_error(h->sig));
+    if (e != hipSuccess) return fail(h, BFTSIM_EHIP, hipGetErrorString(e));
+    for (uint32_t v = 0; v < n; ++v)
+        if (!ok[v] || memcmp(addr.data() + 20u * v, h->addresses.data() + 20u * v, 20) != 0)
+            return fail(h, BFTSIM_EINVAL, "secret " + std::to_string(v) + " does not derive validator address " +
+                                              std::to_string(v));
+    for (int k = 0; k < 4; ++k) h->forged[k] = 0;
+    if (forged)
+        for (uint32_t v = 0; v < n; ++v)
+            if (forged[v]) h->forged[v >> 6] |= 1ull << (v & 63u);
+    h->mlog_cap = log_cap ? log_cap : h->cfg.heights * (4u * n + 8u) + 64u * n;
+    h->crypto = true;
+    free_bufs(h);                                      // the log is allocated by the next prepare
+    return BFTSIM_OK;
+}
+
+int bftsim_crypto_verify(bftsim_t* h, bftsim_crypto_report* out, uint8_t* inst_checksum, uint32_t* inst_messages) {
+    if (!h || !out) return BFTSIM_EINVAL;
+    if (!h->crypto) return fail(h, BFTSIM_EINVAL, "bftsim_set_crypto not called");
+    if (h->last_n == 0 || !h->d_mlog) return fail(h, BFTSIM_EINVAL, "nothing launched");
+    if (int rc = sync_all(h)) return rc;
+    SigApi& sa = sig_api();
+    const uint64_t n = h->last_n;
+    hipStream_t s = h->last_stream;
+    std::vector<uint32_t> cnt(n);
+    HIPCHECK(h, hipMemcpy(cnt.data(), h->d_mlog_n, n * 4, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> off(n);
+    uint64_t M = 0, over = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        off[i] = M;
+        if (cnt[i] > h->mlog_cap) ++over;
+        M += cnt[i] < h->mlog_cap ? cnt[i] : h->mlog_cap;
+        if (inst_messages) inst_messages[i] = cnt[i];
+    }
+    memset(out, 0, sizeof *out);
+    out->log_overflows = over;
+    if (over) return fail(h, BFTSIM_EINVAL, "broadcast log overflow: raise log_cap (bftsim_set_crypto)");
+    // device arrays of the pass (one allocation)
+    const uint64_t Mx = M ? M : 1;
+    const uint64_t sz_msg = 8 + 32 + 4 + 4 + 32 + 65 + 20 + 1, sz_cm = 32 + 32 + 4 + 65 + 1 + 20 + 4;
+    uint8_t* pool = nullptr;
+    const uint64_t bytes = n * 8 + Mx * (sz_msg + sz_cm) + n * 32 + 64 + 256;
+    HIPCHECK(h, hipMalloc(&pool, bytes));
+    uint8_t* q = pool;
+    auto take = [&](uint64_t b) { uint8_t* r = q; q += (b + 15) & ~15ull; return r; };
+    bft::CryptoArgs a{};
+    a.mlog = h->d_mlog; a.mlog_n = h->d_mlog_n; a.cap = h->mlog_cap; a.n_val = h->cfg.n;
+    for (int k = 0; k < 4; ++k) a.forged[k] = h->forged[k];
+    uint64_t* d_off = (uint64_t*)take(n * 8); a.moff = d_off;
+    a.mref = (uint64_t*)take(Mx * 8); a.raw = take(Mx * 32); a.key = (uint32_t*)take(Mx * 4);
+    a.msg_k = (uint32_t*)take(Mx * 4); a.sign_dig = take(Mx * 32); a.sigs = take(Mx * 65);
+    a.rec_addr = take(Mx * 20); a.rec_ok = take(Mx);
+    a.seal_dig = take(Mx * 32); a.seal_raw = take(Mx * 32); a.seal_key = (uint32_t*)take(Mx * 4);
+    a.seals = take(Mx * 65); a.seal_ok = take(Mx); uint8_t* seal_addr = take(Mx * 20);
+    uint8_t* sig_ok = take(Mx);
+    a.ncm = (uint32_t*)take(4); a.inst_ck = (uint32_t*)take(n * 32); a.counts = (unsigned long long*)take(64);
+    int rc = BFTSIM_OK;
+    hipError_t e = hipMemcpyAsync(d_off, off.data(), n * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemsetAsync(a.ncm, 0, 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(a.inst_ck, 0, n * 32, s);
+    if (e == hipSuccess) e = hipMemsetAsync(a.counts, 0, 64, s);
+    bft::Params p = make_params(h, h->last_first, n);
+    uint32_t ncm = 0;
+    if (e == hipSuccess && M) {
+        hipLaunchKernelGGL(bft::bft_crypto_prep_kernel, dim3((uint32_t)n), dim3(64), 0, s, p, a);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(&ncm, a.ncm, 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        // commit seals first: they are part of the Commit's sign payload
+        if (e == hipSuccess && ncm && sa.sign(h->sig, h->d_keys, a.seal_key, a.seal_dig, ncm, a.seals, sig_ok, s) != 0)
+            rc = fail(h, BFTSIM_EHIP, std::string("bftsig_sign (seals): ") + sa.last_error(h->sig));
+        const uint32_t g = (uint32_t)((M + 63) / 64);
+        if (e == hipSuccess && rc == 0) {
+            hipLaunchKernelGGL(bft::bft_crypto_digest_kernel, dim3(g), dim3(64), 0, s, p, a, M);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess && rc == 0 && sa.sign(h->sig, h->d_keys, a.key, a.sign_dig, M, a.sigs, sig_ok, s) != 0)
+            rc = fail(h, BFTSIM_EHIP, std::string("bftsig_sign: ") + sa.last_error(h->sig));
+        // the receivers: recover every message's signer, and every seal (verify_commit)
+        if (e == hipSuccess && rc == 0 && sa.recover(h->sig, a.sign_dig, a.sigs, M, nullptr, a.rec_addr, a.rec_ok, s) != 0)
+            rc = fail(h, BFTSIM_EHIP, std::string("bftsig_recover: ") + sa.last_error(h->sig));
+        if (e == hipSuccess && rc == 0 && ncm &&
+            sa.recover(h->sig, a.seal_raw, a.seals, ncm, nullptr, seal_addr, a.seal_ok, s) != 0)
+            rc = fail(h, BFTSIM_EHIP, std::string("bftsig_recover (seals): ") + sa.last_error(h->sig));
+        if (e == hipSuccess && rc == 0) {
+            hipLaunchKernelGGL(bft::bft_crypto_check_kernel, dim3(g), dim3(64), 0, s, p, a, M);
+            e = hipGetLastError();
+        }
+    }
+    unsigned long long c[8] = {0};
+    if (e == hipSuccess && rc == 0) e = hipMemcpyAsync(c, a.counts, 64, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && rc == 0 && inst_checksum) e = hipMemcpyAsync(inst_checksum, a.inst_ck, n * 32, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(pool);
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(h, BFTSIM_EHIP, std::string("bftsim_crypto_verify: ") + hipGetErrorString(e));
+    out->messages = c[0];
+    out->seals = c[1];
+    out->forged = c[2];
+    out->recovered_as_sender = c[3];
+    out->mismatches = c[4];
+    out->seal_errors = c[5];
+    out->signatures = c[0] + c[1];
+    out->recoveries = c[0] + c[1];
     return BFTSIM_OK;
 }
 

@@ -159,6 +159,37 @@ int bftsim_set_window(bftsim_t *h, uint32_t window);
 int bftsim_fetch_summary(bftsim_t *h, uint64_t *committed_height, uint32_t *flags, uint32_t *ticks,
                          uint64_t *views, uint8_t *tip_hash);
 
+/* real-crypto mode (SPEC.md §11). Every consensus message the simulation
+ * broadcasts is logged; bftsim_crypto_verify then does, batched on the GPU (libbftsig):
+ *   - sign it with its sender's key (finalize_message, core.rs:425-429), the Commit seal first
+ *     (encrypt_commit_bytes, types/votes.rs:94-101);
+ *   - recover its signer and check membership (GossipMessage::address, protocol/mod.rs:103-116;
+ *     handle_message, core.rs:314-322), and recover every seal (verify_commit, commit.rs:94-100).
+ * A `forged` validator signs with a key that is not its own (keccak of its secret): every receiver
+ * drops its consensus messages, which the simulation applies when they are sent. The verify pass
+ * proves that assumption message by message (`mismatches` must be 0). Each message is recovered once,
+ * as every receiver gets the same bytes (the reference recovers it at each receiver).
+ * secrets32: host, n x 32 bytes in the sorted validator order; each must derive the address of its
+ * index (else BFTSIM_EINVAL). forged: host, n bytes (NULL = none). log_cap: messages per instance
+ * (0 = heights * (4n + 8) + 64n). NULL secrets turn the mode off. Takes effect at the next
+ * bftsim_prepare. Needs libbftsig.so next to libbftsim.so; window 0; N = 64 runs the full kernel. */
+typedef struct bftsim_crypto_report {
+    uint64_t messages;             /* consensus messages broadcast (each signed once) */
+    uint64_t seals;                /* Commit seals (signed, then recovered) */
+    uint64_t forged;               /* messages of forged senders */
+    uint64_t recovered_as_sender;  /* messages whose signature recovers their sender */
+    uint64_t mismatches;           /* recovered validity != the simulated delivery: 0 */
+    uint64_t seal_errors;          /* seals that do not recover */
+    uint64_t signatures;           /* ECDSA signs performed: messages + seals */
+    uint64_t recoveries;           /* ECDSA recoveries performed: messages + seals */
+    uint64_t log_overflows;        /* instances whose log exceeded log_cap (then the call fails) */
+} bftsim_crypto_report;
+int bftsim_set_crypto(bftsim_t *h, const uint8_t *secrets32, const uint8_t *forged, uint32_t log_cap);
+/* after a launch: the sign / recover pass of its messages; inst_checksum (host, n x 32, nullable) =
+ * per instance the XOR over its messages of keccak256(signature || seal or 65 zero bytes);
+ * inst_messages (host, n, nullable) = messages per instance */
+int bftsim_crypto_verify(bftsim_t *h, bftsim_crypto_report *out, uint8_t *inst_checksum, uint32_t *inst_messages);
+
 /* ValidatorSet / block helpers on the host (validator.rs, types/block.rs) */
 uint32_t bftsim_two_thirds_majority(uint32_t n);                    /* validator.rs:149-154 */
 uint32_t bftsim_seed_from_hash(const uint8_t hash[32], uint32_t n); /* validator.rs:39-48 (BE) */

@@ -386,6 +386,10 @@ typedef struct {
     int64_t tick;
     uint32_t flags;
     int frozen;
+    /* real-crypto mode (SPEC.md §11): the broadcast log of this instance and the forged senders */
+    const uint64_t *forged;
+    uint32_t *mlog;        /* [mlog_cap][8] */
+    uint32_t mlog_cap, mlog_n;
 } world;
 
 static canon_entry *canon_at(world *w, uint32_t x) { return &w->canon[x]; }
@@ -901,6 +905,33 @@ static int pending_local(world *w) {
     return 0;
 }
 
+/* SPEC.md §11: at the start of a phase the consensus messages of every outbox are broadcast (signed,
+ * core.rs:425-429) in (sender, kind) order; a forged sender's messages are dropped by every receiver
+ * (handle_message, core.rs:314-322), so they leave the outbox */
+static uint64_t blk_pack(blk b) {
+    if (!b.valid) return 0;
+    return (uint64_t)(b.h & 0xffffffu) | ((uint64_t)(b.prop & 0x1ffu) << 24) | ((uint64_t)(b.var & 1u) << 33) |
+           (1ull << 34) | ((uint64_t)b.T << 35);
+}
+static void mlog_put(world *w, uint32_t phase, uint32_t sender, uint32_t code, uint32_t h, uint32_t r, uint64_t b,
+                     uint32_t fl) {
+    uint32_t idx = w->mlog_n++;
+    if (idx >= w->mlog_cap) return;
+    uint32_t *e = w->mlog + (size_t)idx * 8;
+    e[0] = (uint32_t)w->tick; e[1] = phase | (code << 8) | (sender << 16); e[2] = h; e[3] = r;
+    e[4] = (uint32_t)b; e[5] = (uint32_t)(b >> 32); e[6] = fl; e[7] = 0;
+}
+static void crypto_log(world *w, uint32_t sender, outbox *o, uint32_t phase) {
+    int forged = (int)((w->forged[sender >> 6] >> (sender & 63)) & 1);
+    uint32_t ff = forged ? 1u : 0u;                        /* MLOG_FORGED, WILD 2, EQUIV 4, OLD 8 */
+    if (o->has_pp) mlog_put(w, phase, sender, 1, o->pp_h, o->pp_r, blk_pack(o->pp_blk), ff | (o->pp_equiv ? 4u : 0u));
+    if (o->has_pr) mlog_put(w, phase, sender, 2, o->pr_h, o->pr_r, blk_pack(o->pr_d), ff | (o->pr_wild ? 2u : 0u));
+    if (o->has_ocm) mlog_put(w, phase, sender, 3, o->ocm_h, o->ocm_r, blk_pack(o->ocm_d), ff | 8u | (o->ocm_wild ? 2u : 0u));
+    if (o->has_cm) mlog_put(w, phase, sender, 3, o->cm_h, o->cm_r, blk_pack(o->cm_d), ff | (o->cm_wild ? 2u : 0u));
+    if (o->has_rc) mlog_put(w, phase, sender, 4, o->rc_h, o->rc_r, 0, ff);
+    if (forged) o->has_pp = o->has_pr = o->has_ocm = o->has_cm = o->has_rc = 0;
+}
+
 static void run_tick(world *w) {
     uint32_t n = w->n;
     /* T-step (SPEC.md §2) */
@@ -938,6 +969,7 @@ static void run_tick(world *w) {
             val *v = &w->v[i];
             v->cur = v->next;
             memset(&v->next, 0, sizeof(outbox));
+            if (w->mlog && v->running) crypto_log(w, i, &v->cur, p);
             if (capped && !outbox_empty(&v->cur)) w->flags |= ORC_FLAG_PHASE_CAP;
         }
         if (capped) break;
@@ -986,6 +1018,24 @@ static int run_instance(const orc_config *cfg, uint32_t inst, const orc_result *
     return run_instance_ex(cfg, inst, res, idx, trace, max_rec, NULL, NULL);
 }
 
+/* real-crypto mode context of the instance being run (orc_run_crypto; single-threaded) */
+static const uint64_t *g_forged;
+static uint32_t *g_mlog, *g_mlog_n;
+static uint32_t g_mlog_cap;
+
+int orc_run_crypto(const orc_config *cfg, uint64_t first_instance, uint64_t n_instances, const orc_result *res,
+                   const uint64_t forged[4], uint32_t *mlog, uint32_t *mlog_n, uint32_t mlog_cap) {
+    g_forged = forged;
+    g_mlog_cap = mlog_cap;
+    for (uint64_t i = 0; i < n_instances; ++i) {
+        g_mlog = mlog + (size_t)i * mlog_cap * 8;
+        g_mlog_n = mlog_n + i;
+        run_instance(cfg, (uint32_t)(first_instance + i), res, i, NULL, 0);
+    }
+    g_forged = NULL; g_mlog = NULL; g_mlog_n = NULL;
+    return 0;
+}
+
 static int run_instance_ex(const orc_config *cfg, uint32_t inst, const orc_result *res, uint64_t idx,
                            uint64_t *trace, uint32_t max_rec, orc_stream *st, uint64_t *hist) {
     runner *R = (runner *)calloc(1, sizeof(runner));
@@ -997,6 +1047,7 @@ static int run_instance_ex(const orc_config *cfg, uint32_t inst, const orc_resul
     w->n = n;
     w->q = orc_two_thirds_majority(n);
     w->v = (val *)calloc(n, sizeof(val));
+    if (g_mlog) { w->forged = g_forged; w->mlog = g_mlog; w->mlog_cap = g_mlog_cap; w->mlog_n = 0; }
     bl_entry *bl_all = cfg->backlog_mode ? (bl_entry *)calloc((size_t)n * n, sizeof(bl_entry)) : NULL;
     if (bl_all)
         for (uint32_t i = 0; i < n; ++i) w->v[i].bl = bl_all + (size_t)i * n;
@@ -1065,6 +1116,7 @@ static int run_instance_ex(const orc_config *cfg, uint32_t inst, const orc_resul
     }
     if (st) stream_summary(cfg, w, done_tick, st, idx, hist);
     free(bl_all);
+    if (w->mlog) *g_mlog_n = w->mlog_n;
     free(w->v);
     free(w->canon);
     free(R);

@@ -87,6 +87,12 @@ int orc_run(const orc_config *cfg, uint64_t first_instance, uint64_t n_instances
 int orc_run_threads(const orc_config *cfg, uint64_t first_instance, uint64_t n_instances,
                     const orc_result *res, int threads, double *seconds);
 
+/* real-crypto mode (SPEC.md §11), single-threaded: as orc_run, and every consensus message broadcast is
+ * logged per instance into mlog[i * mlog_cap * 8 ..] (8 words each, the layout of the GPU log) with its
+ * count in mlog_n[i]; the messages of `forged` senders are dropped by every receiver */
+int orc_run_crypto(const orc_config *cfg, uint64_t first_instance, uint64_t n_instances, const orc_result *res,
+                   const uint64_t forged[4], uint32_t *mlog, uint32_t *mlog_n, uint32_t mlog_cap);
+
 /* number of instances whose committed header chain does not re-hash to the reported hashes */
 uint64_t orc_verify_chains(const orc_config *cfg, uint64_t first, uint64_t n, const orc_result *res,
                            int threads);

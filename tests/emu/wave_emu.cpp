@@ -271,6 +271,14 @@ extern "C" int emu_run_stream(const bftsim_config* cfg, uint64_t first, uint64_t
     return 0;
 }
 
+// real-crypto mode for the next emu_run (SPEC.md §11): forged senders + the broadcast log
+static const uint64_t* g_forged = nullptr;
+static uint32_t *g_mlog = nullptr, *g_mlog_n = nullptr;
+static uint32_t g_mlog_cap = 0;
+extern "C" void emu_set_crypto(const uint64_t* forged, uint32_t* mlog, uint32_t* mlog_n, uint32_t cap) {
+    g_forged = forged; g_mlog = mlog; g_mlog_n = mlog_n; g_mlog_cap = cap;
+}
+
 extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bftsim_result* out,
                        uint64_t* trace, uint32_t trace_ticks, uint64_t* hist) {
     if (cfg->n < 1 || cfg->n > 256) return -4;
@@ -281,6 +289,11 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
     uint32_t hcap = cfg->heights + 64;
     bft::Params P = bft::params_from_config(*cfg, seg, hcap, gseed, first, n);
     if (getenv("BFT_EMU_SLOW")) P.fast = 0;
+    if (g_mlog) {
+        P.mlog = g_mlog; P.mlog_n = g_mlog_n; P.mlog_cap = g_mlog_cap;
+        for (int k = 0; k < 4; ++k) P.forged[k] = g_forged[k];
+        g_mlog = nullptr;                                  // one run
+    }
     std::vector<uint32_t> ch(n), flags(n), ticks(n);
     std::vector<uint64_t> views(n);
     std::vector<uint32_t> rec(n * hcap * 4, 0);
@@ -307,7 +320,7 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
     // as libbftsim: N = 64 runs the FAST kernel, then the full kernel resumes the instances it handed
     // over (BFT_EMU_FAST=0: the full kernel alone)
     const char* ef = getenv("BFT_EMU_FAST");
-    const bool fast = seg == 64 && cfg->n == 64 && P.fast && !P.need_seed && !trace && !(ef && strcmp(ef, "0") == 0);
+    const bool fast = seg == 64 && cfg->n == 64 && P.fast && !P.mlog && !P.need_seed && !trace && !(ef && strcmp(ef, "0") == 0);
     std::vector<uint32_t> resume, save;
     if (fast) {
         resume.assign(n, 0);

@@ -62,6 +62,21 @@ def run(cfg, first, n_inst, trace_ticks=0):
     return arrs
 
 
+def run_crypto(cfg, first, n_inst, forged=(), cap=4096):
+    """The kernel body in real-crypto mode (SPEC.md §11): results + the per-instance broadcast log."""
+    fm = np.zeros(4, np.uint64)
+    for v in forged:
+        fm[v >> 6] |= np.uint64(1) << np.uint64(v & 63)
+    mlog = np.zeros((n_inst, cap, 8), np.uint32)
+    mlog_n = np.zeros(n_inst, np.uint32)
+    L = lib()
+    L.emu_set_crypto.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32]
+    L.emu_set_crypto(fm.ctypes.data, mlog.ctypes.data, mlog_n.ctypes.data, cap)
+    out = run(cfg, first, n_inst)
+    out["mlog"], out["mlog_n"] = mlog, mlog_n
+    return out
+
+
 def run_stream(cfg, first, n_inst, window=128):
     """The windowed kernel body (ring of `window` rows, in-kernel hashes): per-instance outputs,
     tip hashes and the two histograms."""

@@ -115,6 +115,30 @@ def run(cfg: BftConfig, first: int, n_inst: int, threads: int = 1):
     return arrs
 
 
+def run_crypto(cfg: BftConfig, first: int, n_inst: int, forged=(), cap: int = 4096):
+    """orc_run_crypto (SPEC.md §11): results + the per-instance broadcast log [n][cap][8] and counts."""
+    c, keep = to_orc(cfg)
+    r, arrs = alloc_result(n_inst, cfg.heights)
+    fm = (ctypes.c_uint64 * 4)()
+    for v in forged:
+        fm[v >> 6] |= 1 << (v & 63)
+    mlog = np.zeros((n_inst, cap, 8), np.uint32)
+    mlog_n = np.zeros(n_inst, np.uint32)
+    L = lib()
+    L.orc_run_crypto.argtypes = [ctypes.POINTER(OrcConfig), ctypes.c_uint64, ctypes.c_uint64,
+                                 ctypes.POINTER(OrcResult), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_uint32]
+    L.orc_run_crypto(ctypes.byref(c), first, n_inst, ctypes.byref(r), ctypes.cast(fm, ctypes.c_void_p),
+                     mlog.ctypes.data, mlog_n.ctypes.data, cap)
+    del keep
+    H = cfg.heights
+    for k in ("round", "proposer", "variant", "time_tick"):
+        arrs[k] = arrs[k].reshape(n_inst, H)
+    arrs["block_hash"] = arrs["block_hash"].reshape(n_inst, H, 32)
+    arrs["mlog"], arrs["mlog_n"] = mlog, mlog_n
+    return arrs
+
+
 def verify_chains(cfg: BftConfig, first: int, res: dict, threads: int = 8) -> int:
     """Re-hash every committed header chain of a result dict (any producer); returns the number
     of instances that do not verify."""

@@ -1,0 +1,86 @@
+"""GPU: real-crypto mode (include/bftsim.h bftsim_set_crypto / bftsim_crypto_verify, SPEC.md §11).
+The simulated run equals the oracle's (forged senders' messages dropped at every receiver); the batched
+sign / recover pass recovers every honest message to its sender and no forged one to any validator;
+the per-instance signature checksums equal the CPU reference's (RFC 6979 signatures of the msgpack
+sign payloads, tests/crypto_ref.py), with the reference's own c1..c5 keys."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import crypto_ref as C
+import oracle_lib as O
+from bftsim.configs import BftConfig, cfg1, cfg3
+from parity_util import assert_same
+
+pytestmark = pytest.mark.gpu
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "sig_vectors.json")))
+
+
+def _core(r):
+    return {k: v for k, v in r.items() if k not in ("mlog", "mlog_n", "seconds", "round_hist", "latency_hist")}
+
+
+def _run(cfg, secrets, first, n, forged=()):
+    from bftsim.runtime import Simulator
+    sim = Simulator(cfg)
+    try:
+        sim.set_crypto(secrets, forged)
+        got = sim.run(first, n)
+        rep = sim.crypto_verify()
+    finally:
+        sim.close()
+    return got, rep
+
+
+def _keyed(cfg, seed):
+    from bftsim.crypto import synthetic_secrets, keyed_config, gpu_addresses
+    sec = synthetic_secrets(cfg.n, seed)
+    return keyed_config(cfg, sec, gpu_addresses(sec))
+
+
+def test_reference_keys_cfg1():
+    keys = {bytes.fromhex(k["address"]): bytes.fromhex(k["secret"]) for k in GOLD["reference_keys"]}
+    cfg = cfg1(True, heights=10)
+    secrets = [keys[a] for a in cfg.addresses]           # c1..c5 of examples/*.toml, validator order
+    got, rep = _run(cfg, secrets, 0, 1)
+    ref = O.run_crypto(cfg, 0, 1)
+    assert_same(_core(ref), _core(got), "cfg1 crypto")
+    assert rep["messages"] == int(ref["mlog_n"][0]) > 0
+    assert rep["mismatches"] == 0 and rep["seal_errors"] == 0 and rep["forged"] == 0
+    assert rep["recovered_as_sender"] == rep["messages"]
+    assert rep["seals"] == int(((ref["mlog"][0, : rep["messages"], 1] >> 8) & 0xff == 3).sum())
+    assert np.array_equal(rep["checksum"], C.instance_checksums(cfg, 0, ref, secrets))
+
+
+def test_forged_sender_dropped():
+    cfg, secrets = _keyed(BftConfig(n=4, heights=6, seed=21), 7)
+    got, rep = _run(cfg, secrets, 3, 1, forged=(2,))
+    ref = O.run_crypto(cfg, 3, 1, forged=(2,))
+    assert_same(_core(ref), _core(got), "forged 2")
+    assert rep["messages"] == int(ref["mlog_n"][0])
+    assert rep["forged"] > 0 and rep["mismatches"] == 0 and rep["seal_errors"] == 0
+    assert rep["recovered_as_sender"] == rep["messages"] - rep["forged"]
+    assert np.array_equal(rep["checksum"], C.instance_checksums(cfg, 3, ref, secrets, forged=(2,)))
+
+
+def test_cfg3_keys_and_forgers():
+    cfg, secrets = _keyed(cfg3(heights=4), 3)
+    got, rep = _run(cfg, secrets, 0, 4, forged=(0, 5))
+    ref = O.run_crypto(cfg, 0, 4, forged=(0, 5))
+    assert_same(_core(ref), _core(got), "cfg3 crypto")
+    assert np.array_equal(rep["inst_messages"], ref["mlog_n"])
+    assert rep["mismatches"] == 0 and rep["seal_errors"] == 0 and rep["forged"] > 0
+    assert rep["recovered_as_sender"] == rep["messages"] - rep["forged"]
+
+
+def test_wrong_secret_rejected():
+    from bftsim.runtime import Simulator, BftsimError
+    cfg, secrets = _keyed(BftConfig(n=4, heights=3), 1)
+    sim = Simulator(cfg)
+    try:
+        with pytest.raises(BftsimError):
+            sim.set_crypto(secrets[::-1])                   # keys not in the validator order
+    finally:
+        sim.close()
