@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <dlfcn.h>
+#include <unistd.h>
 #include <rccl/rccl.h>                 // types only: librccl is opened at bftsim_comm_init (dlopen)
 
 #include <mutex>
@@ -703,6 +704,20 @@ Rccl& rccl() {
     });
     return r;
 }
+// RCCL prints its version banner on stdout at initialisation; the callers' stdout carries results
+// (bench.py's one JSON line), so the banner goes to stderr
+struct StdoutToStderr {
+    int saved;
+    StdoutToStderr() {
+        fflush(stdout);
+        saved = dup(1);
+        if (saved >= 0) dup2(2, 1);
+    }
+    ~StdoutToStderr() {
+        fflush(stdout);
+        if (saved >= 0) { dup2(saved, 1); close(saved); }
+    }
+};
 void comm_destroy(ncclComm_t c) {
     if (rccl().ok) (void)rccl().destroy(c);
 }
@@ -1193,6 +1208,7 @@ int bftsim_comm_unique_id(uint8_t out[128]) {
     Rccl& r = rccl();
     if (!r.ok) return BFTSIM_EUNSUPPORTED;
     ncclUniqueId id;
+    StdoutToStderr quiet;
     if (r.get_id(&id) != ncclSuccess) return BFTSIM_EHIP;
     memcpy(out, &id, 128);
     return BFTSIM_OK;
@@ -1207,7 +1223,11 @@ int bftsim_comm_init(bftsim_t* h, int world_size, int rank, const uint8_t unique
     if (h->comm) { comm_destroy(h->comm); h->comm = nullptr; }
     ncclUniqueId id;
     memcpy(&id, unique_id, 128);
-    ncclResult_t e = r.init_rank(&h->comm, world_size, id, rank);
+    ncclResult_t e;
+    {
+        StdoutToStderr quiet;
+        e = r.init_rank(&h->comm, world_size, id, rank);
+    }
     if (e != ncclSuccess) { h->comm = nullptr; return fail(h, BFTSIM_EHIP, std::string("ncclCommInitRank: ") + r.err(e)); }
     if (!h->d_red) HIPCHECK(h, hipMalloc(&h->d_red, sizeof(bftsim_stats)));
     return BFTSIM_OK;
@@ -1230,7 +1250,11 @@ int bftsim_stats_allreduce(bftsim_t* h, bftsim_stats* out) {
     HIPCHECK(h, hipMemcpyAsync(h->d_red, h->d_stats, 11 * 8, hipMemcpyDeviceToDevice, s));
     HIPCHECK(h, hipMemcpyAsync(h->d_red + 11, h->d_hist, bft::HIST_BINS * 8, hipMemcpyDeviceToDevice, s));
     Rccl& r = rccl();
-    ncclResult_t e = r.all_reduce(h->d_red, h->d_red, sizeof(bftsim_stats) / 8, ncclUint64, ncclSum, h->comm, s);
+    ncclResult_t e;
+    {
+        StdoutToStderr quiet;
+        e = r.all_reduce(h->d_red, h->d_red, sizeof(bftsim_stats) / 8, ncclUint64, ncclSum, h->comm, s);
+    }
     if (e != ncclSuccess) return fail(h, BFTSIM_EHIP, std::string("ncclAllReduce: ") + r.err(e));
     HIPCHECK(h, hipMemcpyAsync(out, h->d_red, sizeof(bftsim_stats), hipMemcpyDeviceToHost, s));
     HIPCHECK(h, hipStreamSynchronize(s));

@@ -22,11 +22,11 @@ def _core(r):
     return {k: v for k, v in r.items() if k not in ("mlog", "mlog_n", "seconds", "round_hist", "latency_hist")}
 
 
-def _run(cfg, secrets, first, n, forged=()):
+def _run(cfg, secrets, first, n, forged=(), log_cap=0):
     from bftsim.runtime import Simulator
     sim = Simulator(cfg)
     try:
-        sim.set_crypto(secrets, forged)
+        sim.set_crypto(secrets, forged, log_cap)
         got = sim.run(first, n)
         rep = sim.crypto_verify()
     finally:
@@ -67,8 +67,8 @@ def test_forged_sender_dropped():
 
 def test_cfg3_keys_and_forgers():
     cfg, secrets = _keyed(cfg3(heights=4), 3)
-    got, rep = _run(cfg, secrets, 0, 4, forged=(0, 5))
-    ref = O.run_crypto(cfg, 0, 4, forged=(0, 5))
+    got, rep = _run(cfg, secrets, 0, 4, forged=(0, 5), log_cap=16384)   # round-change storms: 8k+ messages
+    ref = O.run_crypto(cfg, 0, 4, forged=(0, 5), cap=16384)
     assert_same(_core(ref), _core(got), "cfg3 crypto")
     assert np.array_equal(rep["inst_messages"], ref["mlog_n"])
     assert rep["mismatches"] == 0 and rep["seal_errors"] == 0 and rep["forged"] > 0
