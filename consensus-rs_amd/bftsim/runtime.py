@@ -41,6 +41,9 @@ def lib():
         L.bftsim_stats_allreduce.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.CStats)]
         L.bftsim_comm_unique_id.argtypes = [ctypes.c_void_p]
         L.bftsim_set_crypto.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32]
+        L.bftsim_ledger_slot_bytes.argtypes = [ctypes.c_uint32]
+        L.bftsim_ledger_slot_bytes.restype = ctypes.c_uint64
+        L.bftsim_export_ledger.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
         L.bftsim_crypto_verify.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.CCryptoReport), ctypes.c_void_p,
                                            ctypes.c_void_p]
         L.bftsim_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
@@ -234,6 +237,27 @@ class Simulator:
                "bftsim_crypto_verify")
         out = {k: getattr(rep, k) for k, _ in _abi.CCryptoReport._fields_}
         out["checksum"], out["inst_messages"] = ck, cnt
+        return out
+
+    def export_ledger(self):
+        """The ledger Headers with votes of the last launch (after crypto_verify): per instance a list of
+        header byte strings, height 1..committed (include/bftsim.h bftsim_export_ledger)."""
+        n, H = self.n_prepared, self.cfg.heights
+        slot = lib().bftsim_ledger_slot_bytes(self.cfg.n)
+        buf = np.zeros(n * H * slot, np.uint8)
+        lens = np.zeros(n * H, np.uint32)
+        _check(self.h, lib().bftsim_export_ledger(self.h, buf.ctypes.data, slot, lens.ctypes.data),
+               "bftsim_export_ledger")
+        out = []
+        for i in range(n):
+            row = []
+            for x in range(H):
+                k = int(lens[i * H + x])
+                if k == 0:
+                    break
+                o = (i * H + x) * slot
+                row.append(bytes(buf[o:o + k]))
+            out.append(row)
         return out
 
     @staticmethod

@@ -74,6 +74,8 @@ struct Params {
     uint32_t mlog_cap;
     uint32_t pad4;
     uint64_t forged[4];               // validators signing with a key that is not theirs
+    uint32_t* vsnap;                  // [n_inst][seg][8] each lane's commit set at its last Core commit
+    uint32_t* votes;                  // [n_inst][rows][8] the canonical committer's commit set per height
 };
 // one logged broadcast: {tick, phase | code << 8 | sender << 16, height, round, block id lo, hi,
 // flags (MLOG_*), 0}; code = MessageType 1..4 (Preprepare .. RoundChange)

@@ -326,6 +326,13 @@ struct Sim {
         commit_x = x;
         commit_blk = b;
         commit_round = r;
+        if (P.vsnap) {                                      // real-crypto mode: the votes of this commit
+            uint32_t* vs = P.vsnap + ((uint64_t)inst_local * S + me) * 8u;   // (core.rs:402-413)
+            for (uint32_t k = 0; k < 8u; ++k) vs[k] = k < 2u * NW ? (uint32_t)(comm.w[k >> 1] >> (32u * (k & 1u))) : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // read by the recording lane
+#endif
+        }
         uint32_t sd = 0;
         if (NEED_SEED) {
             uint32_t prev[8], out[8];
@@ -746,8 +753,16 @@ struct Sim {
     // record a new canonical height (segment leader; global stores for the outputs). `ctick` is the
     // tick of the previous canonical record; returns the instance-rounds to add (0 beyond H).
     BFT_FN uint32_t record_canon(uint32_t x, uint64_t b, uint32_t round, uint32_t seed, const uint32_t* hs,
-                                 uint32_t ctick) {
+                                 uint32_t ctick, uint32_t committer) {
         uint32_t add = 0;
+        if (P.votes) {                                      // the committer's commit set → the block's votes
+#if defined(__HIP_DEVICE_COMPILE__)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#endif
+            const uint32_t* vs = P.vsnap + ((uint64_t)inst_local * S + committer) * 8u;
+            uint32_t* vo = P.votes + row_of(x) * 8u;
+            for (uint32_t k = 0; k < 8u; ++k) vo[k] = vs[k];
+        }
         if (x <= P.heights) {
             uint32_t lat = (uint32_t)tick - ctick;
             wv.lds_add(hist_slot(round < 64u ? round : 64u), 1u);
@@ -787,7 +802,8 @@ struct Sim {
                 bool fr = badm.any();
                 if (!x0_known && x0 < P.hcap && (!fr || badm.ctz() > lead)) {
                     if (lane == lead)
-                        record_canon(x0, b0, r0, s0, (const uint32_t*)(lds + LDS_CHASH_OFF + lead * 32), canon_tick);
+                        record_canon(x0, b0, r0, s0, (const uint32_t*)(lds + LDS_CHASH_OFF + lead * 32), canon_tick,
+                                     lead - seg_base);
                     views_acc += x0 <= P.heights ? (uint64_t)r0 + 1u : 0u;
                     canon_h = x0; canon_tip = b0; canon_tip_seed = s0; canon_tick = (uint32_t)tick;
                 }
@@ -828,7 +844,8 @@ struct Sim {
             uint32_t tseed = canon_tip_seed, ctick = canon_tick;
             uint64_t va = views_acc;
             if (!x0_known && x0 < P.hcap && (!fr || badm.ctz() > lead)) {
-                va += record_canon(x0, b0, cl[3], cl[4], (const uint32_t*)(lds + LDS_CHASH_OFF + lead * 32), ctick);
+                va += record_canon(x0, b0, cl[3], cl[4], (const uint32_t*)(lds + LDS_CHASH_OFF + lead * 32), ctick,
+                                   lead - seg_base);
                 ch = x0; tip = b0; tseed = cl[4]; ctick = (uint32_t)tick;
             }
             if (x0 >= P.hcap) fr = true;
@@ -861,7 +878,8 @@ struct Sim {
                     if (!blk_eq(cb, b)) { fr = true; break; }
                 } else {
                     // x == ch + 1: heights are recorded contiguously
-                    va += record_canon(x, b, cj[3], cj[4], (const uint32_t*)(lds + LDS_CHASH_OFF + j * 32), ctick);
+                    va += record_canon(x, b, cj[3], cj[4], (const uint32_t*)(lds + LDS_CHASH_OFF + j * 32), ctick,
+                                       j - seg_base);
                     ch = x; tip = b; tseed = cj[4]; ctick = (uint32_t)tick;
                 }
             }

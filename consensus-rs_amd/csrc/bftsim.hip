@@ -543,6 +543,76 @@ __global__ __launch_bounds__(64) void bft_crypto_check_kernel(Params p, CryptoAr
     if (seal_err) atomicAdd(a.counts + 5, 1ull);
 }
 
+
+// pass 4 (lane per message): the signatures of the canonical committer's commit set (the block's votes,
+// core.rs:402-413 → backend.rs:163-174): each Commit of height x, the committed round, the committed
+// block (or a wildcard), from a sender in that set
+__global__ __launch_bounds__(64) void bft_crypto_votes_kernel(Params p, CryptoArgs a, uint64_t M, uint8_t* vsig,
+                                                              uint8_t* vhas) {
+    const uint64_t m = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (m >= M) return;
+    const uint64_t ref = a.mref[m];
+    const uint32_t il = (uint32_t)(ref / a.cap);
+    const uint32_t* e = a.mlog + ref * MLOG_WORDS;
+    const uint32_t code = (e[1] >> 8) & 0xffu, sender = e[1] >> 16, x = e[2], r = e[3];
+    if (code != MT_COMMIT || (e[6] & MLOG_OLD) || x == 0 || x > p.committed_height[il]) return;
+    const uint32_t* row = p.rec + ((uint64_t)il * p.rows + x) * 4;
+    const uint64_t b = (uint64_t)e[4] | ((uint64_t)e[5] << 32);
+    if (row[0] != r) return;
+    if (!(e[6] & MLOG_WILD) && ((row[1] & 0xffffu) != blk_prop(b) || ((row[1] >> 16) & 1u) != blk_var(b))) return;
+    const uint32_t* vo = p.votes + ((uint64_t)il * p.rows + x) * 8;
+    if (!((vo[sender >> 5] >> (sender & 31u)) & 1u)) return;
+    const uint64_t slot = ((uint64_t)il * p.heights + (x - 1)) * p.n + sender;
+    for (int i = 0; i < 65; ++i) vsig[slot * 65 + i] = a.sigs[m * 65 + i];
+    vhas[slot] = 1;
+}
+
+// the ledger's Header of every committed height with its votes (SPEC.md §11): the header bytes of
+// bft_export_kernel with `votes: Some(Votes([signature...]))` in ascending validator order (the
+// reference's order is a HashMap's, protocol/mod.rs:183); thread per (instance, height)
+__global__ __launch_bounds__(64) void bft_export_votes_kernel(Params p, const uint8_t* vsig, const uint8_t* vhas,
+                                                             uint8_t* out, uint64_t slot, uint32_t* lens) {
+    __shared__ __attribute__((aligned(16))) uint64_t wbs[64 * HDR_WORDS];
+    const uint64_t t = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    const uint64_t H = p.heights;
+    if (t >= (uint64_t)p.n_instances * H) return;
+    const uint32_t il = (uint32_t)(t / H), x = (uint32_t)(t % H) + 1u;
+    if (x > p.committed_height[il]) { lens[t] = 0; return; }
+    uint32_t prev[8];
+    if (x == 1) {
+        for (int i = 0; i < 8; ++i)
+            prev[i] = (uint32_t)p.genesis_hash[4 * i] | ((uint32_t)p.genesis_hash[4 * i + 1] << 8) |
+                      ((uint32_t)p.genesis_hash[4 * i + 2] << 16) | ((uint32_t)p.genesis_hash[4 * i + 3] << 24);
+    } else {
+        const uint32_t* ph = (const uint32_t*)(p.hash + ((uint64_t)il * p.rows + (x - 1)) * 32);
+        for (int i = 0; i < 8; ++i) prev[i] = ph[i];
+    }
+    const uint32_t* row = p.rec + ((uint64_t)il * p.rows + x) * 4;
+    const uint32_t prop = row[1] & 0xffffu, var = (row[1] >> 16) & 1u;
+    const uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)row[2] + 1ull);
+    uint64_t* wb = wbs + threadIdx.x * HDR_WORDS;
+    const uint32_t hl = header_raw(wb, prev, p.addresses + 20u * prop, p.seed, p.first_instance + il, x, prop, var, time);
+    uint8_t* o = out + t * slot;
+    const uint8_t* hb = (const uint8_t*)wb;
+    uint64_t k = 0;
+    for (uint32_t i = 0; i + 1 < hl; ++i) o[k++] = hb[i];        // all but the trailing `votes: None`
+    const uint8_t* has = vhas + ((uint64_t)il * H + (x - 1)) * p.n;
+    uint32_t nv = 0;
+    for (uint32_t v = 0; v < p.n; ++v) nv += has[v];
+    if (nv < 16u) o[k++] = (uint8_t)(0x90u | nv);
+    else { o[k++] = 0xdc; o[k++] = (uint8_t)(nv >> 8); o[k++] = (uint8_t)nv; }
+    for (uint32_t v = 0; v < p.n; ++v) {
+        if (!has[v]) continue;
+        const uint8_t* sg = vsig + (((uint64_t)il * H + (x - 1)) * p.n + v) * 65;
+        o[k++] = 0xdc; o[k++] = 0x00; o[k++] = 65;
+        for (int i = 0; i < 65; ++i) {
+            if (sg[i] >= 128u) o[k++] = 0xcc;
+            o[k++] = sg[i];
+        }
+    }
+    lens[t] = (uint32_t)k;
+}
+
 }  // namespace bft
 
 #include "bft_host.h"
@@ -579,6 +649,11 @@ struct bftsim {
     uint32_t* d_mlog = nullptr;       // [cap_inst][mlog_cap][MLOG_WORDS]
     uint32_t* d_mlog_n = nullptr;     // [cap_inst]
     uint8_t* d_keys = nullptr;        // [2N][32]: the validators' secrets, then their forged keys
+    uint32_t* d_vsnap = nullptr;      // [cap_inst][seg][8] commit set at each lane's last commit
+    uint32_t* d_votes = nullptr;      // [cap_inst][rows][8] canonical committer's commit set per height
+    uint8_t* d_vsig = nullptr;        // [last_n][H][N][65] the votes' signatures (bftsim_crypto_verify)
+    uint8_t* d_vhas = nullptr;        // [last_n][H][N]
+    uint64_t vsig_n = 0;              // instances d_vsig holds (0: no verify since the last launch)
     void* sig = nullptr;              // libbftsig handle (bftsig_t*)
     uint8_t* d_tips = nullptr;        // [cap_inst * 32]
     uint32_t* d_rcs = nullptr;        // RoundChangeSet tables, rcs_words(seg) per wave / workgroup
@@ -645,6 +720,8 @@ static void free_bufs(bftsim* h) {
     h->d_backlog = nullptr;
     (void)hipFree(h->d_mlog); (void)hipFree(h->d_mlog_n);
     h->d_mlog = nullptr; h->d_mlog_n = nullptr;
+    (void)hipFree(h->d_vsnap); (void)hipFree(h->d_votes); (void)hipFree(h->d_vsig); (void)hipFree(h->d_vhas);
+    h->d_vsnap = nullptr; h->d_votes = nullptr; h->d_vsig = nullptr; h->d_vhas = nullptr; h->vsig_n = 0;
     h->backlog_bytes = 0;
     (void)hipFree(h->d_resume); (void)hipFree(h->d_save);
     h->d_resume = nullptr; h->d_save = nullptr;
@@ -880,6 +957,8 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         if (h->crypto) {
             HIPCHECK(h, hipMalloc(&h->d_mlog, n * (uint64_t)h->mlog_cap * bft::MLOG_WORDS * 4));
             HIPCHECK(h, hipMalloc(&h->d_mlog_n, n * 4));
+            HIPCHECK(h, hipMalloc(&h->d_vsnap, n * (uint64_t)h->seg * 8 * 4));
+            HIPCHECK(h, hipMalloc(&h->d_votes, n * (uint64_t)h->hcap * 8 * 4));
         }
         if (h->cfg.backlog_mode == BFTSIM_BACKLOG_REPLAY) {
             h->backlog_bytes = blocks * bft::backlog_words(h->seg) * 4;
@@ -953,6 +1032,9 @@ static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
         p.mlog_n = h->d_mlog_n;
         p.mlog_cap = h->mlog_cap;
         for (int k = 0; k < 4; ++k) p.forged[k] = h->forged[k];
+        p.vsnap = h->d_vsnap;
+        p.votes = h->d_votes;
+        p.fast = 0;                  // one message at a time: the commit set at the commit instant (votes)
     }
     if (h->window) {
         p.window_mask = h->window - 1;
@@ -1053,6 +1135,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         }
     }
     h->last_n = n;
+    h->vsig_n = 0;
     h->last_first = first;
     h->last_stream = s;
     return BFTSIM_OK;
@@ -1378,6 +1461,18 @@ int bftsim_crypto_verify(bftsim_t* h, bftsim_crypto_report* out, uint8_t* inst_c
             hipLaunchKernelGGL(bft::bft_crypto_check_kernel, dim3(g), dim3(64), 0, s, p, a, M);
             e = hipGetLastError();
         }
+        // the votes of every committed block, kept for bftsim_export_ledger
+        const uint64_t vs = n * (uint64_t)h->cfg.heights * h->cfg.n;
+        (void)hipFree(h->d_vsig); (void)hipFree(h->d_vhas);
+        h->d_vsig = nullptr; h->d_vhas = nullptr; h->vsig_n = 0;
+        if (e == hipSuccess && rc == 0) e = hipMalloc(&h->d_vsig, vs * 65);
+        if (e == hipSuccess && rc == 0) e = hipMalloc(&h->d_vhas, vs);
+        if (e == hipSuccess && rc == 0) e = hipMemsetAsync(h->d_vhas, 0, vs, s);
+        if (e == hipSuccess && rc == 0) {
+            hipLaunchKernelGGL(bft::bft_crypto_votes_kernel, dim3(g), dim3(64), 0, s, p, a, M, h->d_vsig, h->d_vhas);
+            e = hipGetLastError();
+            if (e == hipSuccess) h->vsig_n = n;
+        }
     }
     unsigned long long c[8] = {0};
     if (e == hipSuccess && rc == 0) e = hipMemcpyAsync(c, a.counts, 64, hipMemcpyDeviceToHost, s);
@@ -1396,6 +1491,32 @@ int bftsim_crypto_verify(bftsim_t* h, bftsim_crypto_report* out, uint8_t* inst_c
     out->recoveries = c[0] + c[1];
     return BFTSIM_OK;
 }
+
+int bftsim_export_ledger(bftsim_t* h, uint8_t* hdr, uint64_t slot_bytes, uint32_t* hdr_len) {
+    if (!h || !hdr || !hdr_len) return BFTSIM_EINVAL;
+    if (!h->crypto || h->vsig_n == 0 || h->vsig_n != h->last_n)
+        return fail(h, BFTSIM_EINVAL, "no votes: bftsim_crypto_verify after the launch first");
+    if (slot_bytes < bftsim_ledger_slot_bytes(h->cfg.n)) return fail(h, BFTSIM_EINVAL, "slot_bytes too small");
+    if (int rc = sync_all(h)) return rc;
+    const uint64_t n = h->last_n, H = h->cfg.heights, cnt = n * H;
+    bft::Params p = make_params(h, h->last_first, n);
+    uint8_t* d_out = nullptr;
+    uint32_t* d_len = nullptr;
+    HIPCHECK(h, hipMalloc(&d_out, cnt * slot_bytes));
+    HIPCHECK(h, hipMalloc(&d_len, cnt * 4));
+    hipLaunchKernelGGL(bft::bft_export_votes_kernel, dim3((uint32_t)((cnt + 63) / 64)), dim3(64), 0, h->last_stream, p,
+                       h->d_vsig, h->d_vhas, d_out, slot_bytes, d_len);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(h->last_stream);
+    if (e == hipSuccess) e = hipMemcpy(hdr, d_out, cnt * slot_bytes, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(hdr_len, d_len, cnt * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d_out);
+    (void)hipFree(d_len);
+    if (e != hipSuccess) return fail(h, BFTSIM_EHIP, std::string("bftsim_export_ledger: ") + hipGetErrorString(e));
+    return BFTSIM_OK;
+}
+
+uint64_t bftsim_ledger_slot_bytes(uint32_t n) { return ((uint64_t)BFTSIM_HEADER_SLOT + 3 + (uint64_t)n * 133 + 7) & ~7ull; }
 
 int bftsim_stats_get(bftsim_t* h, bftsim_stats* out) {
     if (!h || !out) return BFTSIM_EINVAL;

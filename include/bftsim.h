@@ -190,6 +190,16 @@ int bftsim_set_crypto(bftsim_t *h, const uint8_t *secrets32, const uint8_t *forg
  * inst_messages (host, n, nullable) = messages per instance */
 int bftsim_crypto_verify(bftsim_t *h, bftsim_crypto_report *out, uint8_t *inst_checksum, uint32_t *inst_messages);
 
+/* the ledger with votes (real-crypto mode, after bftsim_crypto_verify): for every instance and height
+ * x <= committed_height, in slot [i*H + x-1] of `slot_bytes` bytes, the Header that Backend::commit
+ * inserts (backend.rs:163-174): the block's header (SPEC.md §7) with votes = the signatures of the
+ * Commit messages in the committing Core's commit set at its commit (core.rs:402-413), ascending
+ * validator order. hdr_len = 0 beyond the committed height. The hash of a header is the run's
+ * block_hash of that height (block_hash() ignores votes, types/block.rs:76-80). Together with
+ * block_hash per height this is the ledger's headers + block_hashes_by_height (store/schema.rs). */
+uint64_t bftsim_ledger_slot_bytes(uint32_t n_validators);
+int bftsim_export_ledger(bftsim_t *h, uint8_t *hdr, uint64_t slot_bytes, uint32_t *hdr_len);
+
 /* ValidatorSet / block helpers on the host (validator.rs, types/block.rs) */
 uint32_t bftsim_two_thirds_majority(uint32_t n);                    /* validator.rs:149-154 */
 uint32_t bftsim_seed_from_hash(const uint8_t hash[32], uint32_t n); /* validator.rs:39-48 (BE) */

@@ -56,8 +56,9 @@ def _digest(cfg, res, i, inst, b, genesis):
     return O.keccak256(_header(cfg, inst, x, u["prop"], u["var"], u["T"], _parent(cfg, res, i, x, genesis)))
 
 
-def instance_checksums(cfg, first, res, secrets, forged=()):
-    """[n, 32] XOR over each instance's logged messages of keccak(signature || seal or 0^65)"""
+def instance_checksums(cfg, first, res, secrets, forged=(), sigs_out=None):
+    """[n, 32] XOR over each instance's logged messages of keccak(signature || seal or 0^65);
+    sigs_out (a dict) receives {(instance, sender, code, height, round, old): signature}"""
     n = len(res["committed_height"])
     L = O.lib()
     c, keep = O.to_orc(cfg)
@@ -85,6 +86,8 @@ def instance_checksums(cfg, first, res, secrets, forged=()):
             else:
                 msg = R.subject(r, h, d)
             sig = S.sign(key, O.keccak256(R.gossip(code, ctime, msg, None, seal)))
+            if sigs_out is not None:
+                sigs_out[(i, sender, code, h, r, bool(int(e[6]) & 8))] = sig
             t = O.keccak256(sig + (seal if seal is not None else bytes(65)))
             acc = bytearray(a ^ b_ for a, b_ in zip(acc, t))
         out[i] = np.frombuffer(bytes(acc), np.uint8)

@@ -292,6 +292,7 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
     if (g_mlog) {
         P.mlog = g_mlog; P.mlog_n = g_mlog_n; P.mlog_cap = g_mlog_cap;
         for (int k = 0; k < 4; ++k) P.forged[k] = g_forged[k];
+        P.fast = 0;                                        // as libbftsim in real-crypto mode
         g_mlog = nullptr;                                  // one run
     }
     std::vector<uint32_t> ch(n), flags(n), ticks(n);

@@ -54,6 +54,42 @@ def test_reference_keys_cfg1():
     assert np.array_equal(rep["checksum"], C.instance_checksums(cfg, 0, ref, secrets))
 
 
+def test_ledger_with_votes_cfg1():
+    """bftsim_export_ledger: each committed Header carries, in ascending validator order, the Commit
+    signatures of more than 2N/3 validators for that height and committed round (backend.rs:163-174);
+    without the votes the bytes are the oracle's header, whose hash is the run's block hash."""
+    import msgpack
+    from bftsim.runtime import Simulator
+    keys = {bytes.fromhex(k["address"]): bytes.fromhex(k["secret"]) for k in GOLD["reference_keys"]}
+    cfg = cfg1(True, heights=6)
+    secrets = [keys[a] for a in cfg.addresses]
+    sim = Simulator(cfg)
+    try:
+        sim.set_crypto(secrets)
+        got = sim.run(0, 1)
+        sim.crypto_verify()
+        ledger = sim.export_ledger()[0]
+    finally:
+        sim.close()
+    ref = O.run_crypto(cfg, 0, 1)
+    sigs = {}
+    C.instance_checksums(cfg, 0, ref, secrets, sigs_out=sigs)
+    ch = int(got["committed_height"][0])
+    assert len(ledger) == ch == 6
+    q = (2 * cfg.n) // 3
+    for x, hdr in enumerate(ledger, start=1):
+        fields = msgpack.unpackb(hdr)
+        assert len(fields) == 13 and fields[7] == x
+        votes = [bytes(v) for v in fields[12]]
+        assert len(votes) > q
+        rnd = int(got["round"][0, x - 1])
+        cands = {s: sigs[(0, s, 3, x, rnd, False)] for s in range(cfg.n) if (0, s, 3, x, rnd, False) in sigs}
+        order = [s for s, sg in sorted(cands.items()) if sg in votes]
+        assert [cands[s] for s in order] == votes          # every vote is a sender's Commit, ascending
+        plain = msgpack.packb(fields[:12] + [None])
+        assert O.keccak256(plain) == bytes(got["block_hash"][0, x - 1])
+
+
 def test_forged_sender_dropped():
     cfg, secrets = _keyed(BftConfig(n=4, heights=6, seed=21), 7)
     got, rep = _run(cfg, secrets, 3, 1, forged=(2,))
