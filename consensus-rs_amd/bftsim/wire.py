@@ -33,6 +33,107 @@ class CBatch(ctypes.Structure):
                 ("commit_seal", ctypes.c_void_p), ("ttl", ctypes.c_void_p), ("raw_time", ctypes.c_void_p)]
 
 
+# array-of-structures mirrors of include/bftwire.h (bftwire_tx / _block / _preprepare), C layout
+NONE = 0xFFFFFFFF
+MAX_EXTRA, MAX_VOTES, MAX_TX, MAX_PAYLOAD = 32, 16, 2, 64
+TX_DTYPE = np.dtype({"names": ["nonce", "price", "gas_limit", "amount", "payload_len", "has_recipient", "has_sig",
+                               "recipient", "payload", "sig"],
+                     "formats": ["<u8", "<u8", "<u8", "<u8", "<u4", "u1", "u1", ("u1", 20), ("u1", MAX_PAYLOAD),
+                                 ("u1", 65)],
+                     "offsets": [0, 8, 16, 24, 32, 36, 37, 40, 60, 124], "itemsize": 200})
+BLOCK_DTYPE = np.dtype({"names": ["bloom", "difficulty", "height", "gas_limit", "gas_used", "time", "extra_len",
+                                  "n_votes", "n_tx", "prev_hash", "root", "tx_hash", "receipt_hash", "proposer",
+                                  "extra", "votes", "tx"],
+                        "formats": ["<u8"] * 6 + ["<u4"] * 3 + [("u1", 32)] * 4 + [("u1", 20), ("u1", MAX_EXTRA),
+                                                                                 ("u1", (MAX_VOTES, 65)),
+                                                                                 (TX_DTYPE, MAX_TX)],
+                        "offsets": [0, 8, 16, 24, 32, 40, 48, 52, 56, 64, 96, 128, 160, 192, 212, 244, 1288],
+                        "itemsize": 1688})
+PP_DTYPE = np.dtype({"names": ["round", "height", "create_time", "ttl", "raw_time", "has_sig", "signature", "block"],
+                     "formats": ["<u8"] * 5 + ["u1", ("u1", 65), BLOCK_DTYPE],
+                     "offsets": [0, 8, 16, 24, 32, 40, 48, 120], "itemsize": 1808})
+
+
+def block_to_rec(b: dict, rec):
+    """a block dict (oracle/wire_ref.py keys) into one BLOCK_DTYPE record"""
+    for k in ("bloom", "difficulty", "height", "gas_limit", "gas_used", "time"):
+        rec[k] = b[k]
+    for k in ("prev_hash", "root", "tx_hash", "receipt_hash", "proposer"):
+        rec[k] = np.frombuffer(bytes(b[k]), np.uint8)
+    ex = b.get("extra")
+    rec["extra_len"] = NONE if ex is None else len(ex)
+    if ex is not None:
+        rec["extra"][: len(ex)] = np.frombuffer(bytes(ex), np.uint8)
+    vs = b.get("votes")
+    rec["n_votes"] = NONE if vs is None else len(vs)
+    for j, v in enumerate(vs or []):
+        rec["votes"][j] = np.frombuffer(bytes(v), np.uint8)
+    rec["n_tx"] = len(b["txs"])
+    for j, t in enumerate(b["txs"]):
+        r = rec["tx"][j]
+        for k in ("nonce", "price", "gas_limit", "amount"):
+            r[k] = t[k]
+        r["has_recipient"] = t.get("recipient") is not None
+        if t.get("recipient") is not None:
+            r["recipient"] = np.frombuffer(bytes(t["recipient"]), np.uint8)
+        r["payload_len"] = len(t["payload"])
+        r["payload"][: len(t["payload"])] = np.frombuffer(bytes(t["payload"]), np.uint8)
+        r["has_sig"] = t.get("sig") is not None
+        if t.get("sig") is not None:
+            r["sig"] = np.frombuffer(bytes(t["sig"]), np.uint8)
+        rec["tx"][j] = r
+
+
+def rec_to_block(rec) -> dict:
+    b = {k: int(rec[k]) for k in ("bloom", "difficulty", "height", "gas_limit", "gas_used", "time")}
+    for k in ("prev_hash", "root", "tx_hash", "receipt_hash", "proposer"):
+        b[k] = bytes(rec[k])
+    el, nv = int(rec["extra_len"]), int(rec["n_votes"])
+    b["extra"] = None if el == NONE else bytes(rec["extra"][:el])
+    b["votes"] = None if nv == NONE else [bytes(rec["votes"][j]) for j in range(nv)]
+    b["txs"] = []
+    for j in range(int(rec["n_tx"])):
+        r = rec["tx"][j]
+        b["txs"].append(dict(nonce=int(r["nonce"]), price=int(r["price"]), gas_limit=int(r["gas_limit"]),
+                             amount=int(r["amount"]), recipient=bytes(r["recipient"]) if r["has_recipient"] else None,
+                             payload=bytes(r["payload"][: int(r["payload_len"])]),
+                             sig=bytes(r["sig"]) if r["has_sig"] else None))
+    return b
+
+
+def preprepares_to_array(ms) -> np.ndarray:
+    a = np.zeros(len(ms), PP_DTYPE)
+    for i, m in enumerate(ms):
+        for k in ("round", "height", "create_time"):
+            a[i][k] = m[k]
+        a[i]["ttl"], a[i]["raw_time"] = m.get("ttl", 10), m.get("raw_time", 0)
+        a[i]["has_sig"] = m.get("signature") is not None
+        if m.get("signature") is not None:
+            a[i]["signature"] = np.frombuffer(bytes(m["signature"]), np.uint8)
+        blk = a[i]["block"]
+        block_to_rec(m["block"], blk)
+        a[i]["block"] = blk
+    return a
+
+
+def array_to_preprepares(a) -> list:
+    out = []
+    for r in a:
+        out.append(dict(round=int(r["round"]), height=int(r["height"]), create_time=int(r["create_time"]),
+                        ttl=int(r["ttl"]), raw_time=int(r["raw_time"]),
+                        signature=bytes(r["signature"]) if r["has_sig"] else None, block=rec_to_block(r["block"])))
+    return out
+
+
+def blocks_to_array(blocks) -> np.ndarray:
+    a = np.zeros(len(blocks), BLOCK_DTYPE)
+    for i, b in enumerate(blocks):
+        rec = a[i]
+        block_to_rec(b, rec)
+        a[i] = rec
+    return a
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -47,6 +148,12 @@ def lib():
         L.bftwire_encode.argtypes = [vp, ctypes.POINTER(CBatch), u64, vp, u64, vp, vp, vp, vp, vp]
         L.bftwire_decode.argtypes = [vp, vp, vp, u64, ctypes.POINTER(CBatch), vp, vp, vp, vp]
         L.bftwire_split_frames.argtypes = [vp, u64, vp, u64]
+        L.bftwire_encode_preprepare.argtypes = [vp, vp, u64, vp, u64, vp, vp, vp, vp, vp]
+        L.bftwire_decode_preprepare.argtypes = [vp, vp, vp, u64, vp, vp, vp]
+        L.bftwire_encode_blocks.argtypes = [vp, vp, vp, u64, vp, vp, vp, u64, vp, vp, vp]
+        L.bftwire_decode_blocks.argtypes = [vp, vp, vp, u64, ctypes.c_uint32, vp, vp, vp, vp]
+        L.bftwire_encode_sync.argtypes = [vp, vp, u64, vp, vp, vp, u64, vp, vp, vp]
+        L.bftwire_decode_sync.argtypes = [vp, vp, vp, u64, vp, vp, vp]
         L.bftwire_split_frames.restype = u64
         _lib = L
     return _lib
@@ -145,3 +252,116 @@ class Codec:
                                          hl.data_ptr(), ok.data_ptr(), s), "bftwire_decode")
         out["has_sig"], out["has_seal"] = hs[:n], hl[:n]
         return out, ok[:n]
+
+
+
+    def encode_preprepare(self, ms, cap: int | None = None, hashes: bool = True):
+        """Preprepare frames of a list of dicts (oracle/wire_ref.py keys) -> (stream, offsets, sign_digest,
+        msg_hash, ok) tensors (bftwire_encode_preprepare)"""
+        t = self.torch
+        a = preprepares_to_array(ms)
+        n = len(a)
+        d_in = _dev_bytes(self, a)
+        cap = cap or n * 16384
+        sd = t.zeros((max(n, 1), 32), dtype=t.uint8, device=self.device) if hashes else None
+        mh = t.zeros((max(n, 1), 32), dtype=t.uint8, device=self.device) if hashes else None
+        def go(stream, off, ok):
+            self._check(lib().bftwire_encode_preprepare(self.h, d_in.data_ptr(), n, stream.data_ptr(), cap, off.data_ptr(),
+                                                        sd.data_ptr() if hashes else None,
+                                                        mh.data_ptr() if hashes else None, ok.data_ptr(), None),
+                        "bftwire_encode_preprepare")
+        stream, off, ok = _encode_frames(self, n, go, cap)
+        return stream, off, (sd[:n] if hashes else None), (mh[:n] if hashes else None), ok
+
+
+    def decode_preprepare(self, stream_bytes, frame_off):
+        t = self.torch
+        s = t.as_tensor(np.frombuffer(bytes(stream_bytes), np.uint8) if not t.is_tensor(stream_bytes) else stream_bytes)
+        s = s.to(self.device) if s.numel() else t.zeros(1, dtype=t.uint8, device=self.device)
+        offs = t.as_tensor(np.asarray(frame_off, dtype=np.int64)).to(self.device)
+        n = offs.numel() - 1
+        out = t.zeros(max(n, 1) * PP_DTYPE.itemsize, dtype=t.uint8, device=self.device)
+        ok = t.zeros(max(n, 1), dtype=t.uint8, device=self.device)
+        self._check(lib().bftwire_decode_preprepare(self.h, s.data_ptr(), offs.data_ptr(), n, out.data_ptr(), ok.data_ptr(),
+                                                    None), "bftwire_decode_preprepare")
+        t.cuda.synchronize(self.device)
+        arr = out.cpu().numpy().view(PP_DTYPE)[:n]
+        return arr, ok.cpu().numpy()[:n]
+
+
+    def encode_blocks(self, frames, ttl=None, raw_time=None, cap: int | None = None):
+        """Block frames: `frames` = list of block-dict lists (one RawMessage{Block, Blocks} each)"""
+        t = self.torch
+        blocks = [b for f in frames for b in f]
+        boff = np.cumsum([0] + [len(f) for f in frames]).astype(np.uint64)
+        n = len(frames)
+        d_b = _dev_bytes(self, blocks_to_array(blocks)) if blocks else t.zeros(8, dtype=t.uint8, device=self.device)
+        d_off = t.as_tensor(boff.view(np.int64)).to(self.device)
+        d_ttl = t.as_tensor(np.asarray(ttl, np.int64)).to(self.device) if ttl is not None else None
+        d_rt = t.as_tensor(np.asarray(raw_time, np.int64)).to(self.device) if raw_time is not None else None
+        cap = cap or max(1, len(blocks)) * 16384 + n * 64
+        def go(stream, off, ok):
+            self._check(lib().bftwire_encode_blocks(self.h, d_b.data_ptr(), d_off.data_ptr(), n,
+                                                    d_ttl.data_ptr() if d_ttl is not None else None,
+                                                    d_rt.data_ptr() if d_rt is not None else None, stream.data_ptr(), cap,
+                                                    off.data_ptr(), ok.data_ptr(), None), "bftwire_encode_blocks")
+        return _encode_frames(self, n, go, cap)
+
+
+    def decode_blocks(self, stream_bytes, frame_off, max_per_frame: int = 4):
+        t = self.torch
+        s = t.as_tensor(np.frombuffer(bytes(stream_bytes), np.uint8) if not t.is_tensor(stream_bytes) else stream_bytes)
+        s = s.to(self.device) if s.numel() else t.zeros(1, dtype=t.uint8, device=self.device)
+        offs = t.as_tensor(np.asarray(frame_off, dtype=np.int64)).to(self.device)
+        n = offs.numel() - 1
+        out = t.zeros(max(n, 1) * max_per_frame * BLOCK_DTYPE.itemsize, dtype=t.uint8, device=self.device)
+        cnt = t.zeros(max(n, 1), dtype=t.int32, device=self.device)
+        ok = t.zeros(max(n, 1), dtype=t.uint8, device=self.device)
+        self._check(lib().bftwire_decode_blocks(self.h, s.data_ptr(), offs.data_ptr(), n, max_per_frame, out.data_ptr(),
+                                                cnt.data_ptr(), ok.data_ptr(), None), "bftwire_decode_blocks")
+        t.cuda.synchronize(self.device)
+        arr = out.cpu().numpy().view(BLOCK_DTYPE)[: n * max_per_frame].reshape(n, max_per_frame)
+        return arr, cnt.cpu().numpy()[:n], ok.cpu().numpy()[:n]
+
+
+    def encode_sync(self, heights, ttl=None, raw_time=None, cap: int | None = None):
+        t = self.torch
+        h = t.as_tensor(np.asarray(heights, np.uint64).view(np.int64)).to(self.device)
+        n = h.numel()
+        cap = cap or n * 64
+        def go(stream, off, ok):
+            self._check(lib().bftwire_encode_sync(self.h, h.data_ptr(), n, None, None, stream.data_ptr(), cap,
+                                                  off.data_ptr(), ok.data_ptr(), None), "bftwire_encode_sync")
+        return _encode_frames(self, n, go, cap)
+
+
+    def decode_sync(self, stream_bytes, frame_off):
+        t = self.torch
+        s = t.as_tensor(np.frombuffer(bytes(stream_bytes), np.uint8) if not t.is_tensor(stream_bytes) else stream_bytes)
+        s = s.to(self.device) if s.numel() else t.zeros(1, dtype=t.uint8, device=self.device)
+        offs = t.as_tensor(np.asarray(frame_off, dtype=np.int64)).to(self.device)
+        n = offs.numel() - 1
+        h = t.zeros(max(n, 1), dtype=t.int64, device=self.device)
+        ok = t.zeros(max(n, 1), dtype=t.uint8, device=self.device)
+        self._check(lib().bftwire_decode_sync(self.h, s.data_ptr(), offs.data_ptr(), n, h.data_ptr(), ok.data_ptr(), None),
+                    "bftwire_decode_sync")
+        t.cuda.synchronize(self.device)
+        return h.cpu().numpy()[:n].view(np.uint64), ok.cpu().numpy()[:n]
+
+
+def _dev_bytes(codec, arr: np.ndarray):
+    t = codec.torch
+    return t.from_numpy(np.ascontiguousarray(arr).view(np.uint8).reshape(-1).copy()).to(codec.device)
+
+
+def _encode_frames(codec, n, launch, cap):
+    """shared tail of the block-frame encoders: device offsets / ok, stream of `cap` bytes"""
+    t = codec.torch
+    stream = t.zeros(max(cap, 1), dtype=t.uint8, device=codec.device)
+    off = t.zeros(n + 1, dtype=t.int64, device=codec.device)
+    ok = t.zeros(max(n, 1), dtype=t.uint8, device=codec.device)
+    launch(stream, off, ok)
+    t.cuda.synchronize(codec.device)
+    end = int(off[n].item())
+    return stream[:end], off, ok[:n]
+

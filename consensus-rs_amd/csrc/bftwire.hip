@@ -19,6 +19,7 @@
 
 #include "../../include/bftwire.h"
 #include "bft_wire.h"
+#include "bft_wire_block.h"
 
 namespace bft {
 namespace wire {
@@ -227,6 +228,158 @@ __global__ __launch_bounds__(64) void wire_decode_kernel(const uint8_t* stream, 
     ok[i] = good ? 1 : 0;
 }
 
+
+// ---------------------------------------------------------------- block-carrying frames (SPEC.md §9b)
+// Lane per frame: a counting pass gives every frame's length, a device scan the offsets, a writing pass
+// the bytes at their offsets (and, for Preprepare, the two Keccak-256 digests streamed from the same
+// emitter). These messages are O(N) per round (one Preprepare, block gossip), not the O(N^2) votes.
+__global__ __launch_bounds__(64) void wire_pp_len_kernel(const bftwire_preprepare* in, uint64_t n, uint64_t* lens,
+                                                         uint8_t* ok) {
+    const uint64_t i = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (i >= n) { if (i == n) lens[n] = 0; return; }
+    const bftwire_preprepare& m = in[i];
+    const bool fit = block_fits(m.block);
+    uint32_t L = 0;
+    if (fit) emit_frame(CountE{&L}, P2P_CONSENSUS, m.ttl, m.raw_time, [&](const auto& e) { emit_pp_gossip(e, m, true); });
+    lens[i] = fit ? L : 0;
+    ok[i] = fit ? 1 : 0;
+}
+__global__ __launch_bounds__(64) void wire_pp_write_kernel(const bftwire_preprepare* in, uint64_t n, const uint64_t* off,
+                                                           uint8_t* stream, uint64_t cap, uint8_t* sign_digest,
+                                                           uint8_t* msg_hash, uint8_t* ok) {
+    __shared__ uint8_t kb[64 * 136];
+    const uint64_t i = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (i >= n) return;
+    const bftwire_preprepare& m = in[i];
+    if (ok[i] && off[i + 1] <= cap) {
+        uint32_t w = 0;
+        emit_frame(BufE{stream + off[i], &w, (uint32_t)(off[i + 1] - off[i])}, P2P_CONSENSUS, m.ttl, m.raw_time,
+                   [&](const auto& e) { emit_pp_gossip(e, m, true); });
+    } else {
+        ok[i] = 0;
+    }
+    uint8_t* kbuf = kb + threadIdx.x * 136;
+    if (sign_digest) {
+        crypto::KSink k(kbuf);
+        if (ok[i]) emit_pp_gossip(KE{&k}, m, false);
+        uint8_t o[32];
+        k.finish(o);
+        for (int j = 0; j < 32; ++j) sign_digest[32u * i + j] = ok[i] ? o[j] : 0;
+    }
+    if (msg_hash) {
+        crypto::KSink k(kbuf);
+        if (ok[i]) emit_pp_gossip(KE{&k}, m, true);
+        uint8_t o[32];
+        k.finish(o);
+        for (int j = 0; j < 32; ++j) msg_hash[32u * i + j] = ok[i] ? o[j] : 0;
+    }
+}
+__global__ __launch_bounds__(64) void wire_pp_decode_kernel(const uint8_t* stream, const uint64_t* off, uint64_t n,
+                                                            bftwire_preprepare* out, uint8_t* ok) {
+    const uint64_t i = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (i >= n) return;
+    bftwire_preprepare d;
+    memset(&d, 0, sizeof d);
+    const uint64_t o = off[i], len = off[i + 1] - o;
+    const bool good = len < (1u << 20) && decode_pp_frame(stream + o, (uint32_t)len, d);
+    if (!good) memset(&d, 0, sizeof d);
+    out[i] = d;
+    ok[i] = good ? 1 : 0;
+}
+
+template <class E>
+__device__ inline void emit_blocks_payload(const E& e, const bftwire_block* b, uint64_t lo, uint64_t hi) {
+    mp_arr(e, (uint32_t)(hi - lo));                       // Blocks(Vec<Block>): newtype, transparent
+    for (uint64_t j = lo; j < hi; ++j) emit_block(e, b[j]);
+}
+__global__ __launch_bounds__(64) void wire_blocks_len_kernel(const bftwire_block* b, const uint64_t* boff, uint64_t n,
+                                                             const uint64_t* ttl, const uint64_t* rtime, uint64_t* lens,
+                                                             uint8_t* ok) {
+    const uint64_t k = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (k >= n) { if (k == n) lens[n] = 0; return; }
+    bool fit = true;
+    for (uint64_t j = boff[k]; j < boff[k + 1]; ++j) fit = fit && block_fits(b[j]);
+    uint32_t L = 0;
+    if (fit)
+        emit_frame(CountE{&L}, P2P_BLOCK, ttl ? ttl[k] : DEFAULT_TTL, rtime ? rtime[k] : 0ull,
+                   [&](const auto& e) { emit_blocks_payload(e, b, boff[k], boff[k + 1]); });
+    lens[k] = fit ? L : 0;
+    ok[k] = fit ? 1 : 0;
+}
+__global__ __launch_bounds__(64) void wire_blocks_write_kernel(const bftwire_block* b, const uint64_t* boff, uint64_t n,
+                                                               const uint64_t* ttl, const uint64_t* rtime,
+                                                               const uint64_t* off, uint8_t* stream, uint64_t cap,
+                                                               uint8_t* ok) {
+    const uint64_t k = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (k >= n) return;
+    if (!ok[k] || off[k + 1] > cap) { ok[k] = 0; return; }
+    uint32_t w = 0;
+    emit_frame(BufE{stream + off[k], &w, (uint32_t)(off[k + 1] - off[k])}, P2P_BLOCK, ttl ? ttl[k] : DEFAULT_TTL,
+               rtime ? rtime[k] : 0ull, [&](const auto& e) { emit_blocks_payload(e, b, boff[k], boff[k + 1]); });
+}
+__global__ __launch_bounds__(64) void wire_blocks_decode_kernel(const uint8_t* stream, const uint64_t* off, uint64_t n,
+                                                                uint32_t maxpf, bftwire_block* out, uint32_t* count,
+                                                                uint8_t* ok) {
+    const uint64_t k = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (k >= n) return;
+    const uint64_t o = off[k], len = off[k + 1] - o;
+    const uint8_t* f = stream + o;
+    bool good = len >= 4 && len < (1u << 24) && frame_size(f) == len - 4u;
+    uint32_t cnt = 0;
+    if (good) {
+        Mem m{f + 4, (uint32_t)len - 4u, 0};
+        uint64_t t, rt;
+        uint32_t plen;
+        good = rd_envelope(m, P2P_BLOCK, t, rt, plen);
+        if (good) {
+            Arr<Mem> p{&m, plen, false};
+            good = rd_arr(p, cnt) && cnt <= maxpf;
+            for (uint32_t j = 0; good && j < cnt; ++j) {
+                bftwire_block blk;
+                memset(&blk, 0, sizeof blk);
+                good = rd_block(p, blk);
+                out[k * maxpf + j] = blk;
+            }
+            good = good && p.left == 0 && !p.bad && m.i == m.n;
+        }
+    }
+    count[k] = good ? cnt : 0;
+    ok[k] = good ? 1 : 0;
+}
+
+__global__ __launch_bounds__(64) void wire_sync_len_kernel(const uint64_t* height, uint64_t n, const uint64_t* ttl,
+                                                           const uint64_t* rtime, uint64_t* lens) {
+    const uint64_t i = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (i >= n) { if (i == n) lens[n] = 0; return; }
+    uint32_t L = 0;
+    const uint64_t hv = height[i];
+    emit_frame(CountE{&L}, P2P_SYNC, ttl ? ttl[i] : DEFAULT_TTL, rtime ? rtime[i] : 0ull,
+               [&](const auto& e) { mp_uint(e, hv); });
+    lens[i] = L;
+}
+__global__ __launch_bounds__(64) void wire_sync_write_kernel(const uint64_t* height, uint64_t n, const uint64_t* ttl,
+                                                             const uint64_t* rtime, const uint64_t* off, uint8_t* stream,
+                                                             uint64_t cap, uint8_t* ok) {
+    const uint64_t i = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (i >= n) return;
+    if (off[i + 1] > cap) { ok[i] = 0; return; }
+    uint32_t w = 0;
+    const uint64_t hv = height[i];
+    emit_frame(BufE{stream + off[i], &w, (uint32_t)(off[i + 1] - off[i])}, P2P_SYNC, ttl ? ttl[i] : DEFAULT_TTL,
+               rtime ? rtime[i] : 0ull, [&](const auto& e) { mp_uint(e, hv); });
+    ok[i] = 1;
+}
+__global__ __launch_bounds__(64) void wire_sync_decode_kernel(const uint8_t* stream, const uint64_t* off, uint64_t n,
+                                                              uint64_t* height, uint8_t* ok) {
+    const uint64_t i = (uint64_t)blockIdx.x * 64u + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t o = off[i], len = off[i + 1] - o;
+    uint64_t hv = 0;
+    const bool good = len < (1u << 20) && decode_sync_frame(stream + o, (uint32_t)len, hv);
+    height[i] = good ? hv : 0;
+    ok[i] = good ? 1 : 0;
+}
+
 }  // namespace wire
 }  // namespace bft
 
@@ -343,6 +496,107 @@ int bftwire_decode(bftwire_t* h, const uint8_t* stream, const uint64_t* frame_of
     // lane per frame straight from global memory
     hipLaunchKernelGGL(wire_decode_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream_,
                        stream, frame_off, n, *out, has_sig, has_seal, ok);
+    WCHECK(h, hipGetLastError());
+    return 0;
+}
+
+// the three-pass frame encoders: per-frame lengths, scan into frame_off, bytes at the offsets
+static int frames_scan(bftwire* h, uint64_t n, uint64_t* frame_off, hipStream_t s) {
+    size_t tb = h->scan_bytes;
+    WCHECK(h, hipcub::DeviceScan::ExclusiveSum(h->scan_tmp, tb, h->lens, frame_off, (int)(n + 1), s));
+    return 0;
+}
+static inline dim3 lanes(uint64_t n) { return dim3((unsigned)((n + 1 + 63) / 64)); }
+
+int bftwire_encode_preprepare(bftwire_t* h, const bftwire_preprepare* in, uint64_t n, uint8_t* stream, uint64_t cap,
+                              uint64_t* frame_off, uint8_t* sign_digest, uint8_t* msg_hash, uint8_t* ok, void* stream_) {
+    using namespace bft::wire;
+    if (!h) return -1;
+    if (!frame_off || !ok || (n && (!in || !stream))) return wfail(h, -1, "bftwire_encode_preprepare: null buffer");
+    if (n > 0x7fffffffull) return wfail(h, -1, "bftwire_encode_preprepare: batch too large");
+    hipStream_t s = (hipStream_t)stream_;
+    WCHECK(h, hipSetDevice(h->device));
+    if (n == 0) return hipMemsetAsync(frame_off, 0, 8, s) == hipSuccess ? 0 : wfail(h, -2, "memset");
+    if (int rc = wire_reserve(h, n)) return rc;
+    hipLaunchKernelGGL(wire_pp_len_kernel, lanes(n), dim3(64), 0, s, in, n, h->lens, ok);
+    WCHECK(h, hipGetLastError());
+    if (int rc = frames_scan(h, n, frame_off, s)) return rc;
+    hipLaunchKernelGGL(wire_pp_write_kernel, lanes(n), dim3(64), 0, s, in, n, frame_off, stream, cap, sign_digest, msg_hash, ok);
+    WCHECK(h, hipGetLastError());
+    return 0;
+}
+
+int bftwire_decode_preprepare(bftwire_t* h, const uint8_t* stream, const uint64_t* frame_off, uint64_t n,
+                              bftwire_preprepare* out, uint8_t* ok, void* stream_) {
+    using namespace bft::wire;
+    if (!h) return -1;
+    if (n == 0) return 0;
+    if (!stream || !frame_off || !out || !ok) return wfail(h, -1, "bftwire_decode_preprepare: null buffer");
+    WCHECK(h, hipSetDevice(h->device));
+    hipLaunchKernelGGL(wire_pp_decode_kernel, lanes(n), dim3(64), 0, (hipStream_t)stream_, stream, frame_off, n, out, ok);
+    WCHECK(h, hipGetLastError());
+    return 0;
+}
+
+int bftwire_encode_blocks(bftwire_t* h, const bftwire_block* blocks, const uint64_t* block_off, uint64_t n,
+                          const uint64_t* ttl, const uint64_t* raw_time, uint8_t* stream, uint64_t cap,
+                          uint64_t* frame_off, uint8_t* ok, void* stream_) {
+    using namespace bft::wire;
+    if (!h) return -1;
+    if (!frame_off || !ok || (n && (!blocks || !block_off || !stream))) return wfail(h, -1, "bftwire_encode_blocks: null buffer");
+    if (n > 0x7fffffffull) return wfail(h, -1, "bftwire_encode_blocks: batch too large");
+    hipStream_t s = (hipStream_t)stream_;
+    WCHECK(h, hipSetDevice(h->device));
+    if (n == 0) return hipMemsetAsync(frame_off, 0, 8, s) == hipSuccess ? 0 : wfail(h, -2, "memset");
+    if (int rc = wire_reserve(h, n)) return rc;
+    hipLaunchKernelGGL(wire_blocks_len_kernel, lanes(n), dim3(64), 0, s, blocks, block_off, n, ttl, raw_time, h->lens, ok);
+    WCHECK(h, hipGetLastError());
+    if (int rc = frames_scan(h, n, frame_off, s)) return rc;
+    hipLaunchKernelGGL(wire_blocks_write_kernel, lanes(n), dim3(64), 0, s, blocks, block_off, n, ttl, raw_time, frame_off,
+                       stream, cap, ok);
+    WCHECK(h, hipGetLastError());
+    return 0;
+}
+
+int bftwire_decode_blocks(bftwire_t* h, const uint8_t* stream, const uint64_t* frame_off, uint64_t n, uint32_t max_per_frame,
+                          bftwire_block* out, uint32_t* count, uint8_t* ok, void* stream_) {
+    using namespace bft::wire;
+    if (!h) return -1;
+    if (n == 0) return 0;
+    if (!stream || !frame_off || !out || !count || !ok) return wfail(h, -1, "bftwire_decode_blocks: null buffer");
+    WCHECK(h, hipSetDevice(h->device));
+    hipLaunchKernelGGL(wire_blocks_decode_kernel, lanes(n), dim3(64), 0, (hipStream_t)stream_, stream, frame_off, n,
+                       max_per_frame, out, count, ok);
+    WCHECK(h, hipGetLastError());
+    return 0;
+}
+
+int bftwire_encode_sync(bftwire_t* h, const uint64_t* height, uint64_t n, const uint64_t* ttl, const uint64_t* raw_time,
+                        uint8_t* stream, uint64_t cap, uint64_t* frame_off, uint8_t* ok, void* stream_) {
+    using namespace bft::wire;
+    if (!h) return -1;
+    if (!frame_off || !ok || (n && (!height || !stream))) return wfail(h, -1, "bftwire_encode_sync: null buffer");
+    if (n > 0x7fffffffull) return wfail(h, -1, "bftwire_encode_sync: batch too large");
+    hipStream_t s = (hipStream_t)stream_;
+    WCHECK(h, hipSetDevice(h->device));
+    if (n == 0) return hipMemsetAsync(frame_off, 0, 8, s) == hipSuccess ? 0 : wfail(h, -2, "memset");
+    if (int rc = wire_reserve(h, n)) return rc;
+    hipLaunchKernelGGL(wire_sync_len_kernel, lanes(n), dim3(64), 0, s, height, n, ttl, raw_time, h->lens);
+    WCHECK(h, hipGetLastError());
+    if (int rc = frames_scan(h, n, frame_off, s)) return rc;
+    hipLaunchKernelGGL(wire_sync_write_kernel, lanes(n), dim3(64), 0, s, height, n, ttl, raw_time, frame_off, stream, cap, ok);
+    WCHECK(h, hipGetLastError());
+    return 0;
+}
+
+int bftwire_decode_sync(bftwire_t* h, const uint8_t* stream, const uint64_t* frame_off, uint64_t n, uint64_t* height,
+                        uint8_t* ok, void* stream_) {
+    using namespace bft::wire;
+    if (!h) return -1;
+    if (n == 0) return 0;
+    if (!stream || !frame_off || !height || !ok) return wfail(h, -1, "bftwire_decode_sync: null buffer");
+    WCHECK(h, hipSetDevice(h->device));
+    hipLaunchKernelGGL(wire_sync_decode_kernel, lanes(n), dim3(64), 0, (hipStream_t)stream_, stream, frame_off, n, height, ok);
     WCHECK(h, hipGetLastError());
     return 0;
 }

@@ -10,7 +10,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EMU_DIR = os.path.join(ROOT, "tests", "emu")
 LIB = os.path.join(EMU_DIR, "libwire_host.so")
 SRCS = [os.path.join(EMU_DIR, "wire_host.cpp")] + [
-    os.path.join(ROOT, "consensus-rs_amd", "csrc", f) for f in ("bft_wire.h", "bft_common.h")]
+    os.path.join(ROOT, "consensus-rs_amd", "csrc", f) for f in ("bft_wire.h", "bft_common.h", "bft_wire_block.h",
+                                                               "bft_crypto.h")] + [
+    os.path.join(ROOT, "include", "bftwire.h")]
 _lib = None
 
 
