@@ -108,18 +108,23 @@ BFT_FN uint32_t lds_bytes(uint32_t seg, bool need_seed) {
 
 // Kernel modes:
 //   MODE_FULL    every path;
+//   MODE_EXT     MODE_FULL plus the opt-in modes: backlog replay (SPEC.md §10) and the real-crypto
+//                broadcast log / votes (SPEC.md §11);
 //   MODE_RESUME  (S == 64) the full kernel over the instances the N = 64 FAST kernel (bft_fast64.h)
 //                handed over, from their saved phase: the FAST kernel saves the state below
 //                (SAVE_WORDS per lane, P.save) at the start of a phase it has no closed form for and
 //                sets P.resume_flags.
-constexpr int MODE_FULL = 0, MODE_RESUME = 2;
+constexpr int MODE_FULL = 0, MODE_EXT = 1, MODE_RESUME = 2;
 constexpr uint32_t SAVE_WORDS = 80;
 constexpr uint32_t SAVE_COLD = 72;   // words 72..78: outbox kinds that always take the general path
 
 template <class W, bool NEED_SEED, uint32_t S, int MODE = MODE_FULL>
 struct Sim {
     static constexpr bool RESUME = MODE == MODE_RESUME;
-    static_assert(MODE == MODE_FULL || S == 64, "hand-over modes are for one instance per wave");
+    // the opt-in modes (backlog replay, real-crypto log and votes) exist only in MODE_EXT builds, so
+    // the product kernels carry none of their code or registers
+    static constexpr bool EXT = MODE == MODE_EXT;
+    static_assert(MODE != MODE_RESUME || S == 64, "hand-over modes are for one instance per wave");
     using LY = Layout<S>;
     static constexpr int NW = LY::NW;
     static constexpr int RCS_K = LY::K;
@@ -326,7 +331,7 @@ struct Sim {
         commit_x = x;
         commit_blk = b;
         commit_round = r;
-        if (P.vsnap) {                                      // real-crypto mode: the votes of this commit
+        if (EXT && P.vsnap) {                               // real-crypto mode: the votes of this commit
             uint32_t* vs = P.vsnap + ((uint64_t)inst_local * S + me) * 8u;   // (core.rs:402-413)
             for (uint32_t k = 0; k < 8u; ++k) vs[k] = k < 2u * NW ? (uint32_t)(comm.w[k >> 1] >> (32u * (k & 1u))) : 0u;
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -594,7 +599,7 @@ struct Sim {
     // sender s: words [s][k][lane], k = {valid | code << 1 | wild << 4, height, round, digest lo, hi}.
     BFT_FN uint32_t* bl_p(uint32_t s, uint32_t k) const { return bl_base + (s * 5u + k) * LY::L + lane; }
     BFT_FN void backlog_store(uint32_t src, int code, uint32_t vh, uint32_t vr, uint64_t d, bool wild) {
-        if (!P.backlog_replay) return;
+        if (!EXT || !P.backlog_replay) return;
         if (*bl_p(src, 0) & 1u) return;                  // or_insert_with: the first message stays
         *bl_p(src, 0) = 1u | ((uint32_t)code << 1) | (wild ? 16u : 0u);
         *bl_p(src, 1) = vh; *bl_p(src, 2) = vr;
@@ -708,7 +713,7 @@ struct Sim {
             sync_pending = 0;
         }
         if (!core_dead && timer_tick == tick) { timer_tick = -1; handle_timer_event(); }
-        if (P.backlog_replay) replay_backlog();          // SPEC.md §10
+        if (EXT && P.backlog_replay) replay_backlog();   // SPEC.md §10
     }
 
     // segment collectives: ballots as sender bitmaps; reductions (butterfly inside a wave
@@ -755,7 +760,7 @@ struct Sim {
     BFT_FN uint32_t record_canon(uint32_t x, uint64_t b, uint32_t round, uint32_t seed, const uint32_t* hs,
                                  uint32_t ctick, uint32_t committer) {
         uint32_t add = 0;
-        if (P.votes) {                                      // the committer's commit set → the block's votes
+        if (EXT && P.votes) {                               // the committer's commit set → the block's votes
 #if defined(__HIP_DEVICE_COMPILE__)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #endif
@@ -1147,7 +1152,7 @@ struct Sim {
             return;
         }
         // general path: every delivered non-empty sender, in rotated order, one at a time
-        if (P.backlog_replay) replay_backlog();          // the stored messages first (SPEC.md §10)
+        if (EXT && P.backlog_replay) replay_backlog();   // the stored messages first (SPEC.md §10)
         M any = ps.k_pp | ps.k_pr | ps.k_cm | ps.k_ocm | ps.k_rc | ps.k_sync | ps.k_blk;
         M c = rot(mk & any, off);
         while (c.any()) {
@@ -1221,7 +1226,7 @@ struct Sim {
             off_tick = offset_tick_part(off_inst, (uint32_t)tick);
             BFT_STAMP(7);
             if (act && !resuming) t_step();
-            if (P.backlog_replay && !resuming) resolve_commits();   // replayed commits of the T-step
+            if (EXT && P.backlog_replay && !resuming) resolve_commits();   // replayed commits of the T-step
             BFT_STAMP(0);
             const uint32_t pstart = resuming ? p0 : 0u;
             resuming = false;
@@ -1230,7 +1235,7 @@ struct Sim {
                 M bal = ballot(pend_l);
                 if (bal.none()) break;
                 bool seg_pending = (bal & seg_mask).any();
-                if (P.mlog) crypto_log(act && !frozen, p);      // real-crypto mode (SPEC.md §11)
+                if (EXT && P.mlog) crypto_log(act && !frozen, p);   // real-crypto mode (SPEC.md §11)
                 if (p >= P.phase_cap) {
                     // messages still in flight are dropped (SPEC.md §2)
                     M inflight = ballot(act && nx.f != 0);
@@ -1294,7 +1299,7 @@ struct Sim {
             P.flags[inst_local] = flags;
             P.ticks[inst_local] = done_tick;
             P.views[inst_local] = views;
-            if (P.mlog) P.mlog_n[inst_local] = mlog_cnt;
+            if (EXT && P.mlog) P.mlog_n[inst_local] = mlog_cnt;
         }
     }
 };

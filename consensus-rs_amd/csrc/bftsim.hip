@@ -150,17 +150,17 @@ struct GroupHip {
     __device__ static void gadd64(uint64_t* p, uint64_t v) { atomicAdd((unsigned long long*)p, (unsigned long long)v); }
 };
 
-template <bool NEED_SEED, uint32_t S>
+template <bool NEED_SEED, int MODE, uint32_t S>
 #ifndef BFT_WAVES_PER_SIMD
 #define BFT_WAVES_PER_SIMD 3   // register budget of the one-wave kernels (LDS allows ~2.75 per SIMD)
 #endif
 __global__ __launch_bounds__(S > 64 ? S : 64, S > 64 ? 1 : BFT_WAVES_PER_SIMD) void bft_consensus_kernel(Params p) {
     extern __shared__ uint8_t lds[];
     if constexpr (S > 64) {
-        Sim<GroupHip<(int)(S / 64)>, NEED_SEED, S> sim(p, lds, blockIdx.x);
+        Sim<GroupHip<(int)(S / 64)>, NEED_SEED, S, MODE> sim(p, lds, blockIdx.x);
         sim.run();
     } else {
-        Sim<WaveHip, NEED_SEED, S> sim(p, lds, blockIdx.x);
+        Sim<WaveHip, NEED_SEED, S, MODE> sim(p, lds, blockIdx.x);
         sim.run();
     }
 }
@@ -188,28 +188,28 @@ __global__ __launch_bounds__(64, BFT_WAVES_PER_SIMD) void bft_consensus_resume_k
     sim.run();
 }
 
-template <bool NEED_SEED>
+template <bool NEED_SEED, int MODE>
 static hipError_t launch_consensus(uint32_t seg, dim3 grid, size_t lds, hipStream_t s, const Params& p) {
     switch (seg) {
         case 128: {
-            hipError_t e = hipFuncSetAttribute((const void*)bft_consensus_kernel<NEED_SEED, 128>,
+            hipError_t e = hipFuncSetAttribute((const void*)bft_consensus_kernel<NEED_SEED, MODE, 128>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 128>), grid, dim3(128), lds, s, p);
+            hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, MODE, 128>), grid, dim3(128), lds, s, p);
             break;
         }
         case 256: {
-            hipError_t e = hipFuncSetAttribute((const void*)bft_consensus_kernel<NEED_SEED, 256>,
+            hipError_t e = hipFuncSetAttribute((const void*)bft_consensus_kernel<NEED_SEED, MODE, 256>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 256>), grid, dim3(256), lds, s, p);
+            hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, MODE, 256>), grid, dim3(256), lds, s, p);
             break;
         }
-        case 4: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 4>), grid, dim3(64), lds, s, p); break;
-        case 8: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 8>), grid, dim3(64), lds, s, p); break;
-        case 16: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 16>), grid, dim3(64), lds, s, p); break;
-        case 32: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 32>), grid, dim3(64), lds, s, p); break;
-        default: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, 64>), grid, dim3(64), lds, s, p); break;
+        case 4: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, MODE, 4>), grid, dim3(64), lds, s, p); break;
+        case 8: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, MODE, 8>), grid, dim3(64), lds, s, p); break;
+        case 16: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, MODE, 16>), grid, dim3(64), lds, s, p); break;
+        case 32: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, MODE, 32>), grid, dim3(64), lds, s, p); break;
+        default: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, MODE, 64>), grid, dim3(64), lds, s, p); break;
     }
     return hipGetLastError();
 }
@@ -1103,6 +1103,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     uint32_t grid = (uint32_t)((n + per_block - 1) / per_block);
     size_t lds = bft::lds_bytes(h->seg, p.need_seed != 0);
     const bool fast = h->fast && p.fast && !p.mlog && h->d_save && !p.need_seed && !h->h_trace && h->seg == 64;
+    const bool ext = p.backlog_replay || p.mlog;       // the opt-in modes' kernel build (MODE_EXT)
     HIPCHECK(h, hipEventRecord(ev.c0, s));
     if (fast) {
         // FAST kernel over every instance, then the full kernel over the ones it handed over
@@ -1115,9 +1116,13 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         hipLaunchKernelGGL(bft::bft_consensus_resume_kernel, dim3(grid), dim3(64), lds, s, p);
         HIPCHECK(h, hipGetLastError());
     } else if (p.need_seed) {
-        HIPCHECK(h, bft::launch_consensus<true>(h->seg, dim3(grid), lds, s, p));
+        const hipError_t le = ext ? bft::launch_consensus<true, bft::MODE_EXT>(h->seg, dim3(grid), lds, s, p)
+                                  : bft::launch_consensus<true, bft::MODE_FULL>(h->seg, dim3(grid), lds, s, p);
+        HIPCHECK(h, le);
     } else {
-        HIPCHECK(h, bft::launch_consensus<false>(h->seg, dim3(grid), lds, s, p));
+        const hipError_t le = ext ? bft::launch_consensus<false, bft::MODE_EXT>(h->seg, dim3(grid), lds, s, p)
+                                  : bft::launch_consensus<false, bft::MODE_FULL>(h->seg, dim3(grid), lds, s, p);
+        HIPCHECK(h, le);
     }
     HIPCHECK(h, hipEventRecord(ev.c1, s));
     ev.has_hash = !p.need_seed;

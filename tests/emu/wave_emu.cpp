@@ -126,12 +126,14 @@ void run_sim() {
             return;
         }
     }
+    // as libbftsim: the opt-in modes (replay, crypto) run the MODE_EXT build of the kernel body
+    const bool ext = g->P->backlog_replay || g->P->mlog;
     if constexpr (S > 64) {
-        bft::Sim<EmuGroup<(int)(S / 64)>, NS, S> sim(*g->P, g->lds, g->wave);
-        sim.run();
+        if (ext) { bft::Sim<EmuGroup<(int)(S / 64)>, NS, S, bft::MODE_EXT> sim(*g->P, g->lds, g->wave); sim.run(); }
+        else { bft::Sim<EmuGroup<(int)(S / 64)>, NS, S> sim(*g->P, g->lds, g->wave); sim.run(); }
     } else {
-        bft::Sim<EmuWave, NS, S> sim(*g->P, g->lds, g->wave);
-        sim.run();
+        if (ext) { bft::Sim<EmuWave, NS, S, bft::MODE_EXT> sim(*g->P, g->lds, g->wave); sim.run(); }
+        else { bft::Sim<EmuWave, NS, S> sim(*g->P, g->lds, g->wave); sim.run(); }
     }
 }
 template <bool NS>
