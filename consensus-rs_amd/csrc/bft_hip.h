@@ -1,0 +1,146 @@
+// bft_hip.h — gfx950 wave / workgroup collectives of the consensus kernels and the launchers of the
+// kernel translation units (kern_*.hip), which libbftsim's host code (bftsim.hip) calls. The kernels
+// are split over several translation units so that they compile in parallel.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/bftsim.h"
+#include "bft_common.h"
+#include "bft_wave.h"
+
+namespace bft {
+
+// ------------------------------------------------------------------------------ wave ops (gfx950)
+struct WaveHip {
+    __device__ void init(uint8_t*) {}
+    __device__ static uint32_t lane() { return __lane_id(); }
+    __device__ static uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+    __device__ static uint32_t shfl_xor(uint32_t v, int m) { return (uint32_t)__shfl_xor((int)v, m, 64); }
+    __device__ static uint32_t shfl(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src, 64); }
+    __device__ static uint32_t readlane(uint32_t v, uint32_t l) {      // l wave-uniform
+        return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_amdgcn_readfirstlane((int)l));
+    }
+    // a wave-uniform value held in a VGPR → SGPR (frees the VGPR for the lane state)
+    __device__ static uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+    __device__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
+    __device__ static void sync() {
+        // Intra-wave LDS hand-off: the LDS executes one wave's DS instructions in program order,
+        // so a later ds_read of any lane sees every earlier ds_write of the wave. Only the
+        // compiler must not move memory operations across this point (no s_waitcnt needed).
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+    }
+    __device__ static uint32_t gload(const uint32_t* p) {
+        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ static void gstore(uint32_t* p, uint32_t v) {
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // 16-byte aligned row store (global_store_dwordx4; L1 is write-through, readers use L2 loads)
+    __device__ static void gstore4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+        *(uint4*)p = make_uint4(a, b, c, d);
+    }
+    __device__ static void lds_add(uint32_t* p, uint32_t v) { atomicAdd(p, v); }
+    __device__ static void gadd64(uint64_t* p, uint64_t v) { atomicAdd((unsigned long long*)p, (unsigned long long)v); }
+};
+
+// ------------------------------------------------------------- workgroup ops (S = 64*NW lanes)
+// One instance per workgroup of NW waves. A collective = per-wave partial (ballot / butterfly)
+// written to an LDS slot by each wave's lane 0, one s_barrier, every lane combines the NW
+// partials. The slots alternate between two parities: a slot is rewritten only after the next
+// collective's barrier, which every lane reaches after finishing its reads of this one.
+template <int NW>
+struct GroupHip {
+    uint64_t* slot;       // LDS: [2 parities][4 words]
+    uint32_t par;
+    __device__ void init(uint8_t* p) { slot = (uint64_t*)p; par = 0; }
+    __device__ uint32_t lane() const { return threadIdx.x; }
+    __device__ uint64_t* cur() const { return slot + par * 4u; }
+    __device__ Bits<NW> ballot(bool p) {
+        uint64_t b = __ballot(p);
+        uint64_t* s = cur();
+        if (__lane_id() == 0) s[threadIdx.x >> 6] = b;
+        __syncthreads();
+        Bits<NW> r;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) r.w[k] = s[k];
+        par ^= 1u;
+        return r;
+    }
+    __device__ uint32_t bcast(uint32_t v, uint32_t j) {     // value of lane j (j uniform)
+        uint64_t* s = cur();
+        if (threadIdx.x == j) s[0] = v;
+        __syncthreads();
+        uint32_t r = (uint32_t)s[0];
+        par ^= 1u;
+        return r;
+    }
+    __device__ uint32_t grp_max(uint32_t v) {
+        for (int m = 1; m < 64; m <<= 1) { uint32_t o = (uint32_t)__shfl_xor((int)v, m, 64); v = v > o ? v : o; }
+        uint64_t* s = cur();
+        if (__lane_id() == 0) s[threadIdx.x >> 6] = v;
+        __syncthreads();
+        uint32_t r = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) r = (uint32_t)s[k] > r ? (uint32_t)s[k] : r;
+        par ^= 1u;
+        return r;
+    }
+    __device__ uint32_t grp_or(uint32_t v) {
+        for (int m = 1; m < 64; m <<= 1) v |= (uint32_t)__shfl_xor((int)v, m, 64);
+        uint64_t* s = cur();
+        if (__lane_id() == 0) s[threadIdx.x >> 6] = v;
+        __syncthreads();
+        uint32_t r = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) r |= (uint32_t)s[k];
+        par ^= 1u;
+        return r;
+    }
+    __device__ uint64_t grp_sum64(uint32_t v32) {
+        uint64_t v = v32;
+        for (int m = 1; m < 64; m <<= 1) {
+            uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+            v += (uint64_t)lo | ((uint64_t)hi << 32);
+        }
+        uint64_t* s = cur();
+        if (__lane_id() == 0) s[threadIdx.x >> 6] = v;
+        __syncthreads();
+        uint64_t r = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) r += s[k];
+        par ^= 1u;
+        return r;
+    }
+    __device__ void sync() { __syncthreads(); par ^= 1u; }
+    __device__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
+    __device__ static uint32_t gload(const uint32_t* p) {
+        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ static void gstore(uint32_t* p, uint32_t v) {
+        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // 16-byte aligned row store (global_store_dwordx4; L1 is write-through, readers use L2 loads)
+    __device__ static void gstore4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+        *(uint4*)p = make_uint4(a, b, c, d);
+    }
+    __device__ static void lds_add(uint32_t* p, uint32_t v) { atomicAdd(p, v); }
+    __device__ static void gadd64(uint64_t* p, uint64_t v) { atomicAdd((unsigned long long*)p, (unsigned long long)v); }
+};
+
+// launchers (each in its own translation unit)
+// general kernel, NEED_SEED x MODE_FULL / MODE_EXT builds (kern_general.hip, compiled four times)
+hipError_t launch_general_0_0(uint32_t seg, dim3 grid, size_t lds, hipStream_t s, const Params& p);
+hipError_t launch_general_0_1(uint32_t seg, dim3 grid, size_t lds, hipStream_t s, const Params& p);
+hipError_t launch_general_1_0(uint32_t seg, dim3 grid, size_t lds, hipStream_t s, const Params& p);
+hipError_t launch_general_1_1(uint32_t seg, dim3 grid, size_t lds, hipStream_t s, const Params& p);
+inline hipError_t launch_general(bool need_seed, bool ext, uint32_t seg, dim3 grid, size_t lds, hipStream_t s,
+                                 const Params& p) {
+    if (need_seed) return ext ? launch_general_1_1(seg, grid, lds, s, p) : launch_general_1_0(seg, grid, lds, s, p);
+    return ext ? launch_general_0_1(seg, grid, lds, s, p) : launch_general_0_0(seg, grid, lds, s, p);
+}
+hipError_t launch_fast(dim3 grid, hipStream_t s, const Params& p);               // kern_fast.hip
+hipError_t launch_hash(dim3 grid, hipStream_t s, const Params& p);               // kern_fast.hip
+hipError_t launch_resume(dim3 grid, size_t lds, hipStream_t s, const Params& p);  // kern_resume.hip
+
+}  // namespace bft

@@ -24,291 +24,12 @@
 #include <utility>
 #include <vector>
 
-#include "../../include/bftsim.h"
-#include "bft_common.h"
-#include "bft_wave.h"
+#include "bft_hip.h"
 #include "bft_fast64.h"
 #include "bft_crypto.h"
 
 namespace bft {
 
-// ------------------------------------------------------------------------------ wave ops (gfx950)
-struct WaveHip {
-    __device__ void init(uint8_t*) {}
-    __device__ static uint32_t lane() { return __lane_id(); }
-    __device__ static uint64_t ballot(bool p) { return __ballot(p); }
-    __device__ static uint32_t shfl_xor(uint32_t v, int m) { return (uint32_t)__shfl_xor((int)v, m, 64); }
-    __device__ static uint32_t shfl(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src, 64); }
-    __device__ static uint32_t readlane(uint32_t v, uint32_t l) {      // l wave-uniform
-        return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_amdgcn_readfirstlane((int)l));
-    }
-    // a wave-uniform value held in a VGPR → SGPR (frees the VGPR for the lane state)
-    __device__ static uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-    __device__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
-    __device__ static void sync() {
-        // Intra-wave LDS hand-off: the LDS executes one wave's DS instructions in program order,
-        // so a later ds_read of any lane sees every earlier ds_write of the wave. Only the
-        // compiler must not move memory operations across this point (no s_waitcnt needed).
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-    }
-    __device__ static uint32_t gload(const uint32_t* p) {
-        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __device__ static void gstore(uint32_t* p, uint32_t v) {
-        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // 16-byte aligned row store (global_store_dwordx4; L1 is write-through, readers use L2 loads)
-    __device__ static void gstore4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-        *(uint4*)p = make_uint4(a, b, c, d);
-    }
-    __device__ static void lds_add(uint32_t* p, uint32_t v) { atomicAdd(p, v); }
-    __device__ static void gadd64(uint64_t* p, uint64_t v) { atomicAdd((unsigned long long*)p, (unsigned long long)v); }
-};
-
-// ------------------------------------------------------------- workgroup ops (S = 64*NW lanes)
-// One instance per workgroup of NW waves. A collective = per-wave partial (ballot / butterfly)
-// written to an LDS slot by each wave's lane 0, one s_barrier, every lane combines the NW
-// partials. The slots alternate between two parities: a slot is rewritten only after the next
-// collective's barrier, which every lane reaches after finishing its reads of this one.
-template <int NW>
-struct GroupHip {
-    uint64_t* slot;       // LDS: [2 parities][4 words]
-    uint32_t par;
-    __device__ void init(uint8_t* p) { slot = (uint64_t*)p; par = 0; }
-    __device__ uint32_t lane() const { return threadIdx.x; }
-    __device__ uint64_t* cur() const { return slot + par * 4u; }
-    __device__ Bits<NW> ballot(bool p) {
-        uint64_t b = __ballot(p);
-        uint64_t* s = cur();
-        if (__lane_id() == 0) s[threadIdx.x >> 6] = b;
-        __syncthreads();
-        Bits<NW> r;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) r.w[k] = s[k];
-        par ^= 1u;
-        return r;
-    }
-    __device__ uint32_t bcast(uint32_t v, uint32_t j) {     // value of lane j (j uniform)
-        uint64_t* s = cur();
-        if (threadIdx.x == j) s[0] = v;
-        __syncthreads();
-        uint32_t r = (uint32_t)s[0];
-        par ^= 1u;
-        return r;
-    }
-    __device__ uint32_t grp_max(uint32_t v) {
-        for (int m = 1; m < 64; m <<= 1) { uint32_t o = (uint32_t)__shfl_xor((int)v, m, 64); v = v > o ? v : o; }
-        uint64_t* s = cur();
-        if (__lane_id() == 0) s[threadIdx.x >> 6] = v;
-        __syncthreads();
-        uint32_t r = 0;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) r = (uint32_t)s[k] > r ? (uint32_t)s[k] : r;
-        par ^= 1u;
-        return r;
-    }
-    __device__ uint32_t grp_or(uint32_t v) {
-        for (int m = 1; m < 64; m <<= 1) v |= (uint32_t)__shfl_xor((int)v, m, 64);
-        uint64_t* s = cur();
-        if (__lane_id() == 0) s[threadIdx.x >> 6] = v;
-        __syncthreads();
-        uint32_t r = 0;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) r |= (uint32_t)s[k];
-        par ^= 1u;
-        return r;
-    }
-    __device__ uint64_t grp_sum64(uint32_t v32) {
-        uint64_t v = v32;
-        for (int m = 1; m < 64; m <<= 1) {
-            uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
-            v += (uint64_t)lo | ((uint64_t)hi << 32);
-        }
-        uint64_t* s = cur();
-        if (__lane_id() == 0) s[threadIdx.x >> 6] = v;
-        __syncthreads();
-        uint64_t r = 0;
-#pragma unroll
-        for (int k = 0; k < NW; ++k) r += s[k];
-        par ^= 1u;
-        return r;
-    }
-    __device__ void sync() { __syncthreads(); par ^= 1u; }
-    __device__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
-    __device__ static uint32_t gload(const uint32_t* p) {
-        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __device__ static void gstore(uint32_t* p, uint32_t v) {
-        __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // 16-byte aligned row store (global_store_dwordx4; L1 is write-through, readers use L2 loads)
-    __device__ static void gstore4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-        *(uint4*)p = make_uint4(a, b, c, d);
-    }
-    __device__ static void lds_add(uint32_t* p, uint32_t v) { atomicAdd(p, v); }
-    __device__ static void gadd64(uint64_t* p, uint64_t v) { atomicAdd((unsigned long long*)p, (unsigned long long)v); }
-};
-
-template <bool NEED_SEED, int MODE, uint32_t S>
-#ifndef BFT_WAVES_PER_SIMD
-#define BFT_WAVES_PER_SIMD 3   // register budget of the one-wave kernels (LDS allows ~2.75 per SIMD)
-#endif
-__global__ __launch_bounds__(S > 64 ? S : 64, S > 64 ? 1 : BFT_WAVES_PER_SIMD) void bft_consensus_kernel(Params p) {
-    extern __shared__ uint8_t lds[];
-    if constexpr (S > 64) {
-        Sim<GroupHip<(int)(S / 64)>, NEED_SEED, S, MODE> sim(p, lds, blockIdx.x);
-        sim.run();
-    } else {
-        Sim<WaveHip, NEED_SEED, S, MODE> sim(p, lds, blockIdx.x);
-        sim.run();
-    }
-}
-
-// FAST kernel (N = 64, big-endian seeds): the closed-form phases only (bft_fast64.h); instances
-// needing the general path are saved for the resume kernel
-#ifndef BFT_FAST_WAVES_PER_SIMD
-#define BFT_FAST_WAVES_PER_SIMD 6   // measured best of 4..8 (profiles/r02: 4 → 3.86e8, 5 → 3.97e8, 6 → 4.17e8, 7 → 3.69e8)
-#endif
-__global__ __launch_bounds__(64, BFT_FAST_WAVES_PER_SIMD) void bft_consensus_fast_kernel(Params p) {
-    extern __shared__ uint8_t lds[];
-#ifndef BFT_CONSENSUS_PRIO
-#define BFT_CONSENSUS_PRIO 2
-#endif
-    // win issue arbitration against the hash waves of the previous launch (the hash pass stretches into
-    // the issue gaps and still finishes within the step)
-    __builtin_amdgcn_s_setprio(BFT_CONSENSUS_PRIO);
-    Fast64<WaveHip> sim(p, lds, blockIdx.x);
-    sim.run();
-}
-// the full kernel over the instances the FAST kernel handed over, from their saved phase
-__global__ __launch_bounds__(64, BFT_WAVES_PER_SIMD) void bft_consensus_resume_kernel(Params p) {
-    extern __shared__ uint8_t lds[];
-    Sim<WaveHip, false, 64, MODE_RESUME> sim(p, lds, blockIdx.x);
-    sim.run();
-}
-
-template <bool NEED_SEED, int MODE>
-static hipError_t launch_consensus(uint32_t seg, dim3 grid, size_t lds, hipStream_t s, const Params& p) {
-    switch (seg) {
-        case 128: {
-            hipError_t e = hipFuncSetAttribute((const void*)bft_consensus_kernel<NEED_SEED, MODE, 128>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-            hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, MODE, 128>), grid, dim3(128), lds, s, p);
-            break;
-        }
-        case 256: {
-            hipError_t e = hipFuncSetAttribute((const void*)bft_consensus_kernel<NEED_SEED, MODE, 256>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-            hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, MODE, 256>), grid, dim3(256), lds, s, p);
-            break;
-        }
-        case 4: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, MODE, 4>), grid, dim3(64), lds, s, p); break;
-        case 8: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, MODE, 8>), grid, dim3(64), lds, s, p); break;
-        case 16: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, MODE, 16>), grid, dim3(64), lds, s, p); break;
-        case 32: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, MODE, 32>), grid, dim3(64), lds, s, p); break;
-        default: hipLaunchKernelGGL((bft_consensus_kernel<NEED_SEED, MODE, 64>), grid, dim3(64), lds, s, p); break;
-    }
-    return hipGetLastError();
-}
-
-// one lane PAIR per instance: the even lane holds the low 32-bit half of every
-// Keccak state word, the odd lane the high half. A 64-bit rotation is one v_alignbit_b32 of this
-// lane's half and the partner's (exchanged with one DPP quad_perm swap); theta parities, chi and iota
-// are half-local. Per lane and round ~125 VALU instead of ~205 for a whole state in one lane, and
-// twice the waves for the chip (the chains are sequential in height, so per-chain issue latency,
-// not throughput, bounds this kernel).
-#if defined(__HIP_DEVICE_COMPILE__)
-__device__ inline uint32_t pair_swap(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-}
-template <int N>
-__device__ inline uint32_t rotl_pair(uint32_t mine, uint32_t other) {
-    if constexpr (N == 0) return mine;
-    else if constexpr (N == 32) return other;
-    else if constexpr (N < 32) return __builtin_amdgcn_alignbit(mine, other, 32 - N);
-    else return __builtin_amdgcn_alignbit(other, mine, 64 - N);
-}
-__constant__ uint32_t KECCAK_RC_PAIR[2][24] = {
-    {0x00000001u, 0x00008082u, 0x0000808Au, 0x80008000u, 0x0000808Bu, 0x80000001u, 0x80008081u, 0x00008009u,
-     0x0000008Au, 0x00000088u, 0x80008009u, 0x8000000Au, 0x8000808Bu, 0x0000008Bu, 0x00008089u, 0x00008003u,
-     0x00008002u, 0x00000080u, 0x0000800Au, 0x8000000Au, 0x80008081u, 0x00008080u, 0x80000001u, 0x80008008u},
-    {0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0u, 0u, 0u, 0x80000000u,
-     0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u}};
-
-__device__ inline void keccak_f1600_pair(uint32_t X[25], uint32_t odd) {
-#pragma unroll 1
-    for (int rnd = 0; rnd < 24; ++rnd) {
-        uint32_t c[5], cs[5], d[5], t[25], b[25];
-#pragma unroll
-        for (int x = 0; x < 5; ++x) c[x] = xor3_32(xor3_32(X[x], X[x + 5], X[x + 10]), X[x + 15], X[x + 20]);
-#pragma unroll
-        for (int x = 0; x < 5; ++x) cs[x] = pair_swap(c[x]);
-#pragma unroll
-        for (int x = 0; x < 5; ++x) d[x] = c[(x + 4) % 5] ^ rotl_pair<1>(c[(x + 1) % 5], cs[(x + 1) % 5]);
-#pragma unroll
-        for (int i = 0; i < 25; ++i) t[i] = X[i] ^ d[i % 5];
-        // rho + pi: b[y + 5*((2x+3y)%5)] = rotl(t[x+5y], r[x+5y])
-#define BFT_RHO2(i, n, j) b[j] = rotl_pair<n>(t[i], (n) ? pair_swap(t[i]) : 0u);
-        BFT_RHO2(0, 0, 0) BFT_RHO2(1, 1, 10) BFT_RHO2(2, 62, 20) BFT_RHO2(3, 28, 5) BFT_RHO2(4, 27, 15)
-        BFT_RHO2(5, 36, 16) BFT_RHO2(6, 44, 1) BFT_RHO2(7, 6, 11) BFT_RHO2(8, 55, 21) BFT_RHO2(9, 20, 6)
-        BFT_RHO2(10, 3, 7) BFT_RHO2(11, 10, 17) BFT_RHO2(12, 43, 2) BFT_RHO2(13, 25, 12) BFT_RHO2(14, 39, 22)
-        BFT_RHO2(15, 41, 23) BFT_RHO2(16, 45, 8) BFT_RHO2(17, 15, 18) BFT_RHO2(18, 21, 3) BFT_RHO2(19, 8, 13)
-        BFT_RHO2(20, 18, 14) BFT_RHO2(21, 2, 24) BFT_RHO2(22, 61, 9) BFT_RHO2(23, 56, 19) BFT_RHO2(24, 14, 4)
-#undef BFT_RHO2
-#pragma unroll
-        for (int y = 0; y < 5; ++y)
-#pragma unroll
-            for (int x = 0; x < 5; ++x)
-                X[5 * y + x] = b[5 * y + x] ^ (~b[5 * y + (x + 1) % 5] & b[5 * y + (x + 2) % 5]);
-        X[0] ^= KECCAK_RC_PAIR[odd][rnd];
-    }
-}
-
-#endif
-
-__global__ __launch_bounds__(64) void bft_hash_pair_kernel(Params p) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    __shared__ __attribute__((aligned(16))) uint64_t bufs[64 * HDR_WORDS];
-    const uint32_t odd = threadIdx.x & 1u;
-    const uint32_t il = blockIdx.x * 32u + (threadIdx.x >> 1);
-    if (il >= p.n_instances) return;                  // both lanes of a pair leave together
-    const uint32_t inst = p.first_instance + il;
-    const uint32_t ch = p.committed_height[il];
-    uint32_t prev[8];
-    for (int i = 0; i < 8; ++i)
-        prev[i] = (uint32_t)p.genesis_hash[4 * i] | ((uint32_t)p.genesis_hash[4 * i + 1] << 8) |
-                  ((uint32_t)p.genesis_hash[4 * i + 2] << 16) | ((uint32_t)p.genesis_hash[4 * i + 3] << 24);
-    uint64_t* wb = bufs + threadIdx.x * HDR_WORDS;     // each lane encodes its own copy (no exchange)
-    const uint32_t* wh = (const uint32_t*)wb + odd;   // this lane's halves of the message words
-    for (uint32_t x = 1; x <= ch; ++x) {
-        const uint32_t* row = p.rec + ((uint64_t)il * p.rows + x) * 4;
-        const uint32_t w1 = row[1];
-        const uint32_t prop = w1 & 0xffffu, var = (w1 >> 16) & 1u, T = row[2];
-        const uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)T + 1ull);
-        const uint32_t nb = header_words(wb, prev, p.addresses + 20u * prop, p.seed, inst, x, prop, var, time);
-        uint32_t X[25];
-#pragma unroll
-        for (int i = 0; i < 25; ++i) X[i] = 0;
-#pragma unroll 1
-        for (uint32_t blk = 0; blk < nb; ++blk) {
-#pragma unroll
-            for (int i = 0; i < 17; ++i) X[i] ^= wh[2 * (17u * blk + i)];
-            keccak_f1600_pair(X, odd);
-        }
-        uint32_t* dst = (uint32_t*)(p.hash + ((uint64_t)il * p.rows + x) * 32);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t o = pair_swap(X[i]);
-            dst[2 * i + odd] = X[i];
-            prev[2 * i] = odd ? o : X[i];
-            prev[2 * i + 1] = odd ? X[i] : o;
-        }
-    }
-#endif
-}
 
 // ledger export (core/ledger.rs:193-245): the Header bytes of every committed height, thread per
 // (instance, height), parent hash from the hash table; into 8-aligned BFTSIM_HEADER_SLOT-byte slots
@@ -1111,18 +832,10 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         p.save = h->d_save;
         p.save_stride = n * 64;
         HIPCHECK(h, hipMemsetAsync(h->d_resume, 0, n * 4, s));
-        hipLaunchKernelGGL(bft::bft_consensus_fast_kernel, dim3(grid), dim3(64), bft::lds_bytes_fast64(), s, p);
-        HIPCHECK(h, hipGetLastError());
-        hipLaunchKernelGGL(bft::bft_consensus_resume_kernel, dim3(grid), dim3(64), lds, s, p);
-        HIPCHECK(h, hipGetLastError());
-    } else if (p.need_seed) {
-        const hipError_t le = ext ? bft::launch_consensus<true, bft::MODE_EXT>(h->seg, dim3(grid), lds, s, p)
-                                  : bft::launch_consensus<true, bft::MODE_FULL>(h->seg, dim3(grid), lds, s, p);
-        HIPCHECK(h, le);
+        HIPCHECK(h, bft::launch_fast(dim3(grid), s, p));
+        HIPCHECK(h, bft::launch_resume(dim3(grid), lds, s, p));
     } else {
-        const hipError_t le = ext ? bft::launch_consensus<false, bft::MODE_EXT>(h->seg, dim3(grid), lds, s, p)
-                                  : bft::launch_consensus<false, bft::MODE_FULL>(h->seg, dim3(grid), lds, s, p);
-        HIPCHECK(h, le);
+        HIPCHECK(h, bft::launch_general(p.need_seed != 0, ext, h->seg, dim3(grid), lds, s, p));
     }
     HIPCHECK(h, hipEventRecord(ev.c1, s));
     ev.has_hash = !p.need_seed;
@@ -1131,8 +844,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         hipStream_t t = pipe ? h->sets[h->cur_set].hs : s;
         if (pipe) HIPCHECK(h, hipStreamWaitEvent(t, ev.c1, 0));
         HIPCHECK(h, hipEventRecord(ev.h0, t));
-        hipLaunchKernelGGL(bft::bft_hash_pair_kernel, dim3((uint32_t)((n + 31) / 32)), dim3(64), 0, t, p);
-        HIPCHECK(h, hipGetLastError());
+        HIPCHECK(h, bft::launch_hash(dim3((uint32_t)((n + 31) / 32)), t, p));
         HIPCHECK(h, hipEventRecord(ev.h1, t));
         if (pipe) {
             HIPCHECK(h, hipEventRecord(h->sets[h->cur_set].done, t));

@@ -1,0 +1,129 @@
+// kern_fast.hip — the N = 64 FAST consensus kernel (bft_fast64.h) and the block-hash pass
+// (bft_hash_pair_kernel) of the benchmark workload.
+#include "bft_hip.h"
+#include "bft_fast64.h"
+
+namespace bft {
+
+// FAST kernel (N = 64, big-endian seeds): the closed-form phases only (bft_fast64.h); instances
+// needing the general path are saved for the resume kernel
+#ifndef BFT_FAST_WAVES_PER_SIMD
+#define BFT_FAST_WAVES_PER_SIMD 6   // measured best of 4..8 (profiles/r02: 4 → 3.86e8, 5 → 3.97e8, 6 → 4.17e8, 7 → 3.69e8)
+#endif
+__global__ __launch_bounds__(64, BFT_FAST_WAVES_PER_SIMD) void bft_consensus_fast_kernel(Params p) {
+    extern __shared__ uint8_t lds[];
+#ifndef BFT_CONSENSUS_PRIO
+#define BFT_CONSENSUS_PRIO 2
+#endif
+    // win issue arbitration against the hash waves of the previous launch (the hash pass stretches into
+    // the issue gaps and still finishes within the step)
+    __builtin_amdgcn_s_setprio(BFT_CONSENSUS_PRIO);
+    Fast64<WaveHip> sim(p, lds, blockIdx.x);
+    sim.run();
+}
+hipError_t launch_fast(dim3 grid, hipStream_t s, const Params& p) {
+    hipLaunchKernelGGL(bft_consensus_fast_kernel, grid, dim3(64), lds_bytes_fast64(), s, p);
+    return hipGetLastError();
+}
+
+// one lane PAIR per instance: the even lane holds the low 32-bit half of every
+// Keccak state word, the odd lane the high half. A 64-bit rotation is one v_alignbit_b32 of this
+// lane's half and the partner's (exchanged with one DPP quad_perm swap); theta parities, chi and iota
+// are half-local. Per lane and round ~125 VALU instead of ~205 for a whole state in one lane, and
+// twice the waves for the chip (the chains are sequential in height, so per-chain issue latency,
+// not throughput, bounds this kernel).
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ inline uint32_t pair_swap(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+}
+template <int N>
+__device__ inline uint32_t rotl_pair(uint32_t mine, uint32_t other) {
+    if constexpr (N == 0) return mine;
+    else if constexpr (N == 32) return other;
+    else if constexpr (N < 32) return __builtin_amdgcn_alignbit(mine, other, 32 - N);
+    else return __builtin_amdgcn_alignbit(other, mine, 64 - N);
+}
+__constant__ uint32_t KECCAK_RC_PAIR[2][24] = {
+    {0x00000001u, 0x00008082u, 0x0000808Au, 0x80008000u, 0x0000808Bu, 0x80000001u, 0x80008081u, 0x00008009u,
+     0x0000008Au, 0x00000088u, 0x80008009u, 0x8000000Au, 0x8000808Bu, 0x0000008Bu, 0x00008089u, 0x00008003u,
+     0x00008002u, 0x00000080u, 0x0000800Au, 0x8000000Au, 0x80008081u, 0x00008080u, 0x80000001u, 0x80008008u},
+    {0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0u, 0u, 0u, 0x80000000u,
+     0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u}};
+
+__device__ inline void keccak_f1600_pair(uint32_t X[25], uint32_t odd) {
+#pragma unroll 1
+    for (int rnd = 0; rnd < 24; ++rnd) {
+        uint32_t c[5], cs[5], d[5], t[25], b[25];
+#pragma unroll
+        for (int x = 0; x < 5; ++x) c[x] = xor3_32(xor3_32(X[x], X[x + 5], X[x + 10]), X[x + 15], X[x + 20]);
+#pragma unroll
+        for (int x = 0; x < 5; ++x) cs[x] = pair_swap(c[x]);
+#pragma unroll
+        for (int x = 0; x < 5; ++x) d[x] = c[(x + 4) % 5] ^ rotl_pair<1>(c[(x + 1) % 5], cs[(x + 1) % 5]);
+#pragma unroll
+        for (int i = 0; i < 25; ++i) t[i] = X[i] ^ d[i % 5];
+        // rho + pi: b[y + 5*((2x+3y)%5)] = rotl(t[x+5y], r[x+5y])
+#define BFT_RHO2(i, n, j) b[j] = rotl_pair<n>(t[i], (n) ? pair_swap(t[i]) : 0u);
+        BFT_RHO2(0, 0, 0) BFT_RHO2(1, 1, 10) BFT_RHO2(2, 62, 20) BFT_RHO2(3, 28, 5) BFT_RHO2(4, 27, 15)
+        BFT_RHO2(5, 36, 16) BFT_RHO2(6, 44, 1) BFT_RHO2(7, 6, 11) BFT_RHO2(8, 55, 21) BFT_RHO2(9, 20, 6)
+        BFT_RHO2(10, 3, 7) BFT_RHO2(11, 10, 17) BFT_RHO2(12, 43, 2) BFT_RHO2(13, 25, 12) BFT_RHO2(14, 39, 22)
+        BFT_RHO2(15, 41, 23) BFT_RHO2(16, 45, 8) BFT_RHO2(17, 15, 18) BFT_RHO2(18, 21, 3) BFT_RHO2(19, 8, 13)
+        BFT_RHO2(20, 18, 14) BFT_RHO2(21, 2, 24) BFT_RHO2(22, 61, 9) BFT_RHO2(23, 56, 19) BFT_RHO2(24, 14, 4)
+#undef BFT_RHO2
+#pragma unroll
+        for (int y = 0; y < 5; ++y)
+#pragma unroll
+            for (int x = 0; x < 5; ++x)
+                X[5 * y + x] = b[5 * y + x] ^ (~b[5 * y + (x + 1) % 5] & b[5 * y + (x + 2) % 5]);
+        X[0] ^= KECCAK_RC_PAIR[odd][rnd];
+    }
+}
+
+#endif
+
+__global__ __launch_bounds__(64) void bft_hash_pair_kernel(Params p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __shared__ __attribute__((aligned(16))) uint64_t bufs[64 * HDR_WORDS];
+    const uint32_t odd = threadIdx.x & 1u;
+    const uint32_t il = blockIdx.x * 32u + (threadIdx.x >> 1);
+    if (il >= p.n_instances) return;                  // both lanes of a pair leave together
+    const uint32_t inst = p.first_instance + il;
+    const uint32_t ch = p.committed_height[il];
+    uint32_t prev[8];
+    for (int i = 0; i < 8; ++i)
+        prev[i] = (uint32_t)p.genesis_hash[4 * i] | ((uint32_t)p.genesis_hash[4 * i + 1] << 8) |
+                  ((uint32_t)p.genesis_hash[4 * i + 2] << 16) | ((uint32_t)p.genesis_hash[4 * i + 3] << 24);
+    uint64_t* wb = bufs + threadIdx.x * HDR_WORDS;     // each lane encodes its own copy (no exchange)
+    const uint32_t* wh = (const uint32_t*)wb + odd;   // this lane's halves of the message words
+    for (uint32_t x = 1; x <= ch; ++x) {
+        const uint32_t* row = p.rec + ((uint64_t)il * p.rows + x) * 4;
+        const uint32_t w1 = row[1];
+        const uint32_t prop = w1 & 0xffffu, var = (w1 >> 16) & 1u, T = row[2];
+        const uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)T + 1ull);
+        const uint32_t nb = header_words(wb, prev, p.addresses + 20u * prop, p.seed, inst, x, prop, var, time);
+        uint32_t X[25];
+#pragma unroll
+        for (int i = 0; i < 25; ++i) X[i] = 0;
+#pragma unroll 1
+        for (uint32_t blk = 0; blk < nb; ++blk) {
+#pragma unroll
+            for (int i = 0; i < 17; ++i) X[i] ^= wh[2 * (17u * blk + i)];
+            keccak_f1600_pair(X, odd);
+        }
+        uint32_t* dst = (uint32_t*)(p.hash + ((uint64_t)il * p.rows + x) * 32);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t o = pair_swap(X[i]);
+            dst[2 * i + odd] = X[i];
+            prev[2 * i] = odd ? o : X[i];
+            prev[2 * i + 1] = odd ? X[i] : o;
+        }
+    }
+#endif
+}
+hipError_t launch_hash(dim3 grid, hipStream_t s, const Params& p) {
+    hipLaunchKernelGGL(bft_hash_pair_kernel, grid, dim3(64), 0, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace bft
