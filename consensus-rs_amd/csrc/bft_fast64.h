@@ -45,7 +45,8 @@ struct Fast64 {
     static constexpr uint32_t N = 64, Q = 42;   // floor(2N/3) (validator.rs:149-154)
     // lane flag bits
     static constexpr uint32_t L_ST = 7u, L_WAIT = 8u, L_LOCK = 16u, L_BYZ = 32u, L_RUN = 64u, L_DEAD = 128u,
-                              L_PENDV = 256u, L_CMT = 512u, L_PROP = 1024u;   // L_PROP: proposer is set (= 0)
+                              L_PENDV = 256u, L_CMT = 512u, L_PROP = 1024u,   // L_PROP: proposer is set (= 0)
+                              L_OBX = 2048u;   // FLAG_OUTBOX of this lane (a second message of a kind in one phase)
     enum : uint32_t { P_GENERAL = 0, P_BLK = 1, P_PC = 2, P_PP = 3, P_NONE = 4 };
 
     const Params& P;
@@ -112,6 +113,7 @@ struct Fast64 {
         return (uint64_t)lo | ((uint64_t)hi << 32);
     }
     BFT_FN uint32_t* lane_p(uint32_t w) const { return (uint32_t*)(lds + F64Layout::LANE_OFF) + w * 64u + me; }
+    BFT_FN uint32_t lane_flags() const { return *lane_p(F64Layout::W_LFL) | (has(L_OBX) ? FLAG_OUTBOX : 0u); }
     BFT_FN uint32_t proposer() const { return has(L_PROP) ? 0u : 0xffffffffu; }
     BFT_FN uint32_t st() const { return fl & L_ST; }
     BFT_FN void set_st(uint32_t s) { fl = (fl & ~L_ST) | s; }
@@ -124,9 +126,12 @@ struct Fast64 {
     }
     BFT_FN static uint64_t rotr(uint64_t m, uint32_t off) { return off ? ((m >> off) | (m << (64u - off))) : m; }
     BFT_FN static uint64_t low(uint32_t k) { return k >= 64u ? ~0ull : ((1ull << k) - 1ull); }
+    // blk_eq without short-circuit branches
+    BFT_FN static bool beq(uint64_t a, uint64_t b) { return ((a & b & BLK_VALID) != 0) & (((a ^ b) & BLK_ID_MASK) == 0); }
     BFT_FN static uint32_t popc(uint64_t m) { return (uint32_t)__builtin_popcountll(m); }
     BFT_FN static uint32_t hibit(uint64_t m) { return m ? 63u - (uint32_t)__builtin_clzll(m) : 0u; }
     BFT_FN static uint32_t ctz64(uint64_t m) { return m ? (uint32_t)__builtin_ctzll(m) : 64u; }
+    BFT_FN static uint32_t ff1(uint64_t m) { return (uint32_t)__builtin_ctzll(m | (1ull << 63)); }  // 63 for 0
 
     // ------------------------------------------------------------------ outbound cache (backend.rs:141-148)
     // per kind the last subject sent: {height, 32-bit block id}; the round is always 0 here
@@ -149,17 +154,21 @@ struct Fast64 {
     // the hot paths have no divergent regions that write registers (LLVM's structurizer copies every
     // live value at each nested divergent branch). Only memory stores sit under divergent `if`s, and
     // the rare paths (round changes, sync requests, old Preprepares) run behind uniform ballots.
+    // Lane predicates are combined with the non-short-circuit `&` / `|`: `&&` / `||` on per-lane values
+    // become nested exec-mask branches (three SALU instructions each), and the one scalar unit of a CU
+    // is what bounds this kernel (profiles/r02: +100 SALU per phase cost 2.1x what +100 VALU did).
 
     // a message of `kind` (view (vh, 0), digest d) through the outbound cache into the outbox
     BFT_FN bool send_kind(bool c, uint32_t kind, uint32_t vh, uint64_t d, uint32_t flag, uint32_t wflag) {
         const uint32_t d32 = blk_d32(d);
         uint32_t* cp = cache_p(2u * kind);
         const uint32_t ch = cp[0], cd = cp[64];
-        const bool upd = c && !(cd != 0 && ch == vh && cd == d32);   // cache miss: the message goes out
-        if (upd) { cp[0] = vh; cp[64] = d32; }
-        const bool dup = upd && (nxf & flag) != 0;                     // a second one of its kind this phase
-        if (dup) *lane_p(F64Layout::W_LFL) |= FLAG_OUTBOX;
-        const bool put = upd && !dup;
+        const bool upd = c & !((cd != 0) & (ch == vh) & (cd == d32));   // cache miss: the message goes out
+        cp[0] = upd ? vh : ch;                                         // unconditional (no exec-mask branch)
+        cp[64] = upd ? d32 : cd;
+        const bool dup = upd & ((nxf & flag) != 0);                    // a second one of its kind this phase
+        fl |= dup ? L_OBX : 0u;
+        const bool put = upd & !dup;
         nxf |= put ? (flag | (has(L_BYZ) ? wflag : 0u)) : 0u;
         return put;
     }
@@ -171,8 +180,8 @@ struct Fast64 {
     BFT_FN void out_commit_p(bool c) { send_kind(c, 2, h, pp, F_CM, F_CM_W); }
     BFT_FN void out_blocks_p(bool c, uint32_t lo, uint32_t hi) {  // lo <= hi
         const bool hb = (nxf & F_BLK) != 0;
-        nx_blo = c ? (hb && nx_blo < lo ? nx_blo : lo) : nx_blo;
-        nx_bhi = c ? (hb && nx_bhi > hi ? nx_bhi : hi) : nx_bhi;
+        nx_blo = c ? ((hb & (nx_blo < lo)) ? nx_blo : lo) : nx_blo;
+        nx_bhi = c ? ((hb & (nx_bhi > hi)) ? nx_bhi : hi) : nx_bhi;
         nxf |= c ? F_BLK : 0u;
     }
     // the cold kinds always hand the instance over: fields straight to the hand-over area
@@ -244,29 +253,29 @@ struct Fast64 {
     // ------------------------------------------------------------------ chain, miner, timers
     BFT_FN void chain_insert_core_p(bool c) {                    // Chain::insert_block of pp (chain.rs:45-71)
         const uint32_t x = blk_h(pp);
-        const bool nw = c && x > last;                           // else ChainError::Exists
-        const bool gap = nw && last + 1 < x;                     // Not found ancestor → SyncBlock
+        const bool nw = c & (x > last);                          // else ChainError::Exists
+        const bool gap = nw & (last + 1 < x);                    // Not found ancestor → SyncBlock
         if (ballot(gap) != 0) { if (gap) out_sync(last + 1); }
-        const bool ins = nw && !gap;
+        const bool ins = nw & !gap;
         fl |= ins ? L_CMT : 0u;
         last_T = ins ? (int32_t)blk_T(pp) : last_T;
         last = ins ? x : last;
         out_blocks_p(ins, x, x);                                 // ChainEvent::NewBlock
-        miner_queue = (ins && x > miner_queue) ? x : miner_queue; // ChainEvent::NewHeader
+        miner_queue = (ins & (x > miner_queue)) ? x : miner_queue; // ChainEvent::NewHeader
     }
     // handle_msg_middle Block branch (core.rs:75-82) for the uniform range [lo, hi]
     BFT_FN void handle_blocks_p(bool c, uint32_t lo, uint32_t hi) {
-        const bool nw = c && hi > last;
-        const bool gap = nw && lo > last + 1;
+        const bool nw = c & (hi > last);
+        const bool gap = nw & (lo > last + 1);
         if (ballot(gap) != 0) { if (gap) out_sync(last + 1); }
-        const bool ins = nw && !gap;
+        const bool ins = nw & !gap;
         // time tick of block hi: the canonical tip, or a recorded row (hi is uniform)
         const int32_t T = hi == canon_h ? (int32_t)blk_T(canon_tip) : (int32_t)uni(row_word(hi, 2));
         const uint32_t from = last + 1;
         last = ins ? hi : last;
         last_T = ins ? T : last_T;
         out_blocks_p(ins, from, hi);
-        miner_queue = (ins && hi > miner_queue) ? hi : miner_queue;
+        miner_queue = (ins & (hi > miner_queue)) ? hi : miner_queue;
     }
     BFT_FN void start_new_zero_round_p(bool c) {                 // core.rs:441-470
         h = c ? last + 1 : h;
@@ -278,17 +287,17 @@ struct Fast64 {
         timer_tick = c ? tick + 1 : timer_tick;                  // new_round_change_timer
     }
     BFT_FN void send_preprepare_cand_p(bool c) {                 // preprepare.rs:30-43, req = candidate
-        const bool s = c && h == mint_height && has(L_PROP) && me == 0;
+        const bool s = c & (h == mint_height) & has(L_PROP) & (me == 0);
         if (ballot(s) != 0) {                                    // the proposer (validator 0) proposes
             bool cr = false;
             if (P.crash_on) cr = proposer_crashed(seed(), P.crash_thr32, 1u, inst, h, 0);
-            out_preprepare_p(s && !cr);
+            out_preprepare_p(s & !cr);
         }
     }
     BFT_FN void handle_new_header_event_p(bool c) {              // core.rs:154-163 + request.rs:19-42
-        c = c && !has(L_DEAD);
+        c = c & !has(L_DEAD);
         start_new_zero_round_p(c);
-        const bool pv = c && h == mint_height;                   // accept the own candidate
+        const bool pv = c & (h == mint_height);                  // accept the own candidate
         fl |= pv ? L_PENDV : 0u;
         if (pv) *lane_p(F64Layout::W_PENDT) = cand_T;
         send_preprepare_cand_p(pv);
@@ -298,15 +307,15 @@ struct Fast64 {
         const int32_t T = tick > last_T + 1 ? tick : last_T + 1;
         cand_T = c ? (uint32_t)T : cand_T;
         mint_height = c ? x : mint_height;
-        const bool now = c && T <= tick;                         // seal sleeps until header.time otherwise
+        const bool now = c & (T <= tick);                        // seal sleeps until header.time otherwise
         wake_tick = c ? (now ? -1 : T) : wake_tick;
         if (ballot(now) != 0) handle_new_header_event_p(now);
     }
     BFT_FN void miner_step_p() {                                 // Minner: Handler<NewHeader> (minner/mod.rs:56-69)
-        const bool ev = has(L_RUN) && wake_tick < 0;
+        const bool ev = has(L_RUN) & (wake_tick < 0);
         const uint32_t q = miner_queue;
         miner_queue = ev ? 0u : miner_queue;
-        const bool m = ev && q != 0 && q >= mint_height;
+        const bool m = ev & (q != 0) & (q >= mint_height);
         if (ballot(m) != 0) miner_mine_p(m);
     }
     BFT_FN void new_round_change_timer() { timer_tick = tick + 1; }
@@ -322,26 +331,31 @@ struct Fast64 {
     BFT_FN void t_step() {                                       // SPEC.md §2 T-step (running validators)
         const bool run = has(L_RUN);
         if (tick == 0) { start_new_zero_round_p(run); miner_mine_p(run); return; }
-        const bool w = run && wake_tick == tick;                 // seal wakes up
+        const bool w = run & (wake_tick == tick);                // seal wakes up
         wake_tick = w ? -1 : wake_tick;
         if (ballot(w) != 0) handle_new_header_event_p(w);
-        if (ballot(run && wake_tick < 0 && miner_queue != 0) != 0) miner_step_p();
+        if (ballot(run & (wake_tick < 0) & (miner_queue != 0)) != 0) miner_step_p();
         const uint32_t spv = *lane_p(F64Layout::W_SYNC);
-        const bool sp = run && spv != 0;
+        const bool sp = run & (spv != 0);
         if (ballot(sp) != 0) {
-            if (sp && last < spv) out_sync(last + 1);
+            if (sp & (last < spv)) out_sync(last + 1);
             if (sp) *lane_p(F64Layout::W_SYNC) = 0;
         }
-        const bool tm = run && !has(L_DEAD) && timer_tick == tick;   // TimerEvent (core.rs:207-225)
+        const bool tm = run & !has(L_DEAD) & (timer_tick == tick);  // TimerEvent (core.rs:207-225)
         if (ballot(tm) != 0) {
             timer_tick = tm ? -1 : timer_tick;
-            const bool caught = tm && last >= h;
+            const bool caught = tm & (last >= h);
             fl &= caught ? ~L_WAIT : ~0u;
-            if (tm && !caught) send_next_round_change();
+            if (tm & !caught) send_next_round_change();
         }
     }
+    // an outbox message or a queued chain event (SPEC.md §2). Integer form, no lane-mask logic: a queued
+    // event is wake_tick < 0 and miner_queue >= max(mint_height, 1), i.e. bit 31 of m1 - 1 - mq. A
+    // validator that is not running never has either (every handler and the T-step are gated by L_RUN).
     BFT_FN bool pending_local() const {
-        return has(L_RUN) && (nxf != 0 || (wake_tick < 0 && miner_queue != 0 && miner_queue >= mint_height));
+        const uint32_t mq = wake_tick < 0 ? miner_queue : 0u;
+        const uint32_t m1 = mint_height > 1u ? mint_height : 1u;
+        return (nxf | ((m1 + ~mq) >> 31)) != 0;
     }
 
     // ------------------------------------------------------------------ handlers
@@ -349,11 +363,13 @@ struct Fast64 {
     BFT_FN void handle_preprepare_p(bool c, uint32_t src, uint32_t vh, uint64_t b, bool equiv) {
         if (equiv) {                                             // SPEC.md §6: variant 1 to SPLIT receivers
             const uint64_t sm = split_mask(vh);
-            b |= (me != src && ((sm >> me) & 1ull)) ? (1ull << 33) : 0ull;
+            b |= ((me != src) & (((sm >> me) & 1ull) != 0)) ? (1ull << 33) : 0ull;
         }
-        const int res = check_message_class(MT_PREPREPARE, vh, h, st());
-        bool go = c && (res == CM_OK || res == CM_FUTURE_BLOCK);   // FutureBlockMessage falls through
-        const bool old = c && res == CM_OLD;
+        // check_message (core.rs:366-399) of a Preprepare of height vh (uniform): Unknown for 0, OK at h,
+        // FutureBlock above h (falls through), OldMessage below
+        const bool vok = vh != 0;
+        bool go = c & vok & (vh >= h);
+        const bool old = c & vok & (vh < h);
         if (ballot(old) != 0) {                                  // a Preprepare of a passed height
             if (old) {
                 const uint32_t bh = blk_h(b);
@@ -363,18 +379,18 @@ struct Fast64 {
                 }
             }
         }
-        go = go && has(L_PROP) && src == 0;                      // else NotFromProposer
+        go = go & has(L_PROP) & (src == 0);                      // else NotFromProposer
         const uint32_t bh = blk_h(b);
-        const bool bad = go && (bh == 0 || bh - 1 > last);       // Backend::verify: unknown ancestor
-        const bool acc = go && !bad && st() == ST_ACCEPT_REQUEST;
-        const bool lk = acc && has(L_LOCK);
-        const bool lk_ok = lk && blk_eq(b, pp);                  // locked: same block → commit
-        const bool unl = acc && !has(L_LOCK);                    // unlocked: accept → prepare
-        pp = (lk_ok || unl) ? b : pp;
+        const bool bad = go & ((bh == 0) | (bh - 1 > last));    // Backend::verify: unknown ancestor
+        const bool acc = go & !bad & (st() == ST_ACCEPT_REQUEST);
+        const bool lk = acc & has(L_LOCK);
+        const bool lk_ok = lk & beq(b, pp);                      // locked: same block → commit
+        const bool unl = acc & !has(L_LOCK);                     // unlocked: accept → prepare
+        pp = (lk_ok | unl) ? b : pp;
         fl = lk_ok ? ((fl & ~L_ST) | ST_PREPARED) : unl ? ((fl & ~L_ST) | ST_PREPREPARED) : fl;
         out_prepare_p(unl);                                      // send_prepare
-        out_commit_p(lk_ok || (unl && has(L_BYZ)));              // send_commit / Byzantine commit (SPEC.md §6)
-        const bool rc = bad || (lk && !lk_ok);
+        out_commit_p(lk_ok | (unl & has(L_BYZ)));                // send_commit / Byzantine commit (SPEC.md §6)
+        const bool rc = bad | (lk & !lk_ok);
         if (ballot(rc) != 0) { if (rc) send_next_round_change(); }
     }
     BFT_FN void lock_hash() { if (blk_valid(pp)) fl |= L_LOCK; }   // round_state.rs:100-110 (lock = pp)
@@ -417,58 +433,66 @@ struct Fast64 {
     BFT_FN void deliver_pc(bool rcv, const PC& c, uint64_t mk, uint32_t off) {
         const uint64_t prd = rcv ? (mk & c.kpr) : 0ull, cmd = rcv ? (mk & c.kcm) : 0ull;
         const uint32_t s0 = st();
-        const int rp = check_message_class(MT_PREPARE, c.pr_h, h, s0);
-        const int rm = check_message_class(MT_COMMIT, c.cm_h, h, s0);
+        // check_message (core.rs:366-399) of a Prepare / Commit of the uniform height vh: Unknown for
+        // vh = 0, FutureBlock above h, OK at h once the Core is past AcceptRequest
+        const bool sok = s0 != ST_ACCEPT_REQUEST;
+        const bool prn = c.pr_h != 0, cmn = c.cm_h != 0;
         // FutureBlockMessage → the delayed sync check (core.rs:58-69)
-        const bool fpr = prd != 0 && rp == CM_FUTURE_BLOCK, fcm = cmd != 0 && rm == CM_FUTURE_BLOCK;
-        if (ballot(fpr || fcm) != 0) {
-            if (fpr || fcm) {
+        const bool fpr = (prd != 0) & prn & (c.pr_h > h), fcm = (cmd != 0) & cmn & (c.cm_h > h);
+        if (ballot(fpr | fcm) != 0) {
+            if (fpr | fcm) {
                 uint32_t v = *lane_p(F64Layout::W_SYNC);
-                v = (fpr && c.pr_h > v) ? c.pr_h : v;
-                v = (fcm && c.cm_h > v) ? c.cm_h : v;
+                v = (fpr & (c.pr_h > v)) ? c.pr_h : v;
+                v = (fcm & (c.cm_h > v)) ? c.cm_h : v;
                 *lane_p(F64Layout::W_SYNC) = v;
             }
         }
-        const uint64_t PRacc = (rp == CM_OK && c.pr_h == h) ? prd : 0ull;
-        const uint64_t CMacc = (rm == CM_OK && c.cm_h == h) ? (cmd & class_match_k(c.kcm, c.v1, c.cm_cls, pp)) : 0ull;
+        // digests matching the own pp (class_match_k): a Byzantine sender's wildcard matches both variants
+        const uint64_t vsel = byz_mask | (blk_var(pp) ? c.v1 : ~c.v1);
+        const bool ppv = blk_valid(pp);
+        const bool mpr = ppv & (((c.pr_cls ^ pp) & BLK_HP_MASK) == 0);
+        const bool mcm = ppv & (((c.cm_cls ^ pp) & BLK_HP_MASK) == 0);
+        const uint64_t PRacc = (prn & sok & (c.pr_h == h)) ? prd : 0ull;
+        const uint64_t CMacc = (cmn & sok & (c.cm_h == h) & mcm) ? (cmd & vsel) : 0ull;   // cmd ⊆ kcm
         // Order-free evaluation first. The delivery order (rotation by `off`) only matters when the
         // prepare quorum is crossed by commits delivered before the last prepare, or when a trigger and a
         // commit quorum both occur (which comes last decides Prepared vs Committed); lanes in either case
         // take the exact rotated closed form below (a uniform branch, skipped when no lane needs it).
         const uint64_t U = prep | comm;
-        const uint64_t mpp0 = PRacc & class_match_k(c.kpr, c.v1, c.pr_cls, pp);
+        const uint64_t mpp0 = mpr ? (PRacc & vsel) : 0ull;        // PRacc ⊆ kpr
         const uint32_t nUP = popc(U | PRacc);
-        const bool cexists = CMacc != 0 && popc(comm | CMacc) > Q;
-        const bool tb_amb = PRacc != 0 && CMacc != 0 && nUP <= Q && popc(U | PRacc | CMacc) > Q;
-        bool trig = (PRacc != 0 && nUP > Q) || (has(L_LOCK) && mpp0 != 0);
+        const bool pra = PRacc != 0, cma = CMacc != 0;
+        const bool cexists = cma & (popc(comm | CMacc) > Q);
+        const bool tb_amb = pra & cma & (nUP <= Q) & (popc(U | PRacc | CMacc) > Q);
+        bool trig = (pra & (nUP > Q)) | (has(L_LOCK) & (mpp0 != 0));
         const bool committed = s0 >= ST_COMMITTED;
-        bool fires = !trig && cexists && !committed;
+        bool fires = !trig & cexists & !committed;
         uint32_t fin = trig ? ST_PREPARED : (fires ? ST_COMMITTED : s0);
-        const bool amb = tb_amb || (trig && cexists);
+        const bool amb = tb_amb | (trig & cexists);
         if (ballot(amb) != 0) {
             if (amb) {
                 const uint64_t PR = rotr(PRacc, off), CM = rotr(CMacc, off);
                 const uint64_t U0 = rotr(U, off);
                 const uint32_t lastPR = hibit(PR), lastCM = hibit(CM);
-                const bool trigB = PR != 0 && popc(U0 | PR | (CM & low(lastPR))) > Q;
+                const bool trigB = (PR != 0) & (popc(U0 | PR | (CM & low(lastPR))) > Q);
                 const uint64_t mpp = rotr(mpp0, off);
                 const uint64_t lm = has(L_LOCK) ? mpp : 0ull;       // lock == pp when locked
-                trig = trigB || lm != 0;
+                trig = trigB | (lm != 0);
                 uint32_t t1 = lm ? ctz64(lm) : 64u;
                 const uint32_t lastT = trigB ? lastPR : hibit((mpp & ~low(t1)) | (t1 < 64u ? (1ull << t1) : 0ull));
-                if (trig && committed && trigB) {                  // a re-commit needs a commit after the first trigger
+                if (trig & committed & trigB) {                    // a re-commit needs a commit after the first trigger
                     const uint32_t pstar = first_over(U0, PR, CM);
                     const uint64_t ge = PR & ~low(pstar);
                     const uint32_t tB = ge ? ctz64(ge) : 64u;
                     t1 = tB < t1 ? tB : t1;
                 }
-                fires = trig ? (committed ? (cexists && lastCM >= t1) : cexists) : (cexists && !committed);
-                fin = trig ? ((cexists && lastCM >= lastT) ? ST_COMMITTED : ST_PREPARED) : (fires ? ST_COMMITTED : s0);
+                fires = trig ? (committed ? (cexists & (lastCM >= t1)) : cexists) : (cexists & !committed);
+                fin = trig ? ((cexists & (lastCM >= lastT)) ? ST_COMMITTED : ST_PREPARED) : (fires ? ST_COMMITTED : s0);
             }
         }
         prep |= PRacc;
         comm |= CMacc;
-        fl |= ((trig || fires) && blk_valid(pp)) ? L_LOCK : 0u;  // lock_hash
+        fl |= ((trig | fires) & ppv) ? L_LOCK : 0u;               // lock_hash
         out_commit_p(trig);                                      // send_commit
         chain_insert_core_p(fires);                              // Core::commit → insert_block
         set_st(fin);
@@ -484,12 +508,12 @@ struct Fast64 {
         const uint32_t lead = ctz64(bal);
         const uint32_t x = blk_h(pp);
         const uint32_t x0 = uni(rl(x, lead));
-        if (ballot(c && x != x0) == 0) {
+        if (ballot(c & (x != x0)) == 0) {
             // every committer commits the first one's height (the common case): uniform update
             const uint64_t b0 = rl64(pp, lead);
             const bool known = x0 <= canon_h;
             const uint64_t ref = known ? canon_blk(x0) : b0;
-            const uint64_t badm = ballot(c && !blk_eq(pp, ref));
+            const uint64_t badm = ballot(c & !beq(pp, ref));
             bool fr = badm != 0;
             if (!known && x0 < P.hcap && (!fr || ctz64(badm) > lead)) record_canon(x0, b0);
             if (x0 >= P.hcap) fr = true;
@@ -526,7 +550,7 @@ struct Fast64 {
         const uint64_t ppb = blk_make(h, me, 0, *lane_p(F64Layout::W_PPT));
         const uint32_t w32[29] = {h, 0u, st(), 0u, proposer(), last, 0u, (uint32_t)last_T, (uint32_t)timer_tick,
                                   *lane_p(F64Layout::W_RCLT), (uint32_t)wake_tick, mint_height, miner_queue,
-                                  *lane_p(F64Layout::W_SYNC), *lane_p(F64Layout::W_LFL), canon_h, done_tick, seg_flags, 0u, canon_tick, nxf,
+                                  *lane_p(F64Layout::W_SYNC), lane_flags(), canon_h, done_tick, seg_flags, 0u, canon_tick, nxf,
                                   h, 0u, h, 0u, h, 0u, nx_blo, nx_bhi};
         uint32_t k = 0;
         for (uint32_t i = 0; i < 29; ++i) s[k++] = w32[i];
@@ -587,8 +611,9 @@ struct Fast64 {
             off_tick = offset_tick_part(off_inst, (uint32_t)tick);
             F64_STAMP(7);
             // the T-step, only when some running validator has a tick event
-            if (ballot(has(L_RUN) && (tick == 0 || wake_tick == tick || (wake_tick < 0 && miner_queue != 0) ||
-                                      *lane_p(F64Layout::W_SYNC) != 0 || (!has(L_DEAD) && timer_tick == tick))) != 0) {
+            // (a validator that is not running has no events: wake_tick, timer_tick -1, nothing queued)
+            if (tick == 0 || ballot((wake_tick == tick) | ((wake_tick < 0) & (miner_queue != 0)) |
+                                    (*lane_p(F64Layout::W_SYNC) != 0) | (!has(L_DEAD) & (timer_tick == tick))) != 0) {
                 t_step();
             }
             F64_STAMP(0);
@@ -599,56 +624,36 @@ struct Fast64 {
                     nxf = 0;
                     break;
                 }
-                // what is in flight, by kind (segment = wave)
-                const bool pr = (nxf & F_PR) != 0, cm = (nxf & F_CM) != 0;
-                const uint64_t kpp = ballot((nxf & F_PP) != 0), kpr = ballot(pr), kcm = ballot(cm);
-                const uint64_t kblk = ballot((nxf & F_BLK) != 0);
-                const uint64_t kcold = ballot((nxf & (F_OCM | F_RC | F_SYNC)) != 0);
-                uint32_t path = P_GENERAL;
+                // what is in flight, by kind (segment = wave). The classification is branch-free: every
+                // kind's first sender is read whether or not the kind is present, so no per-path values
+                // are merged at control-flow joins (those merges cost a copy of every live value).
+                const uint32_t f = nxf;
+                const bool pr = (f & F_PR) != 0, cm = (f & F_CM) != 0;
+                const uint64_t kpp = ballot((f & F_PP) != 0), kpr = ballot(pr), kcm = ballot(cm);
+                const uint64_t kblk = ballot((f & F_BLK) != 0);
+                const uint64_t kcold = ballot((f & (F_OCM | F_RC | F_SYNC)) != 0);
+                const uint32_t j = ff1(kpp), jp = ff1(kpr), jc = ff1(kcm), jb = ff1(kblk);
+                const uint64_t cls = pp & BLK_HP_MASK;
                 PC c;
-                uint32_t j = 0, pp_h = 0, pp_T = 0, pp_eq = 0, blo = 0, bhi = 0;
-                if (kcold) {
-                    path = P_GENERAL;
-                } else if (kpp) {
-                    if ((kpr | kcm | kblk) == 0 && popc(kpp) == 1) {
-                        path = P_PP;
-                        j = ctz64(kpp);
-                        pp_h = uni(rl(h, j));
-                        pp_T = uni(rl(*lane_p(F64Layout::W_PPT), j));
-                        pp_eq = uni(rl(nxf & F_PP_EQ, j));
-                    }
-                } else if ((kpr | kcm) == 0) {
-                    if (kblk == 0) {
-                        path = P_NONE;                           // only miner events this phase
-                    } else {
-                        const uint32_t jb = ctz64(kblk);
-                        blo = uni(rl(nx_blo, jb));
-                        bhi = uni(rl(nx_bhi, jb));
-                        const bool bk = (nxf & F_BLK) != 0;
-                        path = ballot(bk && (nx_blo != blo || nx_bhi != bhi)) == 0 ? P_BLK : P_GENERAL;
-                    }
-                } else if (kblk == 0) {
-                    const uint64_t cls = pp & BLK_HP_MASK;
-                    c.kpr = kpr; c.kcm = kcm;
-                    c.pr_h = c.cm_h = 0; c.pr_cls = c.cm_cls = 0;
-                    bool mm = false;
-                    if (kpr) {
-                        const uint32_t jp = ctz64(kpr);
-                        c.pr_h = uni(rl(h, jp));
-                        c.pr_cls = rl64(cls, jp);
-                        mm = pr && (h != c.pr_h || cls != c.pr_cls);
-                    }
-                    if (kcm) {
-                        const uint32_t jc = ctz64(kcm);
-                        c.cm_h = uni(rl(h, jc));
-                        c.cm_cls = rl64(cls, jc);
-                        mm = mm || (cm && (h != c.cm_h || cls != c.cm_cls));
-                    }
-                    if (ballot(mm) == 0) {
-                        path = P_PC;
-                        c.v1 = ballot(blk_var(pp) != 0);
-                    }
-                }
+                c.kpr = kpr; c.kcm = kcm;
+                c.pr_h = kpr ? uni(rl(h, jp)) : 0u;
+                c.cm_h = kcm ? uni(rl(h, jc)) : 0u;
+                c.pr_cls = rl64(cls, jp);
+                c.cm_cls = rl64(cls, jc);
+                c.v1 = ballot(blk_var(pp) != 0);
+                const uint32_t pp_h = uni(rl(h, j));
+                const uint32_t pp_T = uni(rl(*lane_p(F64Layout::W_PPT), j));
+                const uint32_t pp_eq = uni(rl(f & F_PP_EQ, j));
+                const uint32_t blo = uni(rl(nx_blo, jb)), bhi = uni(rl(nx_bhi, jb));
+                uint32_t path;
+                if (kcold) path = P_GENERAL;
+                else if (kpp) path = ((kpr | kcm | kblk) == 0 && (kpp & (kpp - 1ull)) == 0) ? P_PP : P_GENERAL;
+                else if (kpr | kcm) path = kblk ? P_GENERAL : P_PC;
+                else path = kblk ? P_BLK : P_NONE;
+                // a PC phase needs one view and digest class per kind, a BLK phase one block range
+                const bool bad_pc = (pr & ((h != c.pr_h) | (cls != c.pr_cls))) | (cm & ((h != c.cm_h) | (cls != c.cm_cls)));
+                const bool bad_blk = ((f & F_BLK) != 0) & ((nx_blo != blo) | (nx_bhi != bhi));
+                if (ballot(path == P_PC ? bad_pc : ((path == P_BLK) & bad_blk)) != 0) path = P_GENERAL;
                 if (path == P_GENERAL) {                          // hand the instance to the full kernel
                     save_state(p);
                     if (me == 0) P.resume_flags[inst_local] = 1u;
@@ -657,26 +662,42 @@ struct Fast64 {
                     break;
                 }
                 nxf = 0;
+#ifdef BFT_AB_SALU
+                {   // diagnostic: BFT_AB_SALU dependent-free scalar adds per phase (issue-bound probe)
+                    uint32_t d0 = __builtin_amdgcn_readfirstlane(tick), d1 = __builtin_amdgcn_readfirstlane(p);
+#pragma unroll
+                    for (int q = 0; q < BFT_AB_SALU; ++q) asm volatile("s_add_u32 %0, %0, 1\n s_add_u32 %1, %1, 1" : "+s"(d0), "+s"(d1));
+                    asm volatile("" :: "s"(d0), "s"(d1));
+                }
+#endif
+#ifdef BFT_AB_VALU
+                {
+                    uint32_t d0 = me, d1 = me + 1;
+#pragma unroll
+                    for (int q = 0; q < BFT_AB_VALU; ++q) asm volatile("v_add_u32 %0, 1, %0\n v_add_u32 %1, 1, %1" : "+v"(d0), "+v"(d1));
+                    asm volatile("" :: "v"(d0), "v"(d1));
+                }
+#endif
                 F64_STAMP(1);
                 F64_COUNT(8);
                 if (act) {
                     // event step: Minner's NewHeader handler, for the validators with queued chain events
-                    if (ballot(has(L_RUN) && wake_tick < 0 && miner_queue != 0) != 0) miner_step_p();
+                    if (ballot(has(L_RUN) & (wake_tick < 0) & (miner_queue != 0)) != 0) miner_step_p();
                     F64_STAMP(2);
                     if (path != P_NONE) {
                         const uint64_t mk = deliver_mask<1>(seed(), N, P.thr16, inst, (uint32_t)tick, p, me).w[0];
                         if (path == P_PC) {
                             const uint32_t off = offset_from_parts(seed(), N, off_tick, p, me);
-                            deliver_pc(has(L_RUN) && !has(L_DEAD), c, mk, off);
+                            deliver_pc(has(L_RUN) & !has(L_DEAD), c, mk, off);
                             F64_STAMP(4);
                             F64_COUNT(10);
                         } else if (path == P_PP) {
-                            handle_preprepare_p(has(L_RUN) && ((mk >> j) & 1ull) && !has(L_DEAD), j, pp_h,
+                            handle_preprepare_p(has(L_RUN) & (((mk >> j) & 1ull) != 0) & !has(L_DEAD), j, pp_h,
                                                 blk_make(pp_h, j, 0, pp_T), pp_eq != 0);
                             F64_STAMP(3);
                             F64_COUNT(9);
                         } else {                                  // P_BLK
-                            handle_blocks_p(has(L_RUN) && (mk & kblk & ~(1ull << me)) != 0, blo, bhi);
+                            handle_blocks_p(has(L_RUN) & ((mk & kblk & ~(1ull << me)) != 0), blo, bhi);
                             F64_STAMP(5);
                             F64_COUNT(11);
                         }
@@ -703,7 +724,7 @@ struct Fast64 {
             }
             if (me == 0 && views_acc != 0) wv.gadd64(P.hist, views_acc);
         }
-        uint32_t lf = *lane_p(F64Layout::W_LFL);
+        uint32_t lf = lane_flags();
         for (uint32_t m = 1; m < 64u; m <<= 1) lf |= wv.shfl_xor(lf, (int)m);
         if (me == 0 && inst_local < P.n_instances && !bailed) {
             uint32_t flags = lf | seg_flags;
