@@ -248,8 +248,10 @@ BFT_FN uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a
 // loops and keeps it live in SGPRs across the whole body, which spills.
 #if defined(__HIP_DEVICE_COMPILE__)
 #define BFT_OPAQUE_SGPR(x) asm volatile("" : "+s"(x))
+#define BFT_OPAQUE_VGPR(x) asm volatile("" : "+v"(x))   // forces the value (and what is computed from it) onto the vector lanes
 #else
 #define BFT_OPAQUE_SGPR(x) do { } while (0)
+#define BFT_OPAQUE_VGPR(x) do { } while (0)
 #endif
 
 // Philox4x32-10 (Salmon et al. SC'11); 10 rounds of two 32x32→64 multiplies.

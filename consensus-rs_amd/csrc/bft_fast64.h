@@ -334,7 +334,7 @@ struct Fast64 {
         const bool w = run & (wake_tick == tick);                // seal wakes up
         wake_tick = w ? -1 : wake_tick;
         if (ballot(w) != 0) handle_new_header_event_p(w);
-        if (ballot(run & (wake_tick < 0) & (miner_queue != 0)) != 0) miner_step_p();
+        if (ballot(miner_event() != 0) != 0) miner_step_p();
         const uint32_t spv = *lane_p(F64Layout::W_SYNC);
         const bool sp = run & (spv != 0);
         if (ballot(sp) != 0) {
@@ -352,6 +352,9 @@ struct Fast64 {
     // an outbox message or a queued chain event (SPEC.md §2). Integer form, no lane-mask logic: a queued
     // event is wake_tick < 0 and miner_queue >= max(mint_height, 1), i.e. bit 31 of m1 - 1 - mq. A
     // validator that is not running never has either (every handler and the T-step are gated by L_RUN).
+    // the queued chain event of a running validator whose seal is not sleeping: miner_queue if
+    // wake_tick < 0, else 0 (a validator that is not running never queues one)
+    BFT_FN uint32_t miner_event() const { return wake_tick < 0 ? miner_queue : 0u; }
     BFT_FN bool pending_local() const {
         const uint32_t mq = wake_tick < 0 ? miner_queue : 0u;
         const uint32_t m1 = mint_height > 1u ? mint_height : 1u;
@@ -396,9 +399,13 @@ struct Fast64 {
     BFT_FN void lock_hash() { if (blk_valid(pp)) fl |= L_LOCK; }   // round_state.rs:100-110 (lock = pp)
 
     // SPLIT bits of receivers 0..63 for view (vh, 0) (SPEC.md §5; split_bit for v < 64): one uniform draw
+    // Evaluated on the vector lanes (every lane the same draw): as a scalar Philox it is ~100
+    // instructions on the CU's one scalar unit, the kernel's bottleneck.
     BFT_FN uint64_t split_mask(uint32_t vh) const {
+        uint32_t v = vh;
+        BFT_OPAQUE_VGPR(v);
         uint32_t w[4];
-        philox(seed(), inst, vh, 0, DOM_SPLIT, w);
+        philox(seed(), inst, v, 0, DOM_SPLIT, w);
         return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
     }
 
@@ -632,12 +639,15 @@ struct Fast64 {
                 const uint64_t kpp = ballot((f & F_PP) != 0), kpr = ballot(pr), kcm = ballot(cm);
                 const uint64_t kblk = ballot((f & F_BLK) != 0);
                 const uint64_t kcold = ballot((f & (F_OCM | F_RC | F_SYNC)) != 0);
-                const uint32_t j = ff1(kpp), jp = ff1(kpr), jc = ff1(kcm), jb = ff1(kblk);
+                // the only Preprepare sender of the FAST kernel is the round-0 proposer, validator 0
+                // (send_preprepare_cand_p): kpp is 0 or 1
+                const uint32_t j = 0, jp = ff1(kpr), jc = ff1(kcm), jb = ff1(kblk);
                 const uint64_t cls = pp & BLK_HP_MASK;
                 PC c;
                 c.kpr = kpr; c.kcm = kcm;
-                c.pr_h = kpr ? uni(rl(h, jp)) : 0u;
-                c.cm_h = kcm ? uni(rl(h, jc)) : 0u;
+                const uint32_t hp = uni(rl(h, jp)), hc = uni(rl(h, jc));
+                c.pr_h = kpr ? hp : 0u;
+                c.cm_h = kcm ? hc : 0u;
                 c.pr_cls = rl64(cls, jp);
                 c.cm_cls = rl64(cls, jc);
                 c.v1 = ballot(blk_var(pp) != 0);
@@ -647,13 +657,18 @@ struct Fast64 {
                 const uint32_t blo = uni(rl(nx_blo, jb)), bhi = uni(rl(nx_bhi, jb));
                 uint32_t path;
                 if (kcold) path = P_GENERAL;
-                else if (kpp) path = ((kpr | kcm | kblk) == 0 && (kpp & (kpp - 1ull)) == 0) ? P_PP : P_GENERAL;
+                else if (kpp) path = (kpr | kcm | kblk) == 0 ? P_PP : P_GENERAL;
                 else if (kpr | kcm) path = kblk ? P_GENERAL : P_PC;
                 else path = kblk ? P_BLK : P_NONE;
                 // a PC phase needs one view and digest class per kind, a BLK phase one block range
-                const bool bad_pc = (pr & ((h != c.pr_h) | (cls != c.pr_cls))) | (cm & ((h != c.cm_h) | (cls != c.cm_cls)));
-                const bool bad_blk = ((f & F_BLK) != 0) & ((nx_blo != blo) | (nx_bhi != bhi));
-                if (ballot(path == P_PC ? bad_pc : ((path == P_BLK) & bad_blk)) != 0) path = P_GENERAL;
+                // (integer form: a nonzero XOR marks a mismatch, one compare per lane)
+                const uint32_t cls_lo = (uint32_t)cls, cls_hi = (uint32_t)(cls >> 32);
+                const uint32_t bad_pr = (h ^ c.pr_h) | (cls_lo ^ (uint32_t)c.pr_cls) | (cls_hi ^ (uint32_t)(c.pr_cls >> 32));
+                const uint32_t bad_cm = (h ^ c.cm_h) | (cls_lo ^ (uint32_t)c.cm_cls) | (cls_hi ^ (uint32_t)(c.cm_cls >> 32));
+                const uint32_t bad_pc = (pr ? bad_pr : 0u) | (cm ? bad_cm : 0u);
+                const uint32_t bad_blk = (f & F_BLK) ? ((nx_blo ^ blo) | (nx_bhi ^ bhi)) : 0u;
+                const uint32_t bad = path == P_PC ? bad_pc : (path == P_BLK ? bad_blk : 0u);
+                if (ballot(bad != 0) != 0) path = P_GENERAL;
                 if (path == P_GENERAL) {                          // hand the instance to the full kernel
                     save_state(p);
                     if (me == 0) P.resume_flags[inst_local] = 1u;
@@ -682,7 +697,7 @@ struct Fast64 {
                 F64_COUNT(8);
                 if (act) {
                     // event step: Minner's NewHeader handler, for the validators with queued chain events
-                    if (ballot(has(L_RUN) & (wake_tick < 0) & (miner_queue != 0)) != 0) miner_step_p();
+                    if (ballot(miner_event() != 0) != 0) miner_step_p();
                     F64_STAMP(2);
                     if (path != P_NONE) {
                         const uint64_t mk = deliver_mask<1>(seed(), N, P.thr16, inst, (uint32_t)tick, p, me).w[0];
