@@ -234,12 +234,11 @@ struct Fast64 {
     }
     // a new canonical height (uniform): row, histograms, instance-rounds
     BFT_FN void record_canon(uint32_t x, uint64_t b) {
-        if (x <= P.heights) {
-            const uint32_t lat = (uint32_t)tick - canon_tick;
-            if (me == 0) wv.lds_add((uint32_t*)(lds + F64Layout::LAT_OFF) + (lat < 64u ? lat : 64u), 1u);
-            views_acc += 1;
-        }
-        if (me == 0) {
+        const uint32_t cnt = x <= P.heights ? 1u : 0u;             // uniform
+        const uint32_t lat = (uint32_t)tick - canon_tick;
+        views_acc += cnt;
+        if (me == 0) {                                           // one lane: latency histogram and the ring row
+            wv.lds_add((uint32_t*)(lds + F64Layout::LAT_OFF) + (lat < 64u ? lat : 64u), cnt);
             uint32_t* r = ring_row(x);
             r[0] = 0; r[1] = blk_prop(b) | (blk_var(b) << 16) | (1u << 24); r[2] = blk_T(b); r[3] = 0;
         }
