@@ -191,9 +191,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each step's block-hash pass on the launch stream (no overlap across steps)")
-    ap.add_argument("--pipeline-depth", type=int, default=None,
-                    help="row-table sets in the launch ring (bftsim_set_pipeline); default 3, and 6 at <= 2,048 "
-                         "instances per GPU where the hash chains' latency, not the GPU, bounds a launch")
+    ap.add_argument("--pipeline-depth", type=int, default=3,
+                    help="row-table sets in the launch ring (bftsim_set_pipeline); 3 measured best at every shard "
+                         "size (profiles/r02/curve): one hash stream per set, and more streams than the 4 hardware "
+                         "queues serialize the hash passes")
     ap.add_argument("--byz", type=int, default=None,
                     help="cfg2 / cfg5: run the tolerated f as this many equivocating validators (SPEC.md §6: "
                          "cfg2-byz = 1, cfg5-byz = 2)")
@@ -256,8 +257,6 @@ def main():
     else:
         I = args.instances
         first = rank * I
-    if args.pipeline_depth is None:
-        args.pipeline_depth = 6 if I <= 2048 else 3     # profiles/r02/curve: best per shard size
     sim.set_pipeline(pipelined, args.pipeline_depth)
     if c5:
         sim.set_window(args.window)

@@ -697,7 +697,7 @@ struct Sim {
     }
 
     BFT_FN bool pending_local() const {
-        return running && (nx.f != 0 || (wake_tick < 0 && miner_queue != 0 && miner_queue >= mint_height));
+        return running & ((nx.f != 0) | ((wake_tick < 0) & (miner_queue != 0) & (miner_queue >= mint_height)));
     }
 
     BFT_FN void t_step() {
@@ -1005,10 +1005,10 @@ struct Sim {
             ps.pr_h = from_seg_lane(nx.pr_h, j);
             ps.pr_r = from_seg_lane(nx.pr_r, j);
             ps.pr_cls = (uint64_t)from_seg_lane((uint32_t)cls, j) | ((uint64_t)from_seg_lane((uint32_t)(cls >> 32), j) << 32);
-            mm_pr = pr && (nx.pr_h != ps.pr_h || nx.pr_r != ps.pr_r || cls != ps.pr_cls);
-            ps.pr_w = seg_bits(ballot(pr && prw));
-            ps.pr_v0 = seg_bits(ballot(pr && !prw && blk_var(nx.pr_d) == 0));
-            ps.pr_v1 = seg_bits(ballot(pr && !prw && blk_var(nx.pr_d) == 1));
+            mm_pr = pr & ((nx.pr_h != ps.pr_h) | (nx.pr_r != ps.pr_r) | (cls != ps.pr_cls));
+            ps.pr_w = seg_bits(ballot(pr & prw));
+            ps.pr_v0 = seg_bits(ballot(pr & !prw & (blk_var(nx.pr_d) == 0)));
+            ps.pr_v1 = seg_bits(ballot(pr & !prw & (blk_var(nx.pr_d) == 1)));
         }
         if (any_cm) {
             uint32_t j = ps.k_cm.any() ? ps.k_cm.ctz_nz() : 0u;
@@ -1016,16 +1016,16 @@ struct Sim {
             ps.cm_h = from_seg_lane(nx.cm_h, j);
             ps.cm_r = from_seg_lane(nx.cm_r, j);
             ps.cm_cls = (uint64_t)from_seg_lane((uint32_t)cls, j) | ((uint64_t)from_seg_lane((uint32_t)(cls >> 32), j) << 32);
-            mm_cm = cm && (nx.cm_h != ps.cm_h || nx.cm_r != ps.cm_r || cls != ps.cm_cls);
-            ps.cm_w = seg_bits(ballot(cm && cmw));
-            ps.cm_v0 = seg_bits(ballot(cm && !cmw && blk_var(nx.cm_d) == 0));
-            ps.cm_v1 = seg_bits(ballot(cm && !cmw && blk_var(nx.cm_d) == 1));
+            mm_cm = cm & ((nx.cm_h != ps.cm_h) | (nx.cm_r != ps.cm_r) | (cls != ps.cm_cls));
+            ps.cm_w = seg_bits(ballot(cm & cmw));
+            ps.cm_v0 = seg_bits(ballot(cm & !cmw & (blk_var(nx.cm_d) == 0)));
+            ps.cm_v1 = seg_bits(ballot(cm & !cmw & (blk_var(nx.cm_d) == 1)));
         }
         if (any_bk) {
             uint32_t j = ps.k_blk.any() ? ps.k_blk.ctz_nz() : 0u;
             ps.blk_lo = from_seg_lane(nx.blk_lo, j);
             ps.blk_hi = from_seg_lane(nx.blk_hi, j);
-            mm_blk = bk && (nx.blk_lo != ps.blk_lo || nx.blk_hi != ps.blk_hi);
+            mm_blk = bk & ((nx.blk_lo != ps.blk_lo) | (nx.blk_hi != ps.blk_hi));
         }
         if (any_pr | any_cm | any_bk) {
             ps.u_pr = seg_bits(ballot(mm_pr)).none();
@@ -1094,12 +1094,12 @@ struct Sim {
         const uint32_t lastCM = CM.hibit();
         // prepare triggers (prepare.rs:54-63). B fires at some prepare iff it fires at the last
         // one (|prep ∪ commit| only grows); commits of the last prepare's sender come after it.
-        const bool trigB = PR.any() && (U0 | PR | (CM & low(lastPR))).popc() > q;
+        const bool trigB = PR.any() & ((U0 | PR | (CM & low(lastPR))).popc() > q);
         M lm = M::zero();
         if (blk_valid(lock) && PR.any()) lm = rot(PRacc & class_match(ps.pr_cls, ps.pr_v0, ps.pr_v1, ps.pr_w, lock), off);
-        const bool trig = trigB || lm.any();
+        const bool trig = trigB | lm.any();
         // commit quorum events (commit.rs:75-80) exist iff the final count is over q
-        const bool cexists = CM.any() && (C0 | CM).popc() > q;
+        const bool cexists = CM.any() & ((C0 | CM).popc() > q);
         uint32_t lastT = 0, t1 = 64u * NW;
         if (trig) {
             if (lm.any()) t1 = lm.ctz_nz();
@@ -1116,7 +1116,7 @@ struct Sim {
         bool fires;          // some commit event runs Core::commit
         uint32_t fin;
         if (trig) {
-            fin = (cexists && lastCM >= lastT) ? ST_COMMITTED : ST_PREPARED;
+            fin = (cexists & (lastCM >= lastT)) ? ST_COMMITTED : ST_PREPARED;
             if (s0 < ST_COMMITTED) {
                 fires = cexists;
             } else {
@@ -1126,10 +1126,10 @@ struct Sim {
                     uint32_t tB = first_at_or_after(PR, pstar);
                     if (tB < t1) t1 = tB;
                 }
-                fires = cexists && lastCM >= t1;
+                fires = cexists & (lastCM >= t1);
             }
         } else {
-            fires = cexists && s0 < ST_COMMITTED;
+            fires = cexists & (s0 < ST_COMMITTED);
             fin = fires ? ST_COMMITTED : s0;
         }
         (void)n;
@@ -1222,7 +1222,7 @@ struct Sim {
         sync();
         for (tick = tick0; tick < (int32_t)P.max_ticks; ++tick) {
             if (ballot(!seg_done).none()) break;
-            bool act = running && !seg_done && !frozen;
+            bool act = running & !seg_done & !frozen;
             off_tick = offset_tick_part(off_inst, (uint32_t)tick);
             BFT_STAMP(7);
             if (act && !resuming) t_step();
@@ -1231,7 +1231,7 @@ struct Sim {
             const uint32_t pstart = resuming ? p0 : 0u;
             resuming = false;
             for (uint32_t p = pstart;; ++p) {
-                bool pend_l = act && !frozen && pending_local();
+                bool pend_l = act & !frozen & pending_local();
                 M bal = ballot(pend_l);
                 if (bal.none()) break;
                 bool seg_pending = (bal & seg_mask).any();
@@ -1258,7 +1258,7 @@ struct Sim {
                 if (pub) { publish(); sync(); }
                 else outbox_clear(nx);
                 BFT_STAMP(2);
-                if (act && seg_pending) {
+                if (act & seg_pending) {
                     miner_step();                             // event step
                     M mk = deliver_mask<NW>(P.seed, nval(), P.thr16, inst, (uint32_t)tick, p, me);
                     uint32_t off = (path == PATH_GENERAL || path == PATH_PC)
