@@ -19,7 +19,7 @@
 //   the locked block itself), `pend` is None or (h, me, 0, T);
 // * a Core commit is `pp` at round 0: one flag bit.
 // That leaves ~25 live 32-bit values per lane (the general body keeps ~90), so the kernel runs without
-// spills at 8 waves per SIMD, and the phase logic is short, mostly branch-free selects.
+// spills at 6 waves per SIMD (80 VGPRs), and the phase logic is short, mostly branch-free selects.
 #pragma once
 #include "bft_common.h"
 #include "bft_wave.h"
