@@ -32,8 +32,8 @@ struct F64Layout {
     static constexpr uint32_t CACHE_WORDS = 8;                 // 4 kinds (PP, PR, CM, old CM) x 2
     static constexpr uint32_t RING_OFF = CACHE_OFF + CACHE_WORDS * 64 * 4;   // 64 canonical rows x 16 B
     static constexpr uint32_t LAT_OFF = RING_OFF + 64 * 16;    // commit-latency histogram (65 words)
-    // cold per-lane state (SoA [word][lane]): sync_pending, rc_last_tick, pend's time tick, the outbox
-    // Preprepare's time tick, the lane's result flags — off the registers of the hot loop
+    // cold per-lane state (SoA [word][lane]): sync_pending, rc_last_tick, pend's time tick, (unused),
+    // the lane's result flags — off the registers of the hot loop
     static constexpr uint32_t LANE_OFF = LAT_OFF + 65 * 4 + 4;
     static constexpr uint32_t W_SYNC = 0, W_RCLT = 1, W_PENDT = 2, W_PPT = 3, W_LFL = 4, LANE_WORDS = 5;
     static constexpr uint32_t BYTES = LANE_OFF + LANE_WORDS * 64 * 4;
@@ -60,6 +60,7 @@ struct Fast64 {
     uint32_t canon_h, canon_tick, done_tick, seg_flags, flushed;
     uint64_t canon_tip, views_acc;
     uint64_t byz_mask;                 // Byzantine validators of this instance (SPEC.md §6)
+    uint32_t pp_T_out;                 // time tick of validator 0's outbox Preprepare
     int32_t tick;
     // per lane (Core + RoundState + chain tip + miner + timers + outbox)
     uint32_t fl;                       // L_* bits; state in bits 0..2
@@ -90,7 +91,7 @@ struct Fast64 {
         seg_done = !inst_ok;
         frozen = false;
         canon_h = 0; canon_tick = 0; done_tick = p.max_ticks; seg_flags = 0; flushed = 0;
-        canon_tip = 0; views_acc = 0; byz_mask = 0;
+        canon_tip = 0; views_acc = 0; byz_mask = 0; pp_T_out = 0;
         tick = 0;
         h = 0; pp = BLK_NONE; prep = comm = 0;
         cand_T = 0; last = 0;
@@ -174,7 +175,8 @@ struct Fast64 {
     }
     BFT_FN void out_preprepare_p(bool c) {                       // view (h, 0), own candidate; equivocates iff Byzantine
         const bool put = send_kind(c, 0, h, cand(), F_PP, F_PP_EQ);
-        if (put) *lane_p(F64Layout::W_PPT) = cand_T;
+        // only validator 0 proposes here: its Preprepare's time tick is kept wave-uniform (SGPR)
+        if (ballot(put) != 0) pp_T_out = uni(rl(cand_T, 0));
     }
     BFT_FN void out_prepare_p(bool c) { send_kind(c, 1, h, pp, F_PR, F_PR_W); }   // (h, 0, pp)
     BFT_FN void out_commit_p(bool c) { send_kind(c, 2, h, pp, F_CM, F_CM_W); }
@@ -553,7 +555,7 @@ struct Fast64 {
         const uint64_t lock = has(L_LOCK) ? pp : BLK_NONE;
         const uint64_t pend = has(L_PENDV) ? blk_make(h, me, 0, *lane_p(F64Layout::W_PENDT)) : BLK_NONE;
         const uint64_t cd = mint_height ? cand() : BLK_NONE;
-        const uint64_t ppb = blk_make(h, me, 0, *lane_p(F64Layout::W_PPT));
+        const uint64_t ppb = blk_make(h, me, 0, pp_T_out);     // read only where F_PP is set (lane 0)
         const uint32_t w32[29] = {h, 0u, st(), 0u, proposer(), last, 0u, (uint32_t)last_T, (uint32_t)timer_tick,
                                   *lane_p(F64Layout::W_RCLT), (uint32_t)wake_tick, mint_height, miner_queue,
                                   *lane_p(F64Layout::W_SYNC), lane_flags(), canon_h, done_tick, seg_flags, 0u, canon_tick, nxf,
@@ -651,7 +653,7 @@ struct Fast64 {
                 c.cm_cls = rl64(cls, jc);
                 c.v1 = ballot(blk_var(pp) != 0);
                 const uint32_t pp_h = uni(rl(h, j));
-                const uint32_t pp_T = uni(rl(*lane_p(F64Layout::W_PPT), j));
+                const uint32_t pp_T = pp_T_out;
                 const uint32_t pp_eq = uni(rl(f & F_PP_EQ, j));
                 const uint32_t blo = uni(rl(nx_blo, jb)), bhi = uni(rl(nx_bhi, jb));
                 uint32_t path;
