@@ -46,7 +46,8 @@ struct Fast64 {
     // lane flag bits
     static constexpr uint32_t L_ST = 7u, L_WAIT = 8u, L_LOCK = 16u, L_BYZ = 32u, L_RUN = 64u, L_DEAD = 128u,
                               L_PENDV = 256u, L_CMT = 512u, L_PROP = 1024u,   // L_PROP: proposer is set (= 0)
-                              L_OBX = 2048u;   // FLAG_OUTBOX of this lane (a second message of a kind in one phase)
+                              L_OBX = 2048u,   // FLAG_OUTBOX of this lane (a second message of a kind in one phase)
+                              L_SYNCP = 4096u; // W_SYNC (the delayed sync check's height) is nonzero
     enum : uint32_t { P_GENERAL = 0, P_BLK = 1, P_PC = 2, P_PP = 3, P_NONE = 4 };
 
     const Params& P;
@@ -336,11 +337,12 @@ struct Fast64 {
         wake_tick = w ? -1 : wake_tick;
         if (ballot(w) != 0) handle_new_header_event_p(w);
         if (ballot(miner_event() != 0) != 0) miner_step_p();
-        const uint32_t spv = *lane_p(F64Layout::W_SYNC);
-        const bool sp = run & (spv != 0);
+        const bool sp = run & has(L_SYNCP);
         if (ballot(sp) != 0) {
+            const uint32_t spv = *lane_p(F64Layout::W_SYNC);
             if (sp & (last < spv)) out_sync(last + 1);
             if (sp) *lane_p(F64Layout::W_SYNC) = 0;
+            fl &= sp ? ~L_SYNCP : ~0u;
         }
         const bool tm = run & !has(L_DEAD) & (timer_tick == tick);  // TimerEvent (core.rs:207-225)
         if (ballot(tm) != 0) {
@@ -453,6 +455,7 @@ struct Fast64 {
                 v = (fpr & (c.pr_h > v)) ? c.pr_h : v;
                 v = (fcm & (c.cm_h > v)) ? c.cm_h : v;
                 *lane_p(F64Layout::W_SYNC) = v;
+                fl |= L_SYNCP;                                   // v > h >= 1
             }
         }
         // digests matching the own pp (class_match_k): a Byzantine sender's wildcard matches both variants
@@ -621,7 +624,7 @@ struct Fast64 {
             // the T-step, only when some running validator has a tick event
             // (a validator that is not running has no events: wake_tick, timer_tick -1, nothing queued)
             if (tick == 0 || ballot((wake_tick == tick) | ((wake_tick < 0) & (miner_queue != 0)) |
-                                    (*lane_p(F64Layout::W_SYNC) != 0) | (!has(L_DEAD) & (timer_tick == tick))) != 0) {
+                                    has(L_SYNCP) | (!has(L_DEAD) & (timer_tick == tick))) != 0) {
                 t_step();
             }
             F64_STAMP(0);
@@ -698,7 +701,7 @@ struct Fast64 {
                 F64_COUNT(8);
                 if (act) {
                     // event step: Minner's NewHeader handler, for the validators with queued chain events
-                    if (ballot(miner_event() != 0) != 0) miner_step_p();
+                    miner_step_p();   // a no-op for lanes without a queued event (miner_step_p guards the mining)
                     F64_STAMP(2);
                     if (path != P_NONE) {
                         const uint64_t mk = deliver_mask<1>(seed(), N, P.thr16, inst, (uint32_t)tick, p, me).w[0];
