@@ -40,7 +40,9 @@ struct F64Layout {
 };
 constexpr uint32_t lds_bytes_fast64() { return F64Layout::BYTES; }
 
-template <class W>
+// LOSSY = false: the schedule has no link drops and no proposer crashes (thr16 == 0, crash_on == 0,
+// e.g. cfg3), so every delivery mask is all ones at compile time
+template <class W, bool LOSSY = true>
 struct Fast64 {
     static constexpr uint32_t N = 64, Q = 42;   // floor(2N/3) (validator.rs:149-154)
     // lane flag bits
@@ -292,7 +294,7 @@ struct Fast64 {
         const bool s = c & (h == mint_height) & has(L_PROP) & (me == 0);
         if (ballot(s) != 0) {                                    // the proposer (validator 0) proposes
             bool cr = false;
-            if (P.crash_on) cr = proposer_crashed(seed(), P.crash_thr32, 1u, inst, h, 0);
+            if (LOSSY && P.crash_on) cr = proposer_crashed(seed(), P.crash_thr32, 1u, inst, h, 0);
             out_preprepare_p(s & !cr);
         }
     }
@@ -704,7 +706,8 @@ struct Fast64 {
                     miner_step_p();   // a no-op for lanes without a queued event (miner_step_p guards the mining)
                     F64_STAMP(2);
                     if (path != P_NONE) {
-                        const uint64_t mk = deliver_mask<1>(seed(), N, P.thr16, inst, (uint32_t)tick, p, me).w[0];
+                        const uint64_t mk = LOSSY ? deliver_mask<1>(seed(), N, P.thr16, inst, (uint32_t)tick, p, me).w[0]
+                                                  : ~0ull;
                         if (path == P_PC) {
                             const uint32_t off = offset_from_parts(seed(), N, off_tick, p, me);
                             deliver_pc(has(L_RUN) & !has(L_DEAD), c, mk, off);

@@ -10,6 +10,7 @@ namespace bft {
 #ifndef BFT_FAST_WAVES_PER_SIMD
 #define BFT_FAST_WAVES_PER_SIMD 6   // measured best of 4..8 (profiles/r02: 4 → 3.86e8, 5 → 3.97e8, 6 → 4.17e8, 7 → 3.69e8)
 #endif
+template <bool LOSSY>
 __global__ __launch_bounds__(64, BFT_FAST_WAVES_PER_SIMD) void bft_consensus_fast_kernel(Params p) {
     extern __shared__ uint8_t lds[];
 #ifndef BFT_CONSENSUS_PRIO
@@ -18,11 +19,15 @@ __global__ __launch_bounds__(64, BFT_FAST_WAVES_PER_SIMD) void bft_consensus_fas
     // win issue arbitration against the hash waves of the previous launch (the hash pass stretches into
     // the issue gaps and still finishes within the step)
     __builtin_amdgcn_s_setprio(BFT_CONSENSUS_PRIO);
-    Fast64<WaveHip> sim(p, lds, blockIdx.x);
+    Fast64<WaveHip, LOSSY> sim(p, lds, blockIdx.x);
     sim.run();
 }
 hipError_t launch_fast(dim3 grid, hipStream_t s, const Params& p) {
-    hipLaunchKernelGGL(bft_consensus_fast_kernel, grid, dim3(64), lds_bytes_fast64(), s, p);
+    // the lossless build for schedules without drops and proposer crashes (cfg3): masks are constants
+    if (p.thr16 == 0 && p.crash_on == 0)
+        hipLaunchKernelGGL(bft_consensus_fast_kernel<false>, grid, dim3(64), lds_bytes_fast64(), s, p);
+    else
+        hipLaunchKernelGGL(bft_consensus_fast_kernel<true>, grid, dim3(64), lds_bytes_fast64(), s, p);
     return hipGetLastError();
 }
 

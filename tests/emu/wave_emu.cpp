@@ -116,8 +116,13 @@ template <bool NS, uint32_t S>
 void run_sim() {
     if constexpr (S == 64 && !NS) {
         if (g->fast) {                     // bft_consensus_fast_kernel
-            bft::Fast64<EmuWave> sim(*g->P, g->lds, g->wave);
-            sim.run();
+            if (g->P->thr16 == 0 && g->P->crash_on == 0) {   // the lossless build, as launch_fast picks
+                bft::Fast64<EmuWave, false> sim(*g->P, g->lds, g->wave);
+                sim.run();
+            } else {
+                bft::Fast64<EmuWave, true> sim(*g->P, g->lds, g->wave);
+                sim.run();
+            }
             return;
         }
         if (g->P->resume_mode) {           // bft_consensus_resume_kernel
