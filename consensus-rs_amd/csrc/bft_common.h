@@ -331,6 +331,25 @@ BFT_FN bool proposer_crashed(uint64_t seed, uint32_t thr32, uint32_t on, uint32_
 BFT_FN uint64_t rotl64(uint64_t x, int n) { return (x << n) | (x >> (64 - n)); }
 
 BFT_FN void keccak_f1600_u64(uint64_t a[25]);
+// the round constants as 32-bit halves: a constant-memory table on the device (a local array indexed
+// in the round loop would be copied into scratch memory at every call)
+#if defined(__HIP_DEVICE_COMPILE__)
+__constant__ static const uint32_t KECCAK_RC_LO[24] = {
+    0x00000001u, 0x00008082u, 0x0000808Au, 0x80008000u, 0x0000808Bu, 0x80000001u, 0x80008081u, 0x00008009u,
+    0x0000008Au, 0x00000088u, 0x80008009u, 0x8000000Au, 0x8000808Bu, 0x0000008Bu, 0x00008089u, 0x00008003u,
+    0x00008002u, 0x00000080u, 0x0000800Au, 0x8000000Au, 0x80008081u, 0x00008080u, 0x80000001u, 0x80008008u};
+__constant__ static const uint32_t KECCAK_RC_HI[24] = {
+    0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0u, 0u, 0u, 0x80000000u,
+    0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u};
+#else
+static const uint32_t KECCAK_RC_LO[24] = {
+    0x00000001u, 0x00008082u, 0x0000808Au, 0x80008000u, 0x0000808Bu, 0x80000001u, 0x80008081u, 0x00008009u,
+    0x0000008Au, 0x00000088u, 0x80008009u, 0x8000000Au, 0x8000808Bu, 0x0000008Bu, 0x00008089u, 0x00008003u,
+    0x00008002u, 0x00000080u, 0x0000800Au, 0x8000000Au, 0x80008081u, 0x00008080u, 0x80000001u, 0x80008008u};
+static const uint32_t KECCAK_RC_HI[24] = {
+    0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0u, 0u, 0u, 0x80000000u,
+    0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u};
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
 __host__ inline void keccak_f1600(uint64_t a[25]) { keccak_f1600_u64(a); }
 // gfx950 form: the state as 32-bit halves; rotations are two v_alignbit_b32 (funnel shifts),
@@ -344,13 +363,6 @@ __device__ inline void rotl_halves(uint32_t lo, uint32_t hi, uint32_t& ol, uint3
     else { oh = __builtin_amdgcn_alignbit(lo, hi, 64 - N); ol = __builtin_amdgcn_alignbit(hi, lo, 64 - N); }
 }
 __device__ inline void keccak_f1600(uint64_t a[25]) {
-    const uint32_t RCL[24] = {
-        0x00000001u, 0x00008082u, 0x0000808Au, 0x80008000u, 0x0000808Bu, 0x80000001u, 0x80008081u, 0x00008009u,
-        0x0000008Au, 0x00000088u, 0x80008009u, 0x8000000Au, 0x8000808Bu, 0x0000008Bu, 0x00008089u, 0x00008003u,
-        0x00008002u, 0x00000080u, 0x0000800Au, 0x8000000Au, 0x80008081u, 0x00008080u, 0x80000001u, 0x80008008u};
-    const uint32_t RCH[24] = {
-        0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0u, 0u, 0u, 0x80000000u,
-        0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u};
     uint32_t L[25], H[25];
 #pragma unroll
     for (int i = 0; i < 25; ++i) { L[i] = (uint32_t)a[i]; H[i] = (uint32_t)(a[i] >> 32); }
@@ -385,8 +397,8 @@ __device__ inline void keccak_f1600(uint64_t a[25]) {
                 L[5 * y + x] = bl[5 * y + x] ^ (~bl[5 * y + (x + 1) % 5] & bl[5 * y + (x + 2) % 5]);
                 H[5 * y + x] = bh[5 * y + x] ^ (~bh[5 * y + (x + 1) % 5] & bh[5 * y + (x + 2) % 5]);
             }
-        L[0] ^= RCL[rnd];
-        H[0] ^= RCH[rnd];
+        L[0] ^= KECCAK_RC_LO[rnd];
+        H[0] ^= KECCAK_RC_HI[rnd];
     }
 #pragma unroll
     for (int i = 0; i < 25; ++i) a[i] = (uint64_t)L[i] | ((uint64_t)H[i] << 32);

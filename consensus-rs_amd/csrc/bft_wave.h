@@ -124,6 +124,8 @@ struct Sim {
     // the opt-in modes (backlog replay, real-crypto log and votes) exist only in MODE_EXT builds, so
     // the product kernels carry none of their code or registers
     static constexpr bool EXT = MODE == MODE_EXT;
+    // the wave-cooperative header hash of closed-form commits (resolve_deferred_hash)
+    static constexpr bool WAVE_HASH = NEED_SEED && S == 64 && MODE == MODE_FULL;
     static_assert(MODE != MODE_RESUME || S == 64, "hand-over modes are for one instance per wave");
     using LY = Layout<S>;
     static constexpr int NW = LY::NW;
@@ -166,6 +168,9 @@ struct Sim {
     uint32_t commit_x, commit_round, commit_seed;
     uint32_t off_inst, off_tick;     // hoisted parts of delivery_offset (SPEC.md §3)
     uint64_t commit_blk;
+    // (S == 64, NEED_SEED, MODE_FULL) a Core commit of the Prepare/Commit closed form whose header hash
+    // is computed after the delivery by the whole wave (resolve_deferred_hash)
+    bool hash_defer, in_pc;
     uint32_t lane_flags;
     uint32_t* rcs_base;      // this wave's RoundChangeSet table (global)
     uint32_t* bl_base;       // this wave's backlog slots (global, replay mode)
@@ -212,6 +217,7 @@ struct Sim {
         for (uint32_t k = 0; k < 12; ++k) *cache_p(k) = 0;
         outbox_init(nx);
         commit_x = 0; commit_round = 0; commit_seed = 0; commit_blk = 0;
+        hash_defer = false; in_pc = false;
         mlog_cnt = 0;
         lane_flags = 0;
         off_inst = offset_inst_part(p.seed, inst);
@@ -231,6 +237,138 @@ struct Sim {
     BFT_FN void check_window(uint32_t x) {
         if (P.window_mask && x + P.window_mask < canon_h) lane_flags |= FLAG_WINDOW;
     }
+    // ---------------------------------------------------------------- the wave's Keccak (S == 64)
+    // Keccak-f[1600] spread over lanes 0..24: lane x + 5y holds state word A[x][y] as two 32-bit halves
+    // (lanes 25..63 shadow lane 0; their results are never read). Every lane of the wave calls it:
+    // 18 shuffles and ~25 ALU instructions per round, against ~190 with the whole state in one lane.
+    // Rho amounts per source lane and, per destination lane, the source of pi (B[y][2x+3y] = rot(A[x][y]),
+    // the same table as bft_hash_pair_kernel), packed 10 / 12 entries per word.
+    BFT_FN static uint32_t kw_rot(uint32_t l) {
+        const uint64_t R0 = 0ull | 1ull << 6 | 62ull << 12 | 28ull << 18 | 27ull << 24 | 36ull << 30 | 44ull << 36 |
+                            6ull << 42 | 55ull << 48 | 20ull << 54;
+        const uint64_t R1 = 3ull | 10ull << 6 | 43ull << 12 | 25ull << 18 | 39ull << 24 | 41ull << 30 | 45ull << 36 |
+                            15ull << 42 | 21ull << 48 | 8ull << 54;
+        const uint64_t R2 = 18ull | 2ull << 6 | 61ull << 12 | 56ull << 18 | 14ull << 24;
+        const uint64_t w = l < 10u ? R0 : (l < 20u ? R1 : R2);
+        return (uint32_t)(w >> (6u * (l % 10u))) & 63u;
+    }
+    BFT_FN static uint32_t kw_src(uint32_t l) {      // SRC[j] = the lane whose rotated word lands in lane j
+        const uint64_t S0 = 0ull | 6ull << 5 | 12ull << 10 | 18ull << 15 | 24ull << 20 | 3ull << 25 | 9ull << 30 |
+                            10ull << 35 | 16ull << 40 | 22ull << 45 | 1ull << 50 | 7ull << 55;
+        const uint64_t S1 = 13ull | 19ull << 5 | 20ull << 10 | 4ull << 15 | 5ull << 20 | 11ull << 25 | 17ull << 30 |
+                            23ull << 35 | 2ull << 40 | 8ull << 45 | 14ull << 50 | 15ull << 55;
+        const uint64_t S2 = 21ull;
+        const uint64_t w = l < 12u ? S0 : (l < 24u ? S1 : S2);
+        return (uint32_t)(w >> (5u * (l % 12u))) & 31u;
+    }
+    BFT_FN static void rotl64_halves(uint32_t lo, uint32_t hi, uint32_t n, uint32_t& ol, uint32_t& oh) {
+        const uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+        const uint64_t r = n ? ((v << n) | (v >> (64u - n))) : v;
+        ol = (uint32_t)r; oh = (uint32_t)(r >> 32);
+    }
+    BFT_FN void keccak_wave(uint32_t& lo, uint32_t& hi) {
+        const uint32_t l = lane < 25u ? lane : 0u;
+        const uint32_t x = l % 5u, yb = l - x;                     // yb = 5y
+        const uint32_t rot = kw_rot(l), src = kw_src(l);
+        const uint32_t xm = (x + 4u) % 5u, xp = (x + 1u) % 5u, xpp = (x + 2u) % 5u;
+#pragma unroll 1
+        for (int rnd = 0; rnd < 24; ++rnd) {
+            // theta: column parities C[x], then D[x] = C[x-1] ^ rotl(C[x+1], 1)
+            uint32_t cl = lo, ch = hi;
+#pragma unroll
+            for (uint32_t k = 5; k < 25; k += 5) {
+                const uint32_t j = (x + yb + k) % 25u;
+                cl ^= wv.shfl(lo, j);
+                ch ^= wv.shfl(hi, j);
+            }
+            const uint32_t aml = wv.shfl(cl, xm), amh = wv.shfl(ch, xm);
+            const uint32_t apl = wv.shfl(cl, xp), aph = wv.shfl(ch, xp);
+            uint32_t rl, rh;
+            rotl64_halves(apl, aph, 1u, rl, rh);
+            lo ^= aml ^ rl;
+            hi ^= amh ^ rh;
+            // rho at the source, pi as a shuffle
+            uint32_t tl, th;
+            rotl64_halves(lo, hi, rot, tl, th);
+            const uint32_t bl = wv.shfl(tl, src), bh = wv.shfl(th, src);
+            // chi: A[x][y] = B[x][y] ^ (~B[x+1][y] & B[x+2][y])
+            const uint32_t b1l = wv.shfl(bl, yb + xp), b1h = wv.shfl(bh, yb + xp);
+            const uint32_t b2l = wv.shfl(bl, yb + xpp), b2h = wv.shfl(bh, yb + xpp);
+            lo = bl ^ (~b1l & b2l);
+            hi = bh ^ (~b1h & b2h);
+            const bool l0 = lane == 0u;                        // iota
+            lo ^= l0 ? KECCAK_RC_LO[rnd] : 0u;
+            hi ^= l0 ? KECCAK_RC_HI[rnd] : 0u;
+        }
+    }
+    // Keccak-256 of the header of canonical-parent block b at height x by the whole wave; the header is
+    // encoded by lane `enc` into its scratch buffer. Returns the 8 hash words in every lane.
+    BFT_FN void wave_block_hash(uint32_t enc, uint32_t x, uint64_t b, uint32_t out[8]) {
+        uint64_t* wb = (uint64_t*)(lds + LDS_SCR_OFF + enc * LANE_HASH_BUF);
+        uint32_t nb = 0;
+        if (lane == enc) {
+            uint32_t prev[8];
+            prev_hash_words(x - 1u, prev);
+            const uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
+            nb = header_words(wb, prev, P.addresses + 20u * blk_prop(b), P.seed, inst, x, blk_prop(b), blk_var(b), time);
+        }
+        nb = wv.readlane(nb, enc);
+        sync();
+        uint32_t lo = 0, hi = 0;
+        for (uint32_t blk = 0; blk < nb; ++blk) {
+            if (lane < 17u) {
+                const uint64_t w = wb[17u * blk + lane];
+                lo ^= (uint32_t)w;
+                hi ^= (uint32_t)(w >> 32);
+            }
+            keccak_wave(lo, hi);
+        }
+        sync();
+        for (uint32_t i = 0; i < 4u; ++i) {
+            out[2 * i] = wv.readlane(lo, i);
+            out[2 * i + 1] = wv.readlane(hi, i);
+        }
+    }
+    // the deferred hashes of this phase's closed-form Core commits: one wave hash for the first
+    // committer's block, taken by every committer of the same block; any other block by its own lane
+    BFT_FN void resolve_deferred_hash() {
+        const bool pend = hash_defer;
+        const M pb = ballot(pend);
+        if (pb.none()) return;
+        hash_defer = false;
+        const uint32_t lead = pb.ctz_nz();
+        const uint32_t x0 = wv.readlane(commit_x, lead);
+        const uint64_t b0 = (uint64_t)wv.readlane((uint32_t)commit_blk, lead) |
+                            ((uint64_t)wv.readlane((uint32_t)(commit_blk >> 32), lead) << 32);
+        uint32_t out[8];
+        wave_block_hash(lead, x0, b0, out);
+        // the same height and block id (time tick included) is the same header: the parent is the
+        // canonical block x0 - 1 for every lane (chain_insert_core inserts x only on top of x - 1)
+        const bool same = pend & (commit_x == x0) & (commit_blk == b0);
+        if (same) {
+            uint32_t* hs = (uint32_t*)(lds + LDS_CHASH_OFF + lane * 32);
+            for (int i = 0; i < 8; ++i) hs[i] = out[i];
+            const uint32_t sd = seed_from_words(out[0], out[1], nval(), P.seed_le != 0);
+            commit_seed = sd;
+            last_seed = sd;
+        }
+        if (pend & !same) {
+            uint32_t prev[8], o[8];
+            const uint64_t b = commit_blk;
+            const uint32_t x = commit_x;
+            prev_hash_words(x - 1u, prev);
+            const uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
+            lane_block_hash(lds + LDS_SCR_OFF + lane * LANE_HASH_BUF, prev, P.addresses + 20u * blk_prop(b),
+                            P.seed, inst, x, blk_prop(b), blk_var(b), time, o);
+            uint32_t* hs = (uint32_t*)(lds + LDS_CHASH_OFF + lane * 32);
+            for (int i = 0; i < 8; ++i) hs[i] = o[i];
+            const uint32_t sd = seed_from_words(o[0], o[1], nval(), P.seed_le != 0);
+            commit_seed = sd;
+            last_seed = sd;
+        }
+        sync();
+    }
+
     BFT_FN uint32_t canon_seed(uint32_t x) {
         if (x == 0) return P.genesis_seed;
         if (x == canon_h) return canon_tip_seed;
@@ -339,7 +477,11 @@ struct Sim {
 #endif
         }
         uint32_t sd = 0;
-        if (NEED_SEED) {
+        if (WAVE_HASH && in_pc) {
+            // the closed form delivers the whole phase: nothing reads this commit's hash or seed before
+            // resolve_commits, and resolve_deferred_hash runs just before it
+            hash_defer = true;
+        } else if (NEED_SEED) {
             uint32_t prev[8], out[8];
             prev_hash_words(last, prev);
             uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
@@ -1136,7 +1278,7 @@ struct Sim {
         prep |= PRacc;
         comm |= CMacc;
         if (trig) { lock_hash(); send_commit(); }
-        if (fires) { lock_hash(); st = ST_COMMITTED; chain_insert_core(pp); }
+        if (fires) { lock_hash(); st = ST_COMMITTED; in_pc = true; chain_insert_core(pp); in_pc = false; }
         st = fin;
     }
 
@@ -1268,6 +1410,7 @@ struct Sim {
                 }
                 if (pub) sync();                              // records read before the next publish
                 BFT_STAMP(3);
+                if constexpr (WAVE_HASH) resolve_deferred_hash();
                 resolve_commits();
                 BFT_STAMP(4);
                 if (frozen) act = false;
