@@ -683,22 +683,6 @@ struct Fast64 {
                     break;
                 }
                 nxf = 0;
-#ifdef BFT_AB_SALU
-                {   // diagnostic: BFT_AB_SALU dependent-free scalar adds per phase (issue-bound probe)
-                    uint32_t d0 = __builtin_amdgcn_readfirstlane(tick), d1 = __builtin_amdgcn_readfirstlane(p);
-#pragma unroll
-                    for (int q = 0; q < BFT_AB_SALU; ++q) asm volatile("s_add_u32 %0, %0, 1\n s_add_u32 %1, %1, 1" : "+s"(d0), "+s"(d1));
-                    asm volatile("" :: "s"(d0), "s"(d1));
-                }
-#endif
-#ifdef BFT_AB_VALU
-                {
-                    uint32_t d0 = me, d1 = me + 1;
-#pragma unroll
-                    for (int q = 0; q < BFT_AB_VALU; ++q) asm volatile("v_add_u32 %0, 1, %0\n v_add_u32 %1, 1, %1" : "+v"(d0), "+v"(d1));
-                    asm volatile("" :: "v"(d0), "v"(d1));
-                }
-#endif
                 F64_STAMP(1);
                 F64_COUNT(8);
                 if (act) {
