@@ -17,6 +17,14 @@ struct WaveHip {
     __device__ static uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
     __device__ static uint32_t shfl_xor(uint32_t v, int m) { return (uint32_t)__shfl_xor((int)v, m, 64); }
     __device__ static uint32_t shfl(uint32_t v, uint32_t src) { return (uint32_t)__shfl((int)v, (int)src, 64); }
+    // DPP moves inside 16-lane rows: lane i gets lane i + N (row_shl) / i - N (row_shr); lanes whose
+    // source is outside the row get 0
+    template <int N> __device__ static uint32_t row_shl(uint32_t v) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x100 + N, 0xF, 0xF, true);
+    }
+    template <int N> __device__ static uint32_t row_shr(uint32_t v) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x110 + N, 0xF, 0xF, true);
+    }
     __device__ static uint32_t readlane(uint32_t v, uint32_t l) {      // l wave-uniform
         return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_amdgcn_readfirstlane((int)l));
     }

@@ -238,51 +238,57 @@ struct Sim {
         if (P.window_mask && x + P.window_mask < canon_h) lane_flags |= FLAG_WINDOW;
     }
     // ---------------------------------------------------------------- the wave's Keccak (S == 64)
-    // Keccak-f[1600] spread over lanes 0..24: lane x + 5y holds state word A[x][y] as two 32-bit halves
-    // (lanes 25..63 shadow lane 0; their results are never read). Every lane of the wave calls it:
-    // 18 shuffles and ~25 ALU instructions per round, against ~190 with the whole state in one lane.
-    // Rho amounts per source lane and, per destination lane, the source of pi (B[y][2x+3y] = rot(A[x][y]),
-    // the same table as bft_hash_pair_kernel), packed 10 / 12 entries per word.
-    BFT_FN static uint32_t kw_rot(uint32_t l) {
+    // Keccak-f[1600] spread over the wave: lane x + 8y (x, y < 5) holds state word A[x][y] = word x + 5y
+    // as two 32-bit halves, so each row y sits in one 16-lane DPP row. Theta's column parities and pi
+    // are ds_bpermute shuffles; the x-neighbours of D and chi are DPP row shifts (wrap-around by a
+    // second shift and a select). Lanes with x or y >= 5 compute garbage that no valid lane reads.
+    // Every lane of the wave calls it. Rho amounts per word and, per destination word, the source word
+    // of pi (B[y][2x+3y] = rot(A[x][y]), the table of bft_hash_pair_kernel), packed 10 / 12 per u64.
+    BFT_FN static uint32_t kw_rot(uint32_t w) {
         const uint64_t R0 = 0ull | 1ull << 6 | 62ull << 12 | 28ull << 18 | 27ull << 24 | 36ull << 30 | 44ull << 36 |
                             6ull << 42 | 55ull << 48 | 20ull << 54;
         const uint64_t R1 = 3ull | 10ull << 6 | 43ull << 12 | 25ull << 18 | 39ull << 24 | 41ull << 30 | 45ull << 36 |
                             15ull << 42 | 21ull << 48 | 8ull << 54;
         const uint64_t R2 = 18ull | 2ull << 6 | 61ull << 12 | 56ull << 18 | 14ull << 24;
-        const uint64_t w = l < 10u ? R0 : (l < 20u ? R1 : R2);
-        return (uint32_t)(w >> (6u * (l % 10u))) & 63u;
+        const uint64_t v = w < 10u ? R0 : (w < 20u ? R1 : R2);
+        return (uint32_t)(v >> (6u * (w % 10u))) & 63u;
     }
-    BFT_FN static uint32_t kw_src(uint32_t l) {      // SRC[j] = the lane whose rotated word lands in lane j
+    BFT_FN static uint32_t kw_src(uint32_t w) {      // the word whose rotated value lands in word w
         const uint64_t S0 = 0ull | 6ull << 5 | 12ull << 10 | 18ull << 15 | 24ull << 20 | 3ull << 25 | 9ull << 30 |
                             10ull << 35 | 16ull << 40 | 22ull << 45 | 1ull << 50 | 7ull << 55;
         const uint64_t S1 = 13ull | 19ull << 5 | 20ull << 10 | 4ull << 15 | 5ull << 20 | 11ull << 25 | 17ull << 30 |
                             23ull << 35 | 2ull << 40 | 8ull << 45 | 14ull << 50 | 15ull << 55;
         const uint64_t S2 = 21ull;
-        const uint64_t w = l < 12u ? S0 : (l < 24u ? S1 : S2);
-        return (uint32_t)(w >> (5u * (l % 12u))) & 31u;
+        const uint64_t v = w < 12u ? S0 : (w < 24u ? S1 : S2);
+        return (uint32_t)(v >> (5u * (w % 12u))) & 31u;
     }
     BFT_FN static void rotl64_halves(uint32_t lo, uint32_t hi, uint32_t n, uint32_t& ol, uint32_t& oh) {
         const uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
         const uint64_t r = n ? ((v << n) | (v >> (64u - n))) : v;
         ol = (uint32_t)r; oh = (uint32_t)(r >> 32);
     }
+    // A[x-1], A[x+1], A[x+2] of the same row y (x mod 5) by DPP
+    BFT_FN uint32_t xm1(uint32_t v, uint32_t x) { const uint32_t a = wv.template row_shr<1>(v), b = wv.template row_shl<4>(v); return x ? a : b; }
+    BFT_FN uint32_t xp1(uint32_t v, uint32_t x) { const uint32_t a = wv.template row_shl<1>(v), b = wv.template row_shr<4>(v); return x < 4u ? a : b; }
+    BFT_FN uint32_t xp2(uint32_t v, uint32_t x) { const uint32_t a = wv.template row_shl<2>(v), b = wv.template row_shr<3>(v); return x < 3u ? a : b; }
     BFT_FN void keccak_wave(uint32_t& lo, uint32_t& hi) {
-        const uint32_t l = lane < 25u ? lane : 0u;
-        const uint32_t x = l % 5u, yb = l - x;                     // yb = 5y
-        const uint32_t rot = kw_rot(l), src = kw_src(l);
-        const uint32_t xm = (x + 4u) % 5u, xp = (x + 1u) % 5u, xpp = (x + 2u) % 5u;
+        const uint32_t x = lane & 7u, y = lane >> 3;
+        const uint32_t w = (x < 5u && y < 5u) ? x + 5u * y : 0u;   // this lane's word
+        const uint32_t rot = kw_rot(w);
+        const uint32_t sw = kw_src(w), src = (sw % 5u) + 8u * (sw / 5u);
+        const uint32_t xc = x < 5u ? x : 0u;
 #pragma unroll 1
         for (int rnd = 0; rnd < 24; ++rnd) {
-            // theta: column parities C[x], then D[x] = C[x-1] ^ rotl(C[x+1], 1)
+            // theta: column parities C[x] (rows y' != y by shuffle), D[x] = C[x-1] ^ rotl(C[x+1], 1)
             uint32_t cl = lo, ch = hi;
 #pragma unroll
-            for (uint32_t k = 5; k < 25; k += 5) {
-                const uint32_t j = (x + yb + k) % 25u;
+            for (uint32_t k = 1; k < 5u; ++k) {
+                const uint32_t j = xc + 8u * ((y + k) % 5u);
                 cl ^= wv.shfl(lo, j);
                 ch ^= wv.shfl(hi, j);
             }
-            const uint32_t aml = wv.shfl(cl, xm), amh = wv.shfl(ch, xm);
-            const uint32_t apl = wv.shfl(cl, xp), aph = wv.shfl(ch, xp);
+            const uint32_t aml = xm1(cl, xc), amh = xm1(ch, xc);
+            const uint32_t apl = xp1(cl, xc), aph = xp1(ch, xc);
             uint32_t rl, rh;
             rotl64_halves(apl, aph, 1u, rl, rh);
             lo ^= aml ^ rl;
@@ -292,8 +298,8 @@ struct Sim {
             rotl64_halves(lo, hi, rot, tl, th);
             const uint32_t bl = wv.shfl(tl, src), bh = wv.shfl(th, src);
             // chi: A[x][y] = B[x][y] ^ (~B[x+1][y] & B[x+2][y])
-            const uint32_t b1l = wv.shfl(bl, yb + xp), b1h = wv.shfl(bh, yb + xp);
-            const uint32_t b2l = wv.shfl(bl, yb + xpp), b2h = wv.shfl(bh, yb + xpp);
+            const uint32_t b1l = xp1(bl, xc), b1h = xp1(bh, xc);
+            const uint32_t b2l = xp2(bl, xc), b2h = xp2(bh, xc);
             lo = bl ^ (~b1l & b2l);
             hi = bh ^ (~b1h & b2h);
             const bool l0 = lane == 0u;                        // iota
@@ -315,9 +321,10 @@ struct Sim {
         nb = wv.readlane(nb, enc);
         sync();
         uint32_t lo = 0, hi = 0;
+        const uint32_t kx = lane & 7u, word = kx + 5u * (lane >> 3);     // keccak_wave's layout
         for (uint32_t blk = 0; blk < nb; ++blk) {
-            if (lane < 17u) {
-                const uint64_t w = wb[17u * blk + lane];
+            if (kx < 5u && word < 17u) {
+                const uint64_t w = wb[17u * blk + word];
                 lo ^= (uint32_t)w;
                 hi ^= (uint32_t)(w >> 32);
             }

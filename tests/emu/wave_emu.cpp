@@ -69,6 +69,17 @@ struct EmuWave {
         return (uint32_t)g->res[l];
     }
     static uint32_t readlane(uint32_t v, uint32_t src) { return shfl(v, src); }
+    // DPP row_shl / row_shr (16-lane rows; a source outside the row reads 0)
+    template <int N> static uint32_t row_shl(uint32_t v) {
+        const uint32_t l = (uint32_t)g->cur, s = l + N;
+        const uint32_t r = shfl(v, s & 63u);
+        return (s >> 4) == (l >> 4) ? r : 0u;
+    }
+    template <int N> static uint32_t row_shr(uint32_t v) {
+        const uint32_t l = (uint32_t)g->cur, s = l - N;
+        const uint32_t r = shfl(v, s & 63u);
+        return (l >= (uint32_t)N && (s >> 4) == (l >> 4)) ? r : 0u;
+    }
     // readfirstlane on the GPU: here it checks that the value really is wave-uniform
     static uint32_t uni(uint32_t v) {
         uint32_t f = shfl(v, 0);
