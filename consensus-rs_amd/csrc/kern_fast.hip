@@ -126,8 +126,42 @@ __global__ __launch_bounds__(64) void bft_hash_pair_kernel(Params p) {
     }
 #endif
 }
+// one lane per instance, the whole Keccak state in that lane (32-bit halves): ~27 % fewer vector
+// instructions per header than the lane pair, at twice the chain latency. Used for large shards, where
+// the pass shares the GPU with the next launches' consensus kernels and instruction count is what it
+// costs them (profiles/r02/ab_s2: +1 % at 16,384 instances per GPU); small shards are bound by the
+// chain latency and keep the lane pair.
+__global__ __launch_bounds__(64) void bft_hash_lane_kernel(Params p) {
+    __shared__ __attribute__((aligned(16))) uint64_t bufs[64 * HDR_WORDS];
+    const uint32_t il = blockIdx.x * 64u + threadIdx.x;
+    if (il >= p.n_instances) return;
+    const uint32_t inst = p.first_instance + il;
+    const uint32_t ch = p.committed_height[il];
+    uint32_t prev[8];
+    for (int i = 0; i < 8; ++i)
+        prev[i] = (uint32_t)p.genesis_hash[4 * i] | ((uint32_t)p.genesis_hash[4 * i + 1] << 8) |
+                  ((uint32_t)p.genesis_hash[4 * i + 2] << 16) | ((uint32_t)p.genesis_hash[4 * i + 3] << 24);
+    uint8_t* buf = (uint8_t*)(bufs + threadIdx.x * HDR_WORDS);
+    for (uint32_t x = 1; x <= ch; ++x) {
+        const uint32_t* row = p.rec + ((uint64_t)il * p.rows + x) * 4;
+        const uint32_t w1 = row[1];
+        const uint32_t prop = w1 & 0xffffu, var = (w1 >> 16) & 1u, T = row[2];
+        const uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)T + 1ull);
+        uint32_t out[8];
+        lane_block_hash(buf, prev, p.addresses + 20u * prop, p.seed, inst, x, prop, var, time, out);
+        uint4* dst = (uint4*)(p.hash + ((uint64_t)il * p.rows + x) * 32);
+        dst[0] = make_uint4(out[0], out[1], out[2], out[3]);
+        dst[1] = make_uint4(out[4], out[5], out[6], out[7]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) prev[i] = out[i];
+    }
+}
+constexpr uint32_t HASH_LANE_MIN_INSTANCES = 8192;
 hipError_t launch_hash(dim3 grid, hipStream_t s, const Params& p) {
-    hipLaunchKernelGGL(bft_hash_pair_kernel, grid, dim3(64), 0, s, p);
+    if (p.n_instances >= HASH_LANE_MIN_INSTANCES)
+        hipLaunchKernelGGL(bft_hash_lane_kernel, dim3((p.n_instances + 63u) / 64u), dim3(64), 0, s, p);
+    else
+        hipLaunchKernelGGL(bft_hash_pair_kernel, grid, dim3(64), 0, s, p);
     return hipGetLastError();
 }
 
