@@ -512,12 +512,14 @@ struct Fast64 {
     }
 
     // ------------------------------------------------------------------ commits of a phase → canonical chain
-    BFT_FN void resolve_commits() {
+    // Returns the committed height when every committer of the phase committed the same one (each of
+    // them then has the block range [x0, x0] in its outbox, chain_insert_core_p), else 0.
+    BFT_FN uint32_t resolve_commits() {
         const bool c = has(L_CMT);
         const uint64_t bal = ballot(c);
-        if (bal == 0) return;
+        if (bal == 0) return 0;
         fl &= ~L_CMT;
-        if (seg_done) return;
+        if (seg_done) return 0;
         const uint32_t lead = ctz64(bal);
         const uint32_t x = blk_h(pp);
         const uint32_t x0 = uni(rl(x, lead));
@@ -531,7 +533,7 @@ struct Fast64 {
             if (!known && x0 < P.hcap && (!fr || ctz64(badm) > lead)) record_canon(x0, b0);
             if (x0 >= P.hcap) fr = true;
             if (fr) { frozen = true; seg_flags |= FLAG_SAFETY; }
-            return;
+            return x0;
         }
         // mixed heights: replay the commits in lane order (the oracle's receiver order)
         uint64_t bits = bal;
@@ -549,6 +551,7 @@ struct Fast64 {
             }
         }
         if (fr) { frozen = true; seg_flags |= FLAG_SAFETY; }
+        return 0;
     }
 
     // ------------------------------------------------------------------ hand-over to the full kernel
@@ -709,9 +712,24 @@ struct Fast64 {
                         }
                     }
                 }
-                resolve_commits();
+                const uint32_t xc = resolve_commits();
                 F64_STAMP(6);
                 if (frozen) act = false;
+                // The block gossip phase after a commit, fused. When a Prepare/Commit phase ends with
+                // every committer at height xc, the next phase would be a P_BLK phase with the range
+                // [xc, xc] (chain_insert_core_p); if nothing else is in flight and every running
+                // validator already has xc, handle_blocks_p is ChainError::Exists for all of them
+                // (core.rs:75-82) and that phase reduces to its event step. Same phase index, same
+                // miner step: bit-identical, without a second classification per height.
+                if ((path == P_PC) & (xc != 0) & act & (p + 1 < P.phase_cap)) {
+                    if (ballot(((nxf & ~F_BLK) != 0) | (has(L_RUN) & (last < xc))) == 0) {
+                        ++p;
+                        nxf = 0;
+                        miner_step_p();
+                        F64_COUNT(8);
+                        F64_COUNT(11);
+                    }
+                }
             }
             if (!seg_done && (frozen || canon_h >= P.heights)) { seg_done = true; done_tick = (uint32_t)tick + 1; }
         }

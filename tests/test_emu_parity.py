@@ -36,6 +36,12 @@ CASES = [
     ("n64-fast-handover-crash", lambda: BftConfig(n=64, heights=10, seed=22, drop_ppm=100_000,
                                                   proposer_crash_ppm=300_000), 0, 2),
     ("cfg4-n64", lambda: cfg4(64, heights=12), 0, 3),
+    # lossless N = 64 (the cfg3 shape): the FAST kernel's fused block-gossip phase, also with phase caps
+    # that end a tick right at (3) or just after (4) the commit phase
+    ("cfg3-40", lambda: cfg3(heights=40), 11, 4),
+    ("n64-honest-40", lambda: BftConfig(n=64, heights=40, seed=44), 0, 3),
+    ("n64-byz21-cap3", lambda: BftConfig(n=64, heights=20, seed=45, byz_count=21, phase_cap=3), 0, 3),
+    ("n64-byz21-cap4", lambda: BftConfig(n=64, heights=20, seed=46, byz_count=21, phase_cap=4), 0, 3),
     # f >= N/3 equivocators at N = 64: forks freeze instances (the S = 64 commit resolution's safety path)
     ("n64-byz32-fork", lambda: BftConfig(n=64, heights=12, seed=31, byz_count=32), 0, 4),
     ("n64-byz40-drop5-fork", lambda: BftConfig(n=64, heights=12, seed=31, byz_count=40, drop_ppm=50_000), 0, 3),
