@@ -646,10 +646,11 @@ struct Fast64 {
                 const uint32_t f = nxf;
                 // The phase after a height's T-step: validator 0's Preprepare alone in flight. Recognised
                 // from one ballot and one readlane; the same P_PP phase the classification below yields
-                // (kpp = {0}, no other kind, no cold kind), without its ballots and readlanes.
+                // (kpp = {0}, no other kind, no cold kind), without its ballots and readlanes. Lossless
+                // build only: in the lossy one the second copy of the delivery costs spills.
                 const uint64_t kany = ballot(f != 0);
                 const uint32_t f0 = uni(rl(f, 0));
-                if ((kany == 1ull) & ((f0 & ~(F_PP | F_PP_EQ)) == 0)) {
+                if (!LOSSY && (kany == 1ull) & ((f0 & ~(F_PP | F_PP_EQ)) == 0)) {
                     const uint32_t pp_h = uni(rl(h, 0)), pp_T = pp_T_out;   // as sent, before the event step
                     nxf = 0;
                     F64_STAMP(1);
