@@ -644,32 +644,6 @@ struct Fast64 {
                 // kind's first sender is read whether or not the kind is present, so no per-path values
                 // are merged at control-flow joins (those merges cost a copy of every live value).
                 const uint32_t f = nxf;
-                // The phase after a height's T-step: validator 0's Preprepare alone in flight. Recognised
-                // from one ballot and one readlane; the same P_PP phase the classification below yields
-                // (kpp = {0}, no other kind, no cold kind), without its ballots and readlanes. Lossless
-                // build only: in the lossy one the second copy of the delivery costs spills.
-                const uint64_t kany = ballot(f != 0);
-                const uint32_t f0 = uni(rl(f, 0));
-                if (!LOSSY && (kany == 1ull) & ((f0 & ~(F_PP | F_PP_EQ)) == 0)) {
-                    const uint32_t pp_h = uni(rl(h, 0)), pp_T = pp_T_out;   // as sent, before the event step
-                    nxf = 0;
-                    F64_STAMP(1);
-                    F64_COUNT(8);
-                    if (act) {
-                        miner_step_p();
-                        F64_STAMP(2);
-                        const uint64_t mk = LOSSY ? deliver_mask<1>(seed(), N, P.thr16, inst, (uint32_t)tick, p, me).w[0]
-                                                  : ~0ull;
-                        handle_preprepare_p(has(L_RUN) & ((mk & 1ull) != 0) & !has(L_DEAD), 0, pp_h,
-                                            blk_make(pp_h, 0, 0, pp_T), (f0 & F_PP_EQ) != 0);
-                        F64_STAMP(3);
-                        F64_COUNT(9);
-                    }
-                    resolve_commits();
-                    F64_STAMP(6);
-                    if (frozen) act = false;
-                    continue;
-                }
                 const bool pr = (f & F_PR) != 0, cm = (f & F_CM) != 0;
                 const uint64_t kpp = ballot((f & F_PP) != 0), kpr = ballot(pr), kcm = ballot(cm);
                 const uint64_t kblk = ballot((f & F_BLK) != 0);
