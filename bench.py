@@ -274,14 +274,14 @@ def main():
     st = sim.stats()
     # node-wide statistics: one RCCL all-reduce inside libbftsim (bftsim_stats_allreduce, over xGMI);
     # torch.distributed's all-reduce of the same counts only if librccl cannot be opened
-    try:
-        from bftsim.distributed import capi_comm_init
-        capi_comm_init(sim, rank, world)
+    # (the decision is collective: every rank takes the same branch, capi_comm_init)
+    from bftsim.distributed import capi_comm_init
+    if capi_comm_init(sim, rank, world):
         tot = sim.stats_allreduce()
         reduce_via = "libbftsim bftsim_stats_allreduce (RCCL)"
-    except Exception as e:                 # noqa: BLE001 — reported in the JSON line
+    else:
         tot = all_reduce_stats(st, device=dev)
-        reduce_via = f"torch.distributed (bftsim_stats_allreduce failed: {e})"
+        reduce_via = f"torch.distributed (libbftsim's RCCL communicator unavailable: {getattr(sim, 'comm_error', '')})"
     views_all, heights_all = tot["views"], tot["committed_heights"]
     safety_all, timeout_all = tot["flagged"][0], tot["flagged"][4]
 

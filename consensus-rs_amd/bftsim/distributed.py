@@ -45,14 +45,41 @@ def all_reduce_stats(st: Dict, device=None) -> Dict:
     return out
 
 
-def capi_comm_init(sim, rank: int, world: int):
+def capi_comm_init(sim, rank: int, world: int) -> bool:
     """Join `sim` to the node's RCCL communicator of libbftsim (bftsim_comm_init): rank 0 makes the id,
-    the default torch.distributed group carries it to the other ranks (any channel would do)."""
+    the default torch.distributed group carries it to the other ranks (any channel would do).
+
+    Collective and all-or-nothing: every rank returns the same answer, True only if every rank joined.
+    Rank 0 broadcasts a failure marker instead of the id when it cannot make one, and the ranks agree on
+    their join results with one MIN all-reduce, so no rank is left waiting in a collective that the
+    others skipped (they then all take the torch.distributed fallback of all_reduce_stats)."""
+    import torch
     import torch.distributed as dist
-    uid = [sim.comm_unique_id() if rank == 0 else None]
-    if world > 1:
-        dist.broadcast_object_list(uid, src=0)
-    sim.comm_init(world, rank, uid[0])
+    multi = world > 1 and dist.is_available() and dist.is_initialized()
+    uid, why = None, ""
+    if rank == 0:
+        try:
+            uid = sim.comm_unique_id()
+        except Exception as e:                     # noqa: BLE001 — reported by the caller
+            why = str(e)
+    box = [uid]
+    if multi:
+        dist.broadcast_object_list(box, src=0)
+    ok = box[0] is not None
+    if ok:
+        try:
+            sim.comm_init(world, rank, box[0])
+        except Exception as e:                     # noqa: BLE001
+            ok, why = False, str(e)
+    if multi:
+        dev = None
+        if dist.get_backend() == "nccl":
+            dev = torch.device("cuda", torch.cuda.current_device())
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ok = bool(flag.item())
+    sim.comm_error = why
+    return ok
 
 
 def stats_from_result(r) -> Dict:

@@ -12,7 +12,22 @@ from . import _abi
 from .configs import BftConfig
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.environ.get("BFTSIM_LIB") or os.path.join(PKG_DIR, "build", "libbftsim.so")
+
+
+def lib_override(var: str):
+    """A/B builds (scripts/gpu_ab*.sh) may point a binding at another library, but only when
+    BFTSIM_TESTING=1 is set too: a stray BFTSIM_LIB-style variable never swaps the product library silently."""
+    v = os.environ.get(var)
+    if not v:
+        return None
+    if os.environ.get("BFTSIM_TESTING") != "1":
+        raise RuntimeError(f"{var}={v} is set but BFTSIM_TESTING=1 is not: refusing to load a non-product library")
+    import sys
+    print(f"bftsim: {var} override -> {v} (BFTSIM_TESTING)", file=sys.stderr)
+    return v
+
+
+LIB_PATH = lib_override("BFTSIM_LIB") or os.path.join(PKG_DIR, "build", "libbftsim.so")
 
 _lib = None
 HEADER_SLOT = 288                       # BFTSIM_HEADER_SLOT (include/bftsim.h)
@@ -96,6 +111,7 @@ class Simulator:
         self.h = h.value
         _check(self.h, rc, "bftsim_create")
         self.n_prepared = 0
+        self.n_launched = 0             # instances of the last launch: what fetch / crypto_verify read
 
     def close(self):
         if self.h:
@@ -116,7 +132,7 @@ class Simulator:
             _check(self.h, lib().bftsim_set_trace(self.h, tr.ctypes.data, trace_ticks), "set_trace")
         try:
             _check(self.h, lib().bftsim_run(self.h, first, n, ctypes.byref(r)), "bftsim_run")
-            self.n_prepared = n
+            self.n_prepared = self.n_launched = n
         finally:
             if trace_ticks:
                 lib().bftsim_set_trace(self.h, None, 0)
@@ -160,10 +176,12 @@ class Simulator:
 
     def launch(self, first: int, stream: int = 0):
         _check(self.h, lib().bftsim_launch(self.h, first, ctypes.c_void_p(stream)), "bftsim_launch")
+        self.n_launched = self.n_prepared
 
     def fetch(self):
-        """Per-height results of the last launch (all prepared instances), as run() returns them."""
-        n = self.n_prepared
+        """Per-height results of the last launch (all its instances), as run() returns them. Sized by the
+        launch, not by a later prepare: the C side writes the launched count."""
+        n = self.n_launched
         r, arrs = _abi.alloc_result(n, self.cfg.heights)
         _check(self.h, lib().bftsim_fetch(self.h, ctypes.byref(r)), "bftsim_fetch")
         return _abi.shape_result(arrs, n, self.cfg.heights)
@@ -229,7 +247,7 @@ class Simulator:
     def crypto_verify(self):
         """The batched sign / recover pass over the last launch's messages: report dict, per-instance
         checksum [n, 32] (XOR of keccak(signature || seal)) and message counts [n]."""
-        n = self.n_prepared
+        n = self.n_launched
         rep = _abi.CCryptoReport()
         ck = np.zeros((n, 32), np.uint8)
         cnt = np.zeros(n, np.uint32)
@@ -242,7 +260,7 @@ class Simulator:
     def export_ledger(self):
         """The ledger Headers with votes of the last launch (after crypto_verify): per instance a list of
         header byte strings, height 1..committed (include/bftsim.h bftsim_export_ledger)."""
-        n, H = self.n_prepared, self.cfg.heights
+        n, H = self.n_launched, self.cfg.heights
         slot = lib().bftsim_ledger_slot_bytes(self.cfg.n)
         buf = np.zeros(n * H * slot, np.uint8)
         lens = np.zeros(n * H, np.uint32)

@@ -17,8 +17,10 @@ import os
 
 import numpy as np
 
+from .runtime import lib_override
+
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.environ.get("BFTSIG_LIB") or os.path.join(PKG_DIR, "build", "libbftsig.so")
+LIB_PATH = lib_override("BFTSIG_LIB") or os.path.join(PKG_DIR, "build", "libbftsig.so")
 
 _lib = None
 

@@ -18,8 +18,10 @@ import os
 
 import numpy as np
 
+from .runtime import lib_override
+
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.environ.get("BFTWIRE_LIB") or os.path.join(PKG_DIR, "build", "libbftwire.so")
+LIB_PATH = lib_override("BFTWIRE_LIB") or os.path.join(PKG_DIR, "build", "libbftwire.so")
 _lib = None
 
 

@@ -18,6 +18,20 @@
 #include <string>
 
 #include "../../include/bftwire.h"
+
+// the block-frame structs are mirrored by hand-coded numpy dtypes (bftsim/wire.py TX_DTYPE, BLOCK_DTYPE,
+// PP_DTYPE) and by INTEGRATION.md's Rust binding: their layout is part of the ABI
+#include <stddef.h>
+static_assert(sizeof(bftwire_tx) == 200, "bftwire_tx ABI");
+static_assert(offsetof(bftwire_tx, payload_len) == 32 && offsetof(bftwire_tx, recipient) == 40 &&
+              offsetof(bftwire_tx, payload) == 60 && offsetof(bftwire_tx, sig) == 124, "bftwire_tx ABI");
+static_assert(sizeof(bftwire_block) == 1688, "bftwire_block ABI");
+static_assert(offsetof(bftwire_block, extra_len) == 48 && offsetof(bftwire_block, prev_hash) == 64 &&
+              offsetof(bftwire_block, proposer) == 192 && offsetof(bftwire_block, extra) == 212 &&
+              offsetof(bftwire_block, votes) == 244 && offsetof(bftwire_block, tx) == 1288, "bftwire_block ABI");
+static_assert(sizeof(bftwire_preprepare) == 1808, "bftwire_preprepare ABI");
+static_assert(offsetof(bftwire_preprepare, has_sig) == 40 && offsetof(bftwire_preprepare, signature) == 48 &&
+              offsetof(bftwire_preprepare, block) == 120, "bftwire_preprepare ABI");
 #include "bft_wire.h"
 #include "bft_wire_block.h"
 

@@ -70,7 +70,7 @@ typedef struct bftwire_tx {         /* Transaction, serde order (types/transacti
     uint8_t payload[BFTWIRE_MAX_PAYLOAD];
     uint8_t sig[65];
     uint8_t pad2[7];
-} bftwire_tx;                       /* 208 bytes */
+} bftwire_tx;                       /* 200 bytes */
 
 typedef struct bftwire_block {      /* Block {header, transactions} (types/block.rs:16-36, 146-149) */
     uint64_t bloom, difficulty, height, gas_limit, gas_used, time;

@@ -8,7 +8,7 @@ EXTRA=${AB_ARGS:-}
 for i in 1 2; do
   for kv in "$@"; do
     name=${kv%%=*}; f=${kv#*=}
-    BFTSIM_LIB=$f timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-cpu $EXTRA > gpurun_out/ab/$name.$i.json 2>> gpurun_out/ab/ab.err || exit $?
+    BFTSIM_TESTING=1 BFTSIM_LIB=$f timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-cpu $EXTRA > gpurun_out/ab/$name.$i.json 2>> gpurun_out/ab/ab.err || exit $?
     python -c "import json; d=json.load(open('gpurun_out/ab/$name.$i.json')); r=d['roofline']['kernel_ms']; print('$name', round(d['value']/1e6,1), 'M/s  consensus', round(r['bft_consensus_kernel'],3), 'ms  hash', round(r['bft_hash_kernel'],3), 'ms')"
   done
 done

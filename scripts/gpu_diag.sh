@@ -9,7 +9,7 @@ D=gpurun_out/diag
 for lib in base ""; do
   f=consensus-rs_amd/build/libbftsim${lib:+_$lib}.so
   for i in 1 2; do
-    BFTSIM_LIB=$f timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-cpu > $D/ab_${lib:-new}_$i.json 2>> $D/ab.err || exit $?
+    BFTSIM_TESTING=1 BFTSIM_LIB=$f timeout -k 10 120 python bench.py --steps 10 --warmup 2 --no-cpu > $D/ab_${lib:-new}_$i.json 2>> $D/ab.err || exit $?
     python -c "import json,sys; d=json.load(open('$D/ab_${lib:-new}_$i.json')); print('$f', round(d['value']/1e6,1), 'M/s', round(d['roofline']['kernel_ms']['bft_consensus_kernel'],3), 'ms')"
   done
 done

@@ -10,7 +10,7 @@ for lib in "$@"; do
   f=consensus-rs_amd/build/libbftsim_$lib.so
   for k in 1 2; do
     eval P=\$P$k
-    BFTSIM_LIB=$f timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $P -d gpurun_out/pmcab/$lib.$k -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-pipeline > gpurun_out/pmcab/$lib.$k.json 2> gpurun_out/pmcab/$lib.$k.err || exit $?
+    BFTSIM_TESTING=1 BFTSIM_LIB=$f timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $P -d gpurun_out/pmcab/$lib.$k -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu --no-pipeline > gpurun_out/pmcab/$lib.$k.json 2> gpurun_out/pmcab/$lib.$k.err || exit $?
   done
   python3 - "$lib" <<'PY'
 import csv, glob, sys

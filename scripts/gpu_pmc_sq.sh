@@ -7,7 +7,7 @@ C=${SQ_COUNTERS:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRA
 for kv in "$@"; do
   name=${kv%%=*}; f=${kv#*=}
   R=gpurun_out/pmcsq/$name; mkdir -p $R
-  BFTSIM_LIB=$f timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $C -d $R -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu > $R/b.json 2> $R/b.err || exit $?
+  BFTSIM_TESTING=1 BFTSIM_LIB=$f timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $C -d $R -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu > $R/b.json 2> $R/b.err || exit $?
   python3 - "$R" <<'PY'
 import csv, glob, sys, collections
 R = sys.argv[1]

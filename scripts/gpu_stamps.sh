@@ -2,7 +2,7 @@
 # per-section cycle shares of the consensus kernel (diagnostic build; used through gpurun)
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 env BFTSIM_LIB=consensus-rs_amd/build/libbftsim_stamps.so python - <<'PY' > gpurun_out/stamps.txt 2>&1
+timeout -k 10 300 env BFTSIM_TESTING=1 BFTSIM_LIB=consensus-rs_amd/build/libbftsim_stamps.so python - <<'PY' > gpurun_out/stamps.txt 2>&1
 import ctypes, sys
 sys.path.insert(0, "consensus-rs_amd")
 from bftsim import runtime

@@ -3,7 +3,7 @@
 # cfg3 with little-endian seeds (in-kernel hashes) and drop64, 2,048 instances each
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 env BFTSIM_LIB=consensus-rs_amd/build/libbftsim_stamps.so python - <<'PY' > gpurun_out/stamps_general.txt 2>&1
+timeout -k 10 300 env BFTSIM_TESTING=1 BFTSIM_LIB=consensus-rs_amd/build/libbftsim_stamps.so python - <<'PY' > gpurun_out/stamps_general.txt 2>&1
 import ctypes, dataclasses, sys
 sys.path.insert(0, "consensus-rs_amd")
 from bftsim import runtime

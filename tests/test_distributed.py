@@ -64,3 +64,51 @@ def test_gloo_world2_stats_equal_single_process():
     assert sum(tot["latency_hist"]) == tot["committed_heights"] == sum(tot["round_hist"])
     # the per-height rows give the same rounds-to-commit histogram
     assert stats_from_result(O.run(cfg2(heights=15), 0, 16))["round_hist"] == single["round_hist"]
+
+
+class _FakeSim:
+    """stands in for Simulator in the comm-init decision: fails where told to"""
+    def __init__(self, fail_id, fail_init):
+        self.fail_id, self.fail_init, self.joined = fail_id, fail_init, False
+
+    def comm_unique_id(self):
+        if self.fail_id:
+            raise RuntimeError("no librccl")
+        return bytes(128)
+
+    def comm_init(self, world, rank, uid):
+        assert uid == bytes(128)
+        if self.fail_init:
+            raise RuntimeError("init failed")
+        self.joined = True
+
+
+def _comm_worker(rank, world, port, q, fail_id, fail_init_rank):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "consensus-rs_amd"))
+    import torch.distributed as dist
+    from bftsim.distributed import capi_comm_init
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ok = capi_comm_init(_FakeSim(fail_id and rank == 0, rank == fail_init_rank), rank, world)
+    q.put((rank, ok))
+    dist.barrier()                                   # every rank reaches the same next collective
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_id,fail_init_rank,want", [(False, -1, True), (True, -1, False), (False, 1, False)])
+def test_comm_init_decision_is_collective(fail_id, fail_init_rank, want):
+    """bench.py's RCCL-or-fallback choice: a failure on any rank sends every rank to the same branch"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, 2, port, q, fail_id, fail_init_rank)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert got == {0: want, 1: want}

@@ -50,6 +50,10 @@ CASES = [
     ("n16-drop40", lambda: BftConfig(n=16, heights=30, seed=13, drop_ppm=400_000), 0, 16),
     ("n5-2silent", lambda: BftConfig(n=5, heights=30, seed=14, silent=[0, 3]), 0, 8),
     ("n64-byz21-drop5", lambda: BftConfig(n=64, heights=20, seed=15, byz_count=21, drop_ppm=50_000), 0, 4),
+    # lossless N = 64 with phase caps that end a tick at (3) or just after (4) the commit phase: the FAST
+    # kernel's fused block-gossip phase at the cap boundary (bft_fast64.h run, p + 1 < phase_cap)
+    ("n64-byz21-cap3", lambda: BftConfig(n=64, heights=20, seed=45, byz_count=21, phase_cap=3), 0, 16),
+    ("n64-byz21-cap4", lambda: BftConfig(n=64, heights=20, seed=46, byz_count=21, phase_cap=4), 0, 16),
     ("n1", lambda: BftConfig(n=1, heights=20), 0, 8),
     ("n2", lambda: BftConfig(n=2, heights=20, drop_ppm=100_000), 0, 8),
     # N > 64: one workgroup of 128 / 256 lanes per instance

@@ -56,3 +56,26 @@ def test_pipeline_toggle_and_sizes():
             assert_same(O.run(cfg, 32, 32), got, f"pipeline={on}")
     finally:
         sim.close()
+
+
+def test_timed_mode_full_size():
+    """The exact mode bench.py times: cfg3 at 16,384 instances, pipeline depth 3 (so the hash pass is
+    bft_hash_lane_kernel on its set's stream under the ring), repeated launches of the same instances;
+    the last launch's results against the oracle over every instance."""
+    from bftsim.configs import INSTANCES
+    cfg = cfg3()
+    n = INSTANCES["cfg3"]
+    sim = _sim(cfg)
+    try:
+        sim.set_pipeline(True, 3)
+        sim.prepare(n)
+        for _ in range(5):                       # wraps the ring of three sets
+            sim.launch(0)
+        sim.sync()
+        got = sim.fetch()
+        st = sim.stats()
+    finally:
+        sim.close()
+    ref = O.run(cfg, 0, n, threads=16)
+    assert_same(ref, got, "cfg3 16384 pipelined x5")
+    assert st["views"] == int(ref["views"].sum()) == n * 100
