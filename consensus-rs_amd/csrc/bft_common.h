@@ -173,7 +173,12 @@ struct Bits {
         return x;
     }
     BFT_FN bool get(uint32_t i) const { return (word((int)(i >> 6)) >> (i & 63u)) & 1ull; }
-    BFT_FN void set(uint32_t i) { for (int k = 0; k < NW; ++k) if ((i >> 6) == (uint32_t)k) w[k] |= 1ull << (i & 63u); }
+    // value selects, not a conditional store: LLVM turns `if (k == i/64) w[k] |= b` into a store at the
+    // dynamic index w[i/64], which forces the whole kernel object into scratch (S = 256: 840 B/lane)
+    BFT_FN void set(uint32_t i) {
+        const uint64_t b = 1ull << (i & 63u);
+        for (int k = 0; k < NW; ++k) w[k] |= ((i >> 6) == (uint32_t)k) ? b : 0ull;
+    }
     BFT_FN bool any() const { uint64_t x = 0; for (int k = 0; k < NW; ++k) x |= w[k]; return x != 0; }
     BFT_FN bool none() const { return !any(); }
     BFT_FN uint32_t popc() const {

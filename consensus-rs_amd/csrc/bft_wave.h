@@ -602,11 +602,13 @@ struct Sim {
         }
         return mx;
     }
-    BFT_FN int rcs_add(uint32_t round, uint32_t sender) {                    // round_change_set.rs:28-35
+    // the entry of `round` (round_change_set.rs:28-35 `entry().or_insert`), inserted empty in ascending
+    // round order if absent; -1 when the table is full (flagged: outputs after it are not parity-pinned)
+    BFT_FN int rcs_slot(uint32_t round) {
         uint32_t pos = 0;
         while (pos < n_rcs && *rc_round_p(pos) < round) ++pos;
         if (pos == n_rcs || *rc_round_p(pos) != round) {
-            if (n_rcs == (uint32_t)RCS_K) { lane_flags |= FLAG_RCS_OVERFLOW; return 0; }
+            if (n_rcs == (uint32_t)RCS_K) { lane_flags |= FLAG_RCS_OVERFLOW; return -1; }
             for (uint32_t i = n_rcs; i > pos; --i) {
                 *rc_round_p(i) = *rc_round_p(i - 1);
                 for (uint32_t j = 0; j < 2u * NW; ++j) *rc_word_p(i, j) = *rc_word_p(i - 1, j);
@@ -615,8 +617,13 @@ struct Sim {
             rc_set_store(pos, M::zero());
             n_rcs += 1;
         }
-        M set = rc_set_at(pos) | M::bit(sender);
-        rc_set_store(pos, set);
+        return (int)pos;
+    }
+    BFT_FN int rcs_add(uint32_t round, uint32_t sender) {                    // round_change_set.rs:28-35
+        const int pos = rcs_slot(round);
+        if (pos < 0) return 0;
+        M set = rc_set_at((uint32_t)pos) | M::bit(sender);
+        rc_set_store((uint32_t)pos, set);
         return (int)set.popc();
     }
     BFT_FN void send_next_round_change() {                                   // round_change.rs:26-36
@@ -1101,17 +1108,25 @@ struct Sim {
         uint32_t pr_h, pr_r, cm_h, cm_r, blk_lo, blk_hi;
         uint64_t pr_cls, cm_cls;              // (height, proposer) class of the digests
         bool u_pr, u_cm, u_blk;               // one view / one digest class / one range
+        uint32_t pp_src, pp_h, pp_r, pp_eq;   // the first Preprepare sender and its message
+        uint64_t pp_b;
+        uint32_t rc_h, rc_r;                  // the first RoundChange sender's view
+        bool u_rc;                            // every RoundChange of the segment carries that view
     };
     // how a phase is delivered (segment-uniform): the closed forms read the summary only;
     // the general path reads the published LDS records in each receiver's rotated order
-    enum : uint32_t { PATH_GENERAL = 0, PATH_BLK = 1, PATH_PC = 2 };
+    //   PATH_NONE  nothing in flight in the segment (the event step only);
+    //   PATH_PP    one Preprepare and nothing else: every receiver handles that one message;
+    //   PATH_RC    RoundChanges of one view and nothing else (deliver_round_change).
+    enum : uint32_t { PATH_GENERAL = 0, PATH_BLK = 1, PATH_PC = 2, PATH_NONE = 3, PATH_PP = 4, PATH_RC = 5 };
     BFT_FN uint32_t classify(const PhaseSummary& ps) const {
         if (!P.fast) return PATH_GENERAL;
-        const bool rest = (ps.k_ocm | ps.k_rc | ps.k_sync).any();
-        if (rest) return PATH_GENERAL;
-        if (ps.k_pp.any()) return PATH_GENERAL;
-        if (ps.k_pr.none() && ps.k_cm.none()) return (ps.k_blk.any() && ps.u_blk) ? PATH_BLK : PATH_GENERAL;
-        if (ps.k_blk.none() && ps.u_pr && ps.u_cm) return PATH_PC;
+        if ((ps.k_ocm | ps.k_sync).any()) return PATH_GENERAL;
+        const bool pc = ps.k_pr.any() || ps.k_cm.any(), blk = ps.k_blk.any(), pp = ps.k_pp.any();
+        if (ps.k_rc.any()) return (!pp && !pc && !blk && ps.u_rc) ? PATH_RC : PATH_GENERAL;
+        if (pp) return (!pc && !blk && ps.k_pp.popc() == 1u) ? PATH_PP : PATH_GENERAL;
+        if (!pc) return blk ? (ps.u_blk ? PATH_BLK : PATH_GENERAL) : PATH_NONE;
+        if (!blk && ps.u_pr && ps.u_cm) return PATH_PC;
         return PATH_GENERAL;
     }
 
@@ -1144,10 +1159,30 @@ struct Sim {
         ps.u_pr = ps.u_cm = ps.u_blk = true;
         // leader of each kind (the first sender of the segment) and uniformity against it
         // (the wave-wide ballots equal the segment masks when the segment is the whole wave)
+        const bool pp = (f & F_PP) != 0, rc = (f & F_RC) != 0;
         bool any_pr = S == 64 ? ps.k_pr.any() : ballot(pr).any();
         bool any_cm = S == 64 ? ps.k_cm.any() : ballot(cm).any();
         bool any_bk = S == 64 ? ps.k_blk.any() : ballot(bk).any();
-        bool mm_pr = false, mm_cm = false, mm_blk = false;
+        const bool any_pp = S == 64 ? ps.k_pp.any() : ballot(pp).any();
+        const bool any_rc = S == 64 ? ps.k_rc.any() : ballot(rc).any();
+        bool mm_pr = false, mm_cm = false, mm_blk = false, mm_rc = false;
+        ps.pp_src = ps.pp_h = ps.pp_r = ps.pp_eq = 0; ps.pp_b = 0;
+        ps.rc_h = ps.rc_r = 0; ps.u_rc = true;
+        if (any_pp) {
+            const uint32_t j = ps.k_pp.any() ? ps.k_pp.ctz_nz() : 0u;
+            ps.pp_src = j;
+            ps.pp_h = from_seg_lane(nx.pp_h, j);
+            ps.pp_r = from_seg_lane(nx.pp_r, j);
+            ps.pp_b = (uint64_t)from_seg_lane((uint32_t)nx.pp_b, j) | ((uint64_t)from_seg_lane((uint32_t)(nx.pp_b >> 32), j) << 32);
+            ps.pp_eq = from_seg_lane(f & F_PP_EQ, j);
+        }
+        if (any_rc) {
+            const uint32_t j = ps.k_rc.any() ? ps.k_rc.ctz_nz() : 0u;
+            ps.rc_h = from_seg_lane(nx.rc_h, j);
+            ps.rc_r = from_seg_lane(nx.rc_r, j);
+            mm_rc = rc & ((nx.rc_h != ps.rc_h) | (nx.rc_r != ps.rc_r));
+            ps.u_rc = seg_bits(ballot(mm_rc)).none();
+        }
         if (any_pr) {
             uint32_t j = ps.k_pr.any() ? ps.k_pr.ctz_nz() : 0u;
             uint64_t cls = nx.pr_d & BLK_HP_MASK;
@@ -1194,6 +1229,7 @@ struct Sim {
             return (m.shr(off) | m.shl(n - off)) & M::low(n);
         }
     }
+    BFT_FN M unrot(const M& m, uint32_t off) const { return off ? rot(m, nval() - off) : m; }   // inverse of rot
     BFT_FN static M low(uint32_t k) { return M::low(k); }
     // smallest position p in [0,n) with popcount(base | a & low(p+1) | b & low(p)) > q, else n
     BFT_FN uint32_t first_over(const M& base, const M& a, const M& b, uint32_t q) const {
@@ -1289,7 +1325,61 @@ struct Sim {
         st = fin;
     }
 
+    // A phase of RoundChanges that all carry one view (h, R) and nothing else: round_change.rs:65-98 for
+    // every delivered sender in this receiver's rotated order, with the RoundChangeSet entry of R updated
+    // once. The order matters at one point only, the quorum event (count > q while waiting with r < R:
+    // send_round_change + start_new_round, which clears the set; the later senders then fill the fresh
+    // set of R); it is found as a prefix count, as the prepare quorum of deliver_prepare_commit.
+    BFT_FN void deliver_round_change(const PhaseSummary& ps, const M& mk, uint32_t off) {
+        if (core_dead) return;                        // deliver_from: a panicked Core handles nothing
+        const M D = mk & ps.k_rc;
+        if (D.none()) return;
+        const uint32_t R = ps.rc_r;
+        const int res = check_message(MT_ROUND_CHANGE, ps.rc_h);
+        if (res != 0) { if (res == CM_FUTURE_BLOCK) note_future_block(ps.rc_h); return; }
+        const uint32_t k = D.popc();
+        if (r > R && R > 0) {                         // every message: send_round_change(R) (round_change.rs:74-77)
+            if (rc_last_tick == tick) { new_round_change_timer(); return; }   // all suppressed by the limiter
+            rc_last_tick = tick;                      // the first one goes out (r > R: no catchup_round)
+            out_round_change(h, R);
+            if (k >= 2u) new_round_change_timer();   // the later ones are suppressed: timer re-armed
+            return;
+        }
+        const int pos = rcs_slot(R);
+        if (pos < 0) return;                          // table full: every rcs_add returns 0 (flagged)
+        const M set = rc_set_at((uint32_t)pos);
+        const uint32_t n = nval(), q = qval();
+        const M Dr = rot(D, off);
+        uint32_t pe = 64u * NW;                       // position of the quorum event, if any
+        if (wait && r < R) {
+            const uint32_t p0 = first_over(rot(set, off), Dr, M::zero(), q);
+            if (p0 < n) pe = first_at_or_after(Dr, p0);
+        }
+        if (pe >= n) { rc_set_store((uint32_t)pos, set | D); return; }
+        const M later = unrot(Dr & ~low(pe + 1u), off);   // senders after the event
+        send_round_change(R);
+        if (last > h) {                               // start_new_round returns at once (core.rs:476-479):
+            rc_set_store((uint32_t)pos, set | D);     // every later sender repeats the event, suppressed
+            if (later.any()) new_round_change_timer();   // by the limiter
+            return;
+        }
+        rc_set_store((uint32_t)pos, set | (D & ~later));
+        start_new_round(R);                           // clears the RoundChangeSet
+        if (core_dead || later.none()) return;
+        const int p2 = rcs_slot(R);                   // r == R, wait == false: the later ones are only added
+        if (p2 >= 0) rc_set_store((uint32_t)p2, later);
+    }
+
     BFT_FN void deliver_phase(const PhaseSummary& ps, uint32_t path, const M& mk, uint32_t off) {
+        if (path == PATH_NONE) return;
+        if (path == PATH_PP) {                        // one Preprepare: its handler at every receiver
+            if (!core_dead && mk.get(ps.pp_src)) handle_preprepare(ps.pp_src, ps.pp_h, ps.pp_r, ps.pp_b, ps.pp_eq != 0);
+            return;
+        }
+        if (path == PATH_RC) {
+            deliver_round_change(ps, mk, off);
+            return;
+        }
         if (path == PATH_BLK) {                       // block gossip with one range
             if ((mk & ps.k_blk & ~M::bit(me)).any()) handle_blocks(ps.blk_lo, ps.blk_hi);
             BFT_STAMP(8);
@@ -1398,6 +1488,9 @@ struct Sim {
                 summarize(ps);
                 BFT_STAMP(1);
                 const uint32_t path = classify(ps);
+#ifdef BFT_PHASE_CENSUS
+                BFT_PHASE_CENSUS(ps, path, me);               // test-only (tests/emu): phase kinds census
+#endif
 #ifdef BFT_STAMPS
                 st_acc[6] += 1;                               // phases (a count, not cycles)
                 st_acc[11] += path == PATH_GENERAL ? 1 : 0;   // general-path phases
@@ -1410,7 +1503,7 @@ struct Sim {
                 if (act & seg_pending) {
                     miner_step();                             // event step
                     M mk = deliver_mask<NW>(P.seed, nval(), P.thr16, inst, (uint32_t)tick, p, me);
-                    uint32_t off = (path == PATH_GENERAL || path == PATH_PC)
+                    uint32_t off = (path == PATH_GENERAL || path == PATH_PC || path == PATH_RC)
                                        ? offset_from_parts(P.seed, nval(), off_tick, p, me) : 0u;
                     BFT_STAMP(5);
                     deliver_phase(ps, path, mk, off);

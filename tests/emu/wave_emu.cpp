@@ -13,6 +13,28 @@
 #include <vector>
 
 #include "../../consensus-rs_amd/csrc/bft_host.h"
+#ifdef BFT_CENSUS_BUILD
+// analysis build only (scripts/phase_census.py): a histogram of the phase shapes the general kernel sees,
+// keyed by the kinds in flight, the uniformity bits and the chosen path
+#include <map>
+static std::map<uint32_t, uint64_t> g_census;
+#define BFT_PHASE_CENSUS(ps, path, me)                                                                     \
+    do {                                                                                                   \
+        if ((me) == 0) {                                                                                   \
+            uint32_t k_ = (ps.k_pp.any() ? 1u : 0u) | (ps.k_pr.any() ? 2u : 0u) | (ps.k_cm.any() ? 4u : 0u) | \
+                          (ps.k_ocm.any() ? 8u : 0u) | (ps.k_rc.any() ? 16u : 0u) | (ps.k_sync.any() ? 32u : 0u) | \
+                          (ps.k_blk.any() ? 64u : 0u) | (ps.u_pr ? 0 : 128u) | (ps.u_cm ? 0 : 256u) |           \
+                          (ps.u_blk ? 0 : 512u) | ((uint32_t)(path) << 12);                                   \
+            g_census[k_] += 1;                                                                             \
+        }                                                                                                  \
+    } while (0)
+extern "C" int emu_census(uint32_t* keys, uint64_t* counts, int cap) {
+    int i = 0;
+    for (auto& kv : g_census) { if (i < cap) { keys[i] = kv.first; counts[i] = kv.second; } ++i; }
+    g_census.clear();
+    return i;
+}
+#endif
 #include "../../consensus-rs_amd/csrc/bft_wave.h"
 #include "../../consensus-rs_amd/csrc/bft_fast64.h"
 
