@@ -20,8 +20,15 @@
 // * a Core commit is `pp` at round 0: one flag bit.
 // That leaves ~25 live 32-bit values per lane (the general body keeps ~90), so the kernel runs without
 // spills at 6 waves per SIMD (80 VGPRs), and the phase logic is short, mostly branch-free selects.
+//
+// SEEDED = true: the proposer depends on the previous block hash (little-endian U128 seeds,
+// bftsim.h BFTSIM_SEED_LE): proposer = seed(hash of the chain tip) mod 64 at round 0 (validator.rs:33-48,
+// 74-77), the same for every validator whose tip is the same block. Each canonical height is hashed by
+// the whole wave when it is recorded (bft_kwave.h), before any validator can start the next height, and
+// its row carries the seed; a validator's proposer is kept per lane.
 #pragma once
 #include "bft_common.h"
+#include "bft_kwave.h"
 #include "bft_wave.h"
 
 namespace bft {
@@ -37,12 +44,15 @@ struct F64Layout {
     static constexpr uint32_t LANE_OFF = LAT_OFF + 65 * 4 + 4;
     static constexpr uint32_t W_SYNC = 0, W_RCLT = 1, W_PENDT = 2, W_PPT = 3, W_LFL = 4, LANE_WORDS = 5;
     static constexpr uint32_t BYTES = LANE_OFF + LANE_WORDS * 64 * 4;
+    static constexpr uint32_t KW_OFF = BYTES;                  // SEEDED: the header buffer of the wave hash
+    static constexpr uint32_t BYTES_SEEDED = KW_OFF + KW_BUF_BYTES;
+    static_assert(KW_OFF % 8 == 0, "8-aligned header buffer");
 };
-constexpr uint32_t lds_bytes_fast64() { return F64Layout::BYTES; }
+constexpr uint32_t lds_bytes_fast64(bool seeded = false) { return seeded ? F64Layout::BYTES_SEEDED : F64Layout::BYTES; }
 
 // LOSSY = false: the schedule has no link drops and no proposer crashes (thr16 == 0, crash_on == 0,
 // e.g. cfg3), so every delivery mask is all ones at compile time
-template <class W, bool LOSSY = true>
+template <class W, bool LOSSY = true, bool SEEDED = false>
 struct Fast64 {
     static constexpr uint32_t N = 64, Q = 42;   // floor(2N/3) (validator.rs:149-154)
     // lane flag bits
@@ -63,8 +73,10 @@ struct Fast64 {
     uint32_t canon_h, canon_tick, done_tick, seg_flags, flushed;
     uint64_t canon_tip, views_acc;
     uint64_t byz_mask;                 // Byzantine validators of this instance (SPEC.md §6)
-    uint32_t pp_T_out;                 // time tick of validator 0's outbox Preprepare
+    uint32_t pp_T_out;                 // time tick of the proposer's outbox Preprepare
     int32_t tick;
+    // SEEDED: the canonical tip's hash (lane l < 8 holds word l) and seed; each lane's round-0 proposer
+    uint32_t tip_w, canon_seed, prop_l;
     // per lane (Core + RoundState + chain tip + miner + timers + outbox)
     uint32_t fl;                       // L_* bits; state in bits 0..2
     uint32_t h;
@@ -105,6 +117,12 @@ struct Fast64 {
         for (uint32_t k = 0; k < F64Layout::CACHE_WORDS; ++k) *cache_p(k) = 0;
         off_inst = offset_inst_part(p.seed, inst);
         off_tick = 0;
+        canon_seed = p.genesis_seed;
+        prop_l = 0;
+        tip_w = 0;
+        if (SEEDED && me < 8u)
+            tip_w = (uint32_t)p.genesis_hash[4 * me] | ((uint32_t)p.genesis_hash[4 * me + 1] << 8) |
+                    ((uint32_t)p.genesis_hash[4 * me + 2] << 16) | ((uint32_t)p.genesis_hash[4 * me + 3] << 24);
     }
 
     // ------------------------------------------------------------------ small helpers
@@ -118,7 +136,13 @@ struct Fast64 {
     }
     BFT_FN uint32_t* lane_p(uint32_t w) const { return (uint32_t*)(lds + F64Layout::LANE_OFF) + w * 64u + me; }
     BFT_FN uint32_t lane_flags() const { return *lane_p(F64Layout::W_LFL) | (has(L_OBX) ? FLAG_OUTBOX : 0u); }
-    BFT_FN uint32_t proposer() const { return has(L_PROP) ? 0u : 0xffffffffu; }
+    BFT_FN uint32_t proposer() const { return has(L_PROP) ? (SEEDED ? prop_l : 0u) : 0xffffffffu; }
+    // seed of canonical block x as recorded (SEEDED; row word 3, the genesis seed at 0)
+    BFT_FN uint32_t seed_at(uint32_t x) {
+        if (x == 0u) return P.genesis_seed;
+        if (x == canon_h) return canon_seed;
+        return row_word(x, 3);
+    }
     BFT_FN uint32_t st() const { return fl & L_ST; }
     BFT_FN void set_st(uint32_t s) { fl = (fl & ~L_ST) | s; }
     BFT_FN bool has(uint32_t b) const { return (fl & b) != 0; }
@@ -178,8 +202,10 @@ struct Fast64 {
     }
     BFT_FN void out_preprepare_p(bool c) {                       // view (h, 0), own candidate; equivocates iff Byzantine
         const bool put = send_kind(c, 0, h, cand(), F_PP, F_PP_EQ);
-        // only validator 0 proposes here: its Preprepare's time tick is kept wave-uniform (SGPR)
-        if (ballot(put) != 0) pp_T_out = uni(rl(cand_T, 0));
+        // only the round-0 proposer (validator 0 with big-endian seeds) proposes here: its Preprepare's time
+        // tick is kept wave-uniform (SGPR); two proposers in one phase take the general path (run)
+        const uint64_t bp = ballot(put);
+        if (bp != 0) pp_T_out = uni(rl(cand_T, SEEDED ? ff1(bp) : 0u));
     }
     BFT_FN void out_prepare_p(bool c) { send_kind(c, 1, h, pp, F_PR, F_PR_W); }   // (h, 0, pp)
     BFT_FN void out_commit_p(bool c) { send_kind(c, 2, h, pp, F_CM, F_CM_W); }
@@ -242,11 +268,22 @@ struct Fast64 {
         const uint32_t cnt = x <= P.heights ? 1u : 0u;             // uniform
         const uint32_t lat = (uint32_t)tick - canon_tick;
         views_acc += cnt;
+        uint32_t sd = 0;
+        if (SEEDED) {                                            // the block's hash by the wave (x = canon_h + 1)
+            const uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
+            const uint32_t hw = kw50_header_hash(wv, me, lds + F64Layout::KW_OFF, tip_w,
+                                                 P.addresses + 20u * blk_prop(b), seed(), inst, x, blk_prop(b),
+                                                 blk_var(b), time);
+            if (me < 8u) ((uint32_t*)(P.hash + ((uint64_t)inst_local * P.rows + x) * 32))[me] = hw;
+            tip_w = hw;
+            sd = seed_from_words(uni(rl(hw, 0)), uni(rl(hw, 1)), N, P.seed_le != 0);
+        }
         if (me == 0) {                                           // one lane: latency histogram and the ring row
             wv.lds_add((uint32_t*)(lds + F64Layout::LAT_OFF) + (lat < 64u ? lat : 64u), cnt);
             uint32_t* r = ring_row(x);
-            r[0] = 0; r[1] = blk_prop(b) | (blk_var(b) << 16) | (1u << 24); r[2] = blk_T(b); r[3] = 0;
+            r[0] = 0; r[1] = blk_prop(b) | (blk_var(b) << 16) | (1u << 24); r[2] = blk_T(b); r[3] = sd;
         }
+        if (SEEDED) canon_seed = sd;
         wv.sync();
         canon_h = x;
         canon_tip = b;
@@ -283,16 +320,17 @@ struct Fast64 {
     }
     BFT_FN void start_new_zero_round_p(bool c) {                 // core.rs:441-470
         h = c ? last + 1 : h;
+        if (SEEDED) prop_l = c ? (seed_at(last) & 63u) : prop_l;   // (seed(tip) + round 0) mod 64
         fl = c ? ((fl & ~(L_ST | L_WAIT | L_LOCK | L_PENDV)) | ST_ACCEPT_REQUEST) : fl;
         pp = c ? BLK_NONE : pp;
         prep = c ? 0ull : prep;                                  // MessageManage::new
         comm = c ? 0ull : comm;
-        fl |= c ? L_PROP : 0u;                                   // proposer = (seed 0 + round 0) mod 64
+        fl |= c ? L_PROP : 0u;                                   // proposer = (seed + round 0) mod 64
         timer_tick = c ? tick + 1 : timer_tick;                  // new_round_change_timer
     }
     BFT_FN void send_preprepare_cand_p(bool c) {                 // preprepare.rs:30-43, req = candidate
-        const bool s = c & (h == mint_height) & has(L_PROP) & (me == 0);
-        if (ballot(s) != 0) {                                    // the proposer (validator 0) proposes
+        const bool s = c & (h == mint_height) & has(L_PROP) & (me == (SEEDED ? prop_l : 0u));
+        if (ballot(s) != 0) {                                    // the proposer proposes
             bool cr = false;
             if (LOSSY && P.crash_on) cr = proposer_crashed(seed(), P.crash_thr32, 1u, inst, h, 0);
             out_preprepare_p(s & !cr);
@@ -382,12 +420,13 @@ struct Fast64 {
             if (old) {
                 const uint32_t bh = blk_h(b);
                 if (bh <= last && blk_eq(canon_blk(bh), b)) {    // else InvalidProposal
-                    if (src == 0) out_old_commit(vh, b);         // old proposer (seed 0, round 0)
+                    // old proposer (preprepare.rs:61-64): seed of block bh - 1, round 0
+                    if (src == (SEEDED ? (seed_at(bh - 1u) & 63u) : 0u)) out_old_commit(vh, b);
                     go = true;                                   // falls through (preprepare.rs:52-74)
                 }
             }
         }
-        go = go & has(L_PROP) & (src == 0);                      // else NotFromProposer
+        go = go & has(L_PROP) & (src == (SEEDED ? prop_l : 0u));   // else NotFromProposer
         const uint32_t bh = blk_h(b);
         const bool bad = go & ((bh == 0) | (bh - 1 > last));    // Backend::verify: unknown ancestor
         const bool acc = go & !bad & (st() == ST_ACCEPT_REQUEST);
@@ -564,9 +603,11 @@ struct Fast64 {
         const uint64_t pend = has(L_PENDV) ? blk_make(h, me, 0, *lane_p(F64Layout::W_PENDT)) : BLK_NONE;
         const uint64_t cd = mint_height ? cand() : BLK_NONE;
         const uint64_t ppb = blk_make(h, me, 0, pp_T_out);     // read only where F_PP is set (lane 0)
-        const uint32_t w32[29] = {h, 0u, st(), 0u, proposer(), last, 0u, (uint32_t)last_T, (uint32_t)timer_tick,
+        const uint32_t lseed = SEEDED ? seed_at(last) : 0u;
+        const uint32_t cseed = SEEDED ? canon_seed : 0u;
+        const uint32_t w32[29] = {h, 0u, st(), 0u, proposer(), last, lseed, (uint32_t)last_T, (uint32_t)timer_tick,
                                   *lane_p(F64Layout::W_RCLT), (uint32_t)wake_tick, mint_height, miner_queue,
-                                  *lane_p(F64Layout::W_SYNC), lane_flags(), canon_h, done_tick, seg_flags, 0u, canon_tick, nxf,
+                                  *lane_p(F64Layout::W_SYNC), lane_flags(), canon_h, done_tick, seg_flags, cseed, canon_tick, nxf,
                                   h, 0u, h, 0u, h, 0u, nx_blo, nx_bhi};
         uint32_t k = 0;
         for (uint32_t i = 0; i < 29; ++i) s[k++] = w32[i];
@@ -648,9 +689,10 @@ struct Fast64 {
                 const uint64_t kpp = ballot((f & F_PP) != 0), kpr = ballot(pr), kcm = ballot(cm);
                 const uint64_t kblk = ballot((f & F_BLK) != 0);
                 const uint64_t kcold = ballot((f & (F_OCM | F_RC | F_SYNC)) != 0);
-                // the only Preprepare sender of the FAST kernel is the round-0 proposer, validator 0
-                // (send_preprepare_cand_p): kpp is 0 or 1
-                const uint32_t j = 0, jp = ff1(kpr), jc = ff1(kcm), jb = ff1(kblk);
+                // the only Preprepare sender of the FAST kernel is the round-0 proposer (send_preprepare_cand_p):
+                // validator 0 with big-endian seeds (kpp is 0 or 1); with SEEDED the proposer of the senders'
+                // height, and two senders (validators at different heights) take the general path
+                const uint32_t j = SEEDED ? ff1(kpp) : 0u, jp = ff1(kpr), jc = ff1(kcm), jb = ff1(kblk);
                 const uint64_t cls = pp & BLK_HP_MASK;
                 PC c;
                 c.kpr = kpr; c.kcm = kcm;
@@ -665,7 +707,7 @@ struct Fast64 {
                 const uint32_t pp_eq = uni(rl(f & F_PP_EQ, j));
                 const uint32_t blo = uni(rl(nx_blo, jb)), bhi = uni(rl(nx_bhi, jb));
                 uint32_t path;
-                if (kcold) path = P_GENERAL;
+                if (kcold | (SEEDED ? (kpp & (kpp - 1ull)) : 0ull)) path = P_GENERAL;
                 else if (kpp) path = (kpr | kcm | kblk) == 0 ? P_PP : P_GENERAL;
                 else if (kpr | kcm) path = kblk ? P_GENERAL : P_PC;
                 else path = kblk ? P_BLK : P_NONE;

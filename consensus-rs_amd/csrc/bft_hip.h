@@ -25,6 +25,14 @@ struct WaveHip {
     template <int N> __device__ static uint32_t row_shr(uint32_t v) {
         return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x110 + N, 0xF, 0xF, true);
     }
+    // ds_bpermute_b32: this lane gets v of lane addr / 4 (addr = byte address, per lane)
+    __device__ static uint32_t bperm(uint32_t addr, uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)addr, (int)v); }
+    // the value of lane ^ 1 (DPP quad_perm [1,0,3,2])
+    __device__ static uint32_t pair_swap(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false); }
+    // set bits of m below this lane (v_mbcnt_lo / hi)
+    __device__ static uint32_t rank_below(uint64_t m) {
+        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    }
     __device__ static uint32_t readlane(uint32_t v, uint32_t l) {      // l wave-uniform
         return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_amdgcn_readfirstlane((int)l));
     }

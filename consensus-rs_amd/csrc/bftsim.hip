@@ -823,7 +823,10 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     uint32_t per_block = h->seg > 64 ? 1u : 64u / h->seg;      // instances per workgroup
     uint32_t grid = (uint32_t)((n + per_block - 1) / per_block);
     size_t lds = bft::lds_bytes(h->seg, p.need_seed != 0);
-    const bool fast = h->fast && p.fast && !p.mlog && h->d_save && !p.need_seed && !h->h_trace && h->seg == 64;
+    // FAST + resume for N = 64: big-endian seeds (proposer 0, hashes in the post-pass) or little-endian
+    // seeds (SEEDED: hashes in-kernel); not for windowed rows, traces or the opt-in modes
+    const bool fast = h->fast && p.fast && !p.mlog && h->d_save && !h->window && !h->h_trace && h->seg == 64 &&
+                      h->cfg.n == 64;
     const bool ext = p.backlog_replay || p.mlog;       // the opt-in modes' kernel build (MODE_EXT)
     HIPCHECK(h, hipEventRecord(ev.c0, s));
     if (fast) {

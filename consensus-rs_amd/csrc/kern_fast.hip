@@ -10,8 +10,12 @@ namespace bft {
 #ifndef BFT_FAST_WAVES_PER_SIMD
 #define BFT_FAST_WAVES_PER_SIMD 6   // measured best of 4..8 (profiles/r02: 4 → 3.86e8, 5 → 3.97e8, 6 → 4.17e8, 7 → 3.69e8)
 #endif
-template <bool LOSSY>
-__global__ __launch_bounds__(64, BFT_FAST_WAVES_PER_SIMD) void bft_consensus_fast_kernel(Params p) {
+#ifndef BFT_FAST_SEEDED_WAVES_PER_SIMD
+#define BFT_FAST_SEEDED_WAVES_PER_SIMD 5   // the in-kernel wave hash needs registers: 6 spills SGPRs to scratch
+#endif
+template <bool LOSSY, bool SEEDED>
+__global__ __launch_bounds__(64, SEEDED ? BFT_FAST_SEEDED_WAVES_PER_SIMD : BFT_FAST_WAVES_PER_SIMD)
+void bft_consensus_fast_kernel(Params p) {
     extern __shared__ uint8_t lds[];
 #ifndef BFT_CONSENSUS_PRIO
 #define BFT_CONSENSUS_PRIO 2
@@ -19,15 +23,21 @@ __global__ __launch_bounds__(64, BFT_FAST_WAVES_PER_SIMD) void bft_consensus_fas
     // win issue arbitration against the hash waves of the previous launch (the hash pass stretches into
     // the issue gaps and still finishes within the step)
     __builtin_amdgcn_s_setprio(BFT_CONSENSUS_PRIO);
-    Fast64<WaveHip, LOSSY> sim(p, lds, blockIdx.x);
+    Fast64<WaveHip, LOSSY, SEEDED> sim(p, lds, blockIdx.x);
     sim.run();
 }
 hipError_t launch_fast(dim3 grid, hipStream_t s, const Params& p) {
-    // the lossless build for schedules without drops and proposer crashes (cfg3): masks are constants
-    if (p.thr16 == 0 && p.crash_on == 0)
-        hipLaunchKernelGGL(bft_consensus_fast_kernel<false>, grid, dim3(64), lds_bytes_fast64(), s, p);
-    else
-        hipLaunchKernelGGL(bft_consensus_fast_kernel<true>, grid, dim3(64), lds_bytes_fast64(), s, p);
+    // the lossless build for schedules without drops and proposer crashes (cfg3): masks are constants;
+    // SEEDED (little-endian seeds): the proposer follows the block hashes, computed in-kernel
+    const bool lossy = !(p.thr16 == 0 && p.crash_on == 0), seeded = p.need_seed != 0;
+    const size_t lds = lds_bytes_fast64(seeded);
+    if (seeded) {
+        if (lossy) hipLaunchKernelGGL((bft_consensus_fast_kernel<true, true>), grid, dim3(64), lds, s, p);
+        else hipLaunchKernelGGL((bft_consensus_fast_kernel<false, true>), grid, dim3(64), lds, s, p);
+    } else {
+        if (lossy) hipLaunchKernelGGL((bft_consensus_fast_kernel<true, false>), grid, dim3(64), lds, s, p);
+        else hipLaunchKernelGGL((bft_consensus_fast_kernel<false, false>), grid, dim3(64), lds, s, p);
+    }
     return hipGetLastError();
 }
 

@@ -91,6 +91,12 @@ struct EmuWave {
         return (uint32_t)g->res[l];
     }
     static uint32_t readlane(uint32_t v, uint32_t src) { return shfl(v, src); }
+    static uint32_t bperm(uint32_t addr, uint32_t v) { return shfl(v, (addr >> 2) & 63u); }   // ds_bpermute_b32
+    static uint32_t pair_swap(uint32_t v) { return shfl(v, (uint32_t)g->cur ^ 1u); }           // DPP quad [1,0,3,2]
+    static uint32_t rank_below(uint64_t m) {                                                   // mbcnt
+        const uint32_t l = (uint32_t)g->cur;
+        return (uint32_t)__builtin_popcountll(l ? (m & ((1ull << l) - 1ull)) : 0ull);
+    }
     // DPP row_shl / row_shr (16-lane rows; a source outside the row reads 0)
     template <int N> static uint32_t row_shl(uint32_t v) {
         const uint32_t l = (uint32_t)g->cur, s = l + N;
@@ -147,19 +153,19 @@ struct EmuGroup {
 
 template <bool NS, uint32_t S>
 void run_sim() {
-    if constexpr (S == 64 && !NS) {
-        if (g->fast) {                     // bft_consensus_fast_kernel
+    if constexpr (S == 64) {
+        if (g->fast) {                     // bft_consensus_fast_kernel (SEEDED = NS: little-endian seeds)
             if (g->P->thr16 == 0 && g->P->crash_on == 0) {   // the lossless build, as launch_fast picks
-                bft::Fast64<EmuWave, false> sim(*g->P, g->lds, g->wave);
+                bft::Fast64<EmuWave, false, NS> sim(*g->P, g->lds, g->wave);
                 sim.run();
             } else {
-                bft::Fast64<EmuWave, true> sim(*g->P, g->lds, g->wave);
+                bft::Fast64<EmuWave, true, NS> sim(*g->P, g->lds, g->wave);
                 sim.run();
             }
             return;
         }
         if (g->P->resume_mode) {           // bft_consensus_resume_kernel
-            bft::Sim<EmuWave, false, 64, bft::MODE_RESUME> sim(*g->P, g->lds, g->wave);
+            bft::Sim<EmuWave, NS, 64, bft::MODE_RESUME> sim(*g->P, g->lds, g->wave);
             sim.run();
             return;
         }
@@ -361,14 +367,14 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
     // as libbftsim: N = 64 runs the FAST kernel, then the full kernel resumes the instances it handed
     // over (BFT_EMU_FAST=0: the full kernel alone)
     const char* ef = getenv("BFT_EMU_FAST");
-    const bool fast = seg == 64 && cfg->n == 64 && P.fast && !P.mlog && !P.need_seed && !trace && !(ef && strcmp(ef, "0") == 0);
+    const bool fast = seg == 64 && cfg->n == 64 && P.fast && !P.mlog && !trace && !(ef && strcmp(ef, "0") == 0);
     std::vector<uint32_t> resume, save;
     if (fast) {
         resume.assign(n, 0);
         save.assign((size_t)n * 64 * bft::SAVE_WORDS, 0xcdcdcdcdu);
         P.resume_flags = resume.data();
         P.save = save.data();
-        std::vector<uint8_t> lds_fast(bft::lds_bytes_fast64());   // the FAST kernel's exact LDS size
+        std::vector<uint8_t> lds_fast(bft::lds_bytes_fast64(P.need_seed != 0));   // the FAST kernel's exact LDS size
         for (uint32_t w = 0; w < waves; ++w) {
             memset(lds_fast.data(), 0xcd, lds_fast.size());
             if (run_wave(P, w, lds_fast, 64, true)) return -1;

@@ -15,7 +15,7 @@ from bftsim import _abi  # noqa: E402
 EMU_DIR = os.path.join(ROOT, "tests", "emu")
 LIB = os.path.join(EMU_DIR, "libwave_emu.so")
 SRCS = [os.path.join(EMU_DIR, "wave_emu.cpp")] + [
-    os.path.join(ROOT, "consensus-rs_amd", "csrc", f) for f in ("bft_wave.h", "bft_fast64.h", "bft_common.h", "bft_host.h")]
+    os.path.join(ROOT, "consensus-rs_amd", "csrc", f) for f in ("bft_wave.h", "bft_fast64.h", "bft_kwave.h", "bft_common.h", "bft_host.h")]
 
 _lib = None
 

@@ -1,7 +1,7 @@
 """Randomized parity fuzz: CPU wave emulator (the kernel body) vs the oracle on random configs.
 Usage: python tests/fuzz_parity.py [seconds] [rng seed] [big]. `big` draws N in 65..256 (the
 workgroup-segment kernels), `n64` N = 64 (the FAST kernel and its hand-overs); a fourth argument
-`replay` runs every config in backlog replay mode (SPEC.md §10). Test-only tool (not collected by pytest)."""
+`replay` runs every config in backlog replay mode (SPEC.md §10), `le` with little-endian U128 seeds. Test-only tool (not collected by pytest)."""
 import random
 import sys
 import time
@@ -12,7 +12,7 @@ from bftsim.configs import BftConfig
 from parity_util import mismatches
 
 
-def random_config(rng, big=False, n64=False, replay=False):
+def random_config(rng, big=False, n64=False, replay=False, le=False):
     if n64:                              # the FAST kernel (bft_fast64.h) and its hand-overs
         n = 64
     elif big:
@@ -27,8 +27,9 @@ def random_config(rng, big=False, n64=False, replay=False):
     heights = rng.choice([5, 20, 40])
     return BftConfig(n=n, heights=heights, seed=rng.randrange(1 << 40), byz_count=byz,
                      drop_ppm=drop, proposer_crash_ppm=crash, phase_cap=cap, silent=silent,
-                     max_ticks=heights * 4 + 16, backlog_mode=1 if replay else 0,
-                     name=f"n{n}-b{byz}-d{drop}-c{crash}-cap{cap}-s{len(silent)}{'-replay' if replay else ''}")
+                     max_ticks=heights * 4 + 16, backlog_mode=1 if replay else 0, seed_byte_order=1 if le else 0,
+                     name=f"n{n}-b{byz}-d{drop}-c{crash}-cap{cap}-s{len(silent)}{'-replay' if replay else ''}"
+                          f"{'-le' if le else ''}")
 
 
 def main():
@@ -37,9 +38,10 @@ def main():
     big = len(sys.argv) > 3 and sys.argv[3] == "big"
     n64 = len(sys.argv) > 3 and sys.argv[3] == "n64"
     replay = "replay" in sys.argv[3:]
+    le = "le" in sys.argv[3:]                     # little-endian U128 seeds (hash-dependent proposers)
     t0, runs, fails = time.time(), 0, 0
     while time.time() - t0 < budget:
-        cfg = random_config(rng, big, n64, replay)
+        cfg = random_config(rng, big, n64, replay, le)
         first = rng.randrange(1 << 20)
         n_inst = rng.choice([1, 2] if big else [1, 3, 8])
         a = O.run(cfg, first, n_inst)
