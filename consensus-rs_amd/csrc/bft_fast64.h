@@ -86,7 +86,7 @@ struct Fast64 {
     uint32_t mint_height, miner_queue;
     uint32_t nxf, nx_blo, nx_bhi;
 #ifdef BFT_STAMPS
-    uint64_t st_acc[12];
+    uint64_t st_acc[NSTAMP];
     uint64_t st_t;
 #define F64_STAMP(k) do { uint64_t t_ = wv.clock(); st_acc[k] += t_ - st_t; st_t = t_; } while (0)
 #define F64_COUNT(k) do { st_acc[k] += 1; } while (0)
@@ -118,6 +118,7 @@ struct Fast64 {
         off_inst = offset_inst_part(p.seed, inst);
         off_tick = 0;
         canon_seed = p.genesis_seed;
+        hashed_h = 0;
         prop_l = 0;
         tip_w = 0;
         if (SEEDED && me < 8u)
@@ -268,22 +269,11 @@ struct Fast64 {
         const uint32_t cnt = x <= P.heights ? 1u : 0u;             // uniform
         const uint32_t lat = (uint32_t)tick - canon_tick;
         views_acc += cnt;
-        uint32_t sd = 0;
-        if (SEEDED) {                                            // the block's hash by the wave (x = canon_h + 1)
-            const uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
-            const uint32_t hw = kw50_header_hash(wv, me, lds + F64Layout::KW_OFF, tip_w,
-                                                 P.addresses + 20u * blk_prop(b), seed(), inst, x, blk_prop(b),
-                                                 blk_var(b), time);
-            if (me < 8u) ((uint32_t*)(P.hash + ((uint64_t)inst_local * P.rows + x) * 32))[me] = hw;
-            tip_w = hw;
-            sd = seed_from_words(uni(rl(hw, 0)), uni(rl(hw, 1)), N, P.seed_le != 0);
-        }
         if (me == 0) {                                           // one lane: latency histogram and the ring row
             wv.lds_add((uint32_t*)(lds + F64Layout::LAT_OFF) + (lat < 64u ? lat : 64u), cnt);
             uint32_t* r = ring_row(x);
-            r[0] = 0; r[1] = blk_prop(b) | (blk_var(b) << 16) | (1u << 24); r[2] = blk_T(b); r[3] = sd;
+            r[0] = 0; r[1] = blk_prop(b) | (blk_var(b) << 16) | (1u << 24); r[2] = blk_T(b); r[3] = 0;   // seed: hash_pending
         }
-        if (SEEDED) canon_seed = sd;
         wv.sync();
         canon_h = x;
         canon_tip = b;
@@ -553,7 +543,35 @@ struct Fast64 {
     // ------------------------------------------------------------------ commits of a phase → canonical chain
     // Returns the committed height when every committer of the phase committed the same one (each of
     // them then has the block range [x0, x0] in its outbox, chain_insert_core_p), else 0.
+    // SEEDED: the hash and seed of every height recorded since the last call, in height order (one call site,
+    // so the wave hash is inlined once), before any validator can start the next height
+    uint32_t hashed_h;
+    BFT_FN void hash_pending() {
+        while (hashed_h < canon_h) {                             // uniform
+            const uint32_t x = hashed_h + 1u;
+            const uint64_t b = canon_blk(x);
+            const uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
+            const uint32_t hw = kw50_header_hash(wv, me, lds + F64Layout::KW_OFF, tip_w,
+                                                 P.addresses + 20u * blk_prop(b), seed(), inst, x, blk_prop(b),
+                                                 blk_var(b), time);
+            if (me < 8u) ((uint32_t*)(P.hash + ((uint64_t)inst_local * P.rows + x) * 32))[me] = hw;
+            tip_w = hw;
+            const uint32_t sd = seed_from_words(uni(rl(hw, 0)), uni(rl(hw, 1)), N, P.seed_le != 0);
+            if (me == 0) {                                       // the row's seed word, wherever the row is now
+                if (x > flushed) ring_row(x)[3] = sd;
+                else wv.gstore(rec_row(x) + 3, sd);
+            }
+            wv.sync();
+            if (x == canon_h) canon_seed = sd;
+            hashed_h = x;
+        }
+    }
     BFT_FN uint32_t resolve_commits() {
+        const uint32_t xc = resolve_commits_core();
+        if (SEEDED) hash_pending();
+        return xc;
+    }
+    BFT_FN uint32_t resolve_commits_core() {
         const bool c = has(L_CMT);
         const uint64_t bal = ballot(c);
         if (bal == 0) return 0;
@@ -652,7 +670,7 @@ struct Fast64 {
     // ------------------------------------------------------------------ the run
     BFT_FN void run() {
 #ifdef BFT_STAMPS
-        for (int k = 0; k < 12; ++k) st_acc[k] = 0;
+        for (int k = 0; k < NSTAMP; ++k) st_acc[k] = 0;
         st_t = wv.clock();
 #endif
         if (P.byz_count > 0) init_byzantine();
@@ -779,7 +797,7 @@ struct Fast64 {
 #ifdef BFT_STAMPS
         F64_STAMP(7);
         if (me == 0 && P.stamps)
-            for (int k = 0; k < 12; ++k) P.stamps[(uint64_t)inst_local * 12 + k] = st_acc[k];
+            for (int k = 0; k < NSTAMP; ++k) P.stamps[(uint64_t)inst_local * NSTAMP + k] = st_acc[k];
 #endif
         // this wave's histograms → the launch totals: every height recorded here was a round-0 commit
         wv.sync();

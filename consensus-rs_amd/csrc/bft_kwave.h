@@ -20,6 +20,15 @@ namespace bft {
 
 constexpr uint32_t KW_BUF_BYTES = LANE_HASH_BUF;     // 3 rate blocks (a header is at most 274 bytes)
 
+// the Keccak round constants as compile-time halves (immediates in the unrolled rounds)
+constexpr uint32_t KW_RC_LO[24] = {
+    0x00000001u, 0x00008082u, 0x0000808Au, 0x80008000u, 0x0000808Bu, 0x80000001u, 0x80008081u, 0x00008009u,
+    0x0000008Au, 0x00000088u, 0x80008009u, 0x8000000Au, 0x8000808Bu, 0x0000008Bu, 0x00008089u, 0x00008003u,
+    0x00008002u, 0x00000080u, 0x0000800Au, 0x8000000Au, 0x80008081u, 0x00008080u, 0x80000001u, 0x80008008u};
+constexpr uint32_t KW_RC_HI[24] = {
+    0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0u, 0u, 0u, 0x80000000u,
+    0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u};
+
 // rho amount of word w (Keccak rotation offsets r[x + 5y])
 BFT_FN uint32_t kw50_rho(uint32_t w) {
     const uint64_t R0 = 0ull | 1ull << 6 | 62ull << 12 | 28ull << 18 | 27ull << 24 | 36ull << 30 | 44ull << 36 |
@@ -41,7 +50,7 @@ BFT_FN uint32_t kw50_alignbit(uint32_t hi, uint32_t lo, uint32_t s) {   // ((hi:
 
 // Keccak-f[1600] over the wave (layout above): `a` = this lane's half word, in place
 template <class W>
-BFT_FN void kw50_permute(W& wv, uint32_t lane, uint32_t& a) {
+BFT_FN __attribute__((always_inline)) void kw50_permute(W& wv, uint32_t lane, uint32_t& a) {
     const uint32_t ln = lane < 50u ? lane : 0u;
     const uint32_t w = ln >> 1, hf = ln & 1u, x = w % 5u, y = w / 5u;
     // ds_bpermute byte addresses of the sources, same half
@@ -54,8 +63,10 @@ BFT_FN void kw50_permute(W& wv, uint32_t lane, uint32_t& a) {
     const uint32_t r = kw50_rho(w);
     const bool swp = (r == 0u) | (r > 32u);
     const uint32_t s = ((r == 0u) | (r == 32u)) ? 0u : (r < 32u ? 32u - r : 64u - r);
-    const bool io_lo = lane == 0u, io_hi = lane == 1u;
-#pragma unroll 1
+    // iota masks: the round constant goes to lanes 0 (low half) and 1 (high half) of word 0
+    const uint32_t m_lo = lane == 0u ? 0xffffffffu : 0u, m_hi = lane == 1u ? 0xffffffffu : 0u;
+    // fully unrolled: the round constants become immediates (no per-round table load, no loop branch)
+#pragma unroll
     for (int rnd = 0; rnd < 24; ++rnd) {
         // theta: C[x] (this half), E[x] = rotl1(C[x]), A ^= C[x-1] ^ E[x+1]
         const uint32_t c = a ^ wv.bperm(p1, a) ^ wv.bperm(p2, a) ^ wv.bperm(p3, a) ^ wv.bperm(p4, a);
@@ -69,7 +80,7 @@ BFT_FN void kw50_permute(W& wv, uint32_t lane, uint32_t& a) {
         const uint32_t b1 = wv.bperm(pxp, b), b2 = wv.bperm(pxp2, b);
         a = b ^ (~b1 & b2);
         // iota
-        a ^= (io_lo ? KECCAK_RC_LO[rnd] : 0u) | (io_hi ? KECCAK_RC_HI[rnd] : 0u);
+        a ^= (KW_RC_LO[rnd] & m_lo) | (KW_RC_HI[rnd] & m_hi);
     }
 }
 
@@ -77,17 +88,18 @@ BFT_FN void kw50_permute(W& wv, uint32_t lane, uint32_t& a) {
 BFT_FN uint32_t kw50_uint_len(uint64_t v) {
     return v < 128u ? 1u : v < 256u ? 2u : v < 65536u ? 3u : v < 4294967296ull ? 5u : 9u;
 }
-BFT_FN uint32_t kw50_uint_byte(uint64_t v, uint32_t len, uint32_t i) {
-    if (len == 1u) return (uint32_t)v;
-    if (i == 0u) return len == 2u ? 0xccu : len == 3u ? 0xcdu : len == 5u ? 0xceu : 0xcfu;
-    return (uint32_t)(v >> (8u * (len - 1u - i))) & 0xffu;        // big-endian payload
+BFT_FN uint32_t kw50_uint_byte(uint64_t v, uint32_t len, uint32_t i) {    // selects only (per-lane i)
+    const uint32_t tag = len == 2u ? 0xccu : len == 3u ? 0xcdu : len == 5u ? 0xceu : 0xcfu;
+    const uint32_t sh = 8u * ((len - 1u - i) & 7u);
+    const uint32_t pay = (uint32_t)(v >> sh) & 0xffu;                  // big-endian payload
+    return len == 1u ? (uint32_t)v & 0xffu : (i == 0u ? tag : pay);
 }
 
 // Keccak-256 of the header of block (h, prop, var) at `time` whose parent hash is `prev_w` (lane l < 8
 // holds its little-endian word l), by the whole wave; `buf` = KW_BUF_BYTES of this wave's LDS, 8-aligned.
 // Returns the hash the same way (lane l < 8: word l; the other lanes: unspecified).
 template <class W>
-BFT_FN uint32_t kw50_header_hash(W& wv, uint32_t lane, uint8_t* buf, uint32_t prev_w, const uint8_t* addr20,
+BFT_FN __attribute__((always_inline)) uint32_t kw50_header_hash(W& wv, uint32_t lane, uint8_t* buf, uint32_t prev_w, const uint8_t* addr20,
                                  uint64_t seed, uint32_t inst, uint32_t h, uint32_t prop, uint32_t var,
                                  uint64_t time) {
     // the 64 variable-length elements: prev_hash byte l (l < 32) and tx_hash byte l - 32 (SPEC.md §5 TX)
@@ -117,45 +129,32 @@ BFT_FN uint32_t kw50_header_hash(W& wv, uint32_t lane, uint8_t* buf, uint32_t pr
         buf[off] = (uint8_t)(big ? 0xccu : eb);
         if (big) buf[off + 1u] = (uint8_t)eb;
     }
-    if (lane < 44u) {   // proposer: str8 "0x" + 40 lowercase hex digits
-        const uint32_t j = lane - 4u;
-        uint32_t v = lane == 0u ? 0xd9u : lane == 1u ? 0x2au : lane == 2u ? 0x30u : 0x78u;
-        if (lane >= 4u) {
-            const uint32_t ab = addr20[j >> 1];
-            v = hexdigit((j & 1u) ? (ab & 15u) : (ab >> 4));
-        }
-        buf[o_addr + lane] = (uint8_t)v;
+    {   // proposer: str8 "0x" + 40 lowercase hex digits, lanes 0..43 (selects; one predicated store)
+        const uint32_t j = lane >= 4u ? lane - 4u : 0u;
+        const uint32_t ab = addr20[(j >> 1) < 20u ? (j >> 1) : 19u];
+        const uint32_t hx = hexdigit((j & 1u) ? (ab & 15u) : (ab >> 4));
+        const uint32_t v = lane == 0u ? 0xd9u : lane == 1u ? 0x2au : lane == 2u ? 0x30u : lane == 3u ? 0x78u : hx;
+        if (lane < 44u) buf[o_addr + lane] = (uint8_t)v;
     }
-    {   // the other non-zero fixed bytes, one per lane: array headers, height, time, extra, votes, padding
-        uint32_t off = 0, v = 0;
-        bool wr = true;
+    {   // the other non-zero fixed bytes, one per lane k (selects; one predicated store): array headers (k < 9),
+        // height (9..13), time (14..22), extra + votes (23..35), padding (36, 37)
         const uint32_t k = lane;
-        if (k == 0u) { off = 0u; v = 0x9du; }                      // array(13)
-        else if (k == 1u) { off = 1u; v = 0xdcu; }                 // prev_hash: array16(32)
-        else if (k == 2u) { off = 3u; v = 0x20u; }
-        else if (k == 3u) { off = o_root; v = 0xdcu; }             // root = EMPTY_HASH
-        else if (k == 4u) { off = o_root + 2u; v = 0x20u; }
-        else if (k == 5u) { off = o_txp; v = 0xdcu; }              // tx_hash
-        else if (k == 6u) { off = o_txp + 2u; v = 0x20u; }
-        else if (k == 7u) { off = o_rec; v = 0xdcu; }              // receipt_hash = EMPTY_HASH
-        else if (k == 8u) { off = o_rec + 2u; v = 0x20u; }
-        else if (k < 14u) {                                        // height (<= 5 bytes)
-            const uint32_t i = k - 9u;
-            wr = i < hl; off = o_h + i; v = kw50_uint_byte(h, hl, i);
-        } else if (k < 23u) {                                      // time (<= 9 bytes)
-            const uint32_t i = k - 14u;
-            wr = i < tl; off = o_t + i; v = kw50_uint_byte(time, tl, i);
-        } else if (k < 36u) {                                      // extra "Coinse base" + votes nil
-            const uint32_t i = k - 23u;
-            const uint64_t E0 = 0x2065736e696f439bull, E1 = 0xc065736162ull;
-            off = o_e + i; v = (uint32_t)((i < 8u ? E0 >> (8u * i) : E1 >> (8u * (i - 8u))) & 0xffu);
-        } else if (k == 36u) {                                     // pad10*1, Keccak domain 0x01
-            off = len; v = 0x01u | (len == 136u * nb - 1u ? 0x80u : 0u);
-        } else if (k == 37u) {
-            off = 136u * nb - 1u; v = 0x80u | (len == 136u * nb - 1u ? 0x01u : 0u);
-        } else {
-            wr = false;
-        }
+        const uint32_t pair = (k + 1u) >> 1;
+        const uint32_t hb_off = (pair == 1u ? 1u : pair == 2u ? o_root : pair == 3u ? o_txp : o_rec) + ((k & 1u) ? 0u : 2u);
+        const uint32_t hb_v = (k & 1u) ? 0xdcu : 0x20u;
+        const uint32_t ih = k - 9u, it = k - 14u, ie = k - 23u;
+        const uint64_t E0 = 0x2065736e696f439bull, E1 = 0xc065736162ull;
+        const uint32_t ev = (uint32_t)((ie < 8u ? E0 >> (8u * (ie & 7u)) : E1 >> (8u * ((ie - 8u) & 7u))) & 0xffu);
+        const bool last_byte = len == 136u * nb - 1u;
+        uint32_t off = k == 0u ? 0u : hb_off, v = k == 0u ? 0x9du : hb_v;
+        bool wr = k < 9u;
+        const bool in_h = (k >= 9u) & (k < 14u), in_t = (k >= 14u) & (k < 23u), in_e = (k >= 23u) & (k < 36u);
+        off = in_h ? o_h + ih : off;  v = in_h ? kw50_uint_byte(h, hl, ih) : v;  wr = in_h ? ih < hl : wr;
+        off = in_t ? o_t + it : off;  v = in_t ? kw50_uint_byte(time, tl, it) : v;  wr = in_t ? it < tl : wr;
+        off = in_e ? o_e + ie : off;  v = in_e ? ev : v;  wr = in_e | wr;
+        off = k == 36u ? len : off;  v = k == 36u ? (0x01u | (last_byte ? 0x80u : 0u)) : v;   // pad10*1
+        off = k == 37u ? 136u * nb - 1u : off;  v = k == 37u ? (0x80u | (last_byte ? 0x01u : 0u)) : v;
+        wr = wr | (k == 36u) | (k == 37u);
         if (wr) buf[off] = (uint8_t)v;
     }
     wv.sync();

@@ -176,7 +176,7 @@ struct Sim {
     uint32_t* bl_base;       // this wave's backlog slots (global, replay mode)
     uint32_t mlog_cnt;       // real-crypto mode: messages logged so far by this instance (segment-uniform)
 #ifdef BFT_STAMPS
-    uint64_t st_acc[12];
+    uint64_t st_acc[NSTAMP];
     uint64_t st_t;
 #define BFT_STAMP(k) do { uint64_t t_ = wv.clock(); st_acc[k] += t_ - st_t; st_t = t_; } while (0)
 #else
@@ -1374,10 +1374,12 @@ struct Sim {
         if (path == PATH_NONE) return;
         if (path == PATH_PP) {                        // one Preprepare: its handler at every receiver
             if (!core_dead && mk.get(ps.pp_src)) handle_preprepare(ps.pp_src, ps.pp_h, ps.pp_r, ps.pp_b, ps.pp_eq != 0);
+            BFT_STAMP(12);
             return;
         }
         if (path == PATH_RC) {
             deliver_round_change(ps, mk, off);
+            BFT_STAMP(13);
             return;
         }
         if (path == PATH_BLK) {                       // block gossip with one range
@@ -1441,7 +1443,7 @@ struct Sim {
     // ---------------------------------------------------------------- the run
     BFT_FN void run() {
 #ifdef BFT_STAMPS
-        for (int k = 0; k < 12; ++k) st_acc[k] = 0;
+        for (int k = 0; k < NSTAMP; ++k) st_acc[k] = 0;
         st_t = wv.clock();
 #endif
         // resume mode (S == 64): only instances a FAST launch handed over, from their saved phase
@@ -1494,6 +1496,8 @@ struct Sim {
 #ifdef BFT_STAMPS
                 st_acc[6] += 1;                               // phases (a count, not cycles)
                 st_acc[11] += path == PATH_GENERAL ? 1 : 0;   // general-path phases
+                st_acc[14] += path == PATH_RC ? 1 : 0;        // round-change phases
+                st_acc[15] += path == PATH_NONE ? 1 : 0;      // phases with nothing in flight
 #endif
                 // records go to LDS only if some segment of the wave takes the general path
                 const bool pub = ballot(path == PATH_GENERAL).any();
@@ -1522,7 +1526,7 @@ struct Sim {
 #ifdef BFT_STAMPS
         BFT_STAMP(7);
         if (lane == 0 && P.stamps)
-            for (int k = 0; k < 12; ++k) P.stamps[(uint64_t)(S >= 64 ? inst_local : inst_local / (64u / S)) * 12 + k] = st_acc[k];
+            for (int k = 0; k < NSTAMP; ++k) P.stamps[(uint64_t)(S >= 64 ? inst_local : inst_local / (64u / S)) * NSTAMP + k] = st_acc[k];
 #endif
         // outputs (segment lane 0); instance-rounds = sum of (round + 1) over heights <= H
         uint32_t lf = seg_or(lane_flags);

@@ -562,13 +562,13 @@ extern "C" {
 
 #ifdef BFT_STAMPS
 // diagnostic builds only: per-section cycle sums of the last launch, summed over waves
-int bftsim_debug_stamps(uint64_t out[12]) {
-    std::vector<uint64_t> v(g_stamp_waves * 12);
+int bftsim_debug_stamps(uint64_t out[bft::NSTAMP]) {
+    std::vector<uint64_t> v(g_stamp_waves * bft::NSTAMP);
     if (hipDeviceSynchronize() != hipSuccess) return -2;
     if (hipMemcpy(v.data(), g_stamps, v.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return -2;
-    for (int k = 0; k < 12; ++k) out[k] = 0;
+    for (int k = 0; k < bft::NSTAMP; ++k) out[k] = 0;
     for (uint64_t w = 0; w < g_stamp_waves; ++w)
-        for (int k = 0; k < 12; ++k) out[k] += v[w * 12 + k];
+        for (int k = 0; k < bft::NSTAMP; ++k) out[k] += v[w * bft::NSTAMP + k];
     return 0;
 }
 #endif
@@ -786,8 +786,8 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         static uint64_t cap = 0;
         uint64_t per = h->seg > 64 ? 1 : 64 / h->seg;
         uint64_t waves = (n + per - 1) / per;
-        if (waves > cap) { (void)hipFree(d_st); HIPCHECK(h, hipMalloc(&d_st, waves * 96)); cap = waves; }
-        HIPCHECK(h, hipMemsetAsync(d_st, 0, waves * 96, s));
+        if (waves > cap) { (void)hipFree(d_st); HIPCHECK(h, hipMalloc(&d_st, waves * 8 * bft::NSTAMP)); cap = waves; }
+        HIPCHECK(h, hipMemsetAsync(d_st, 0, waves * 8 * bft::NSTAMP, s));
         p.stamps = d_st;
         g_stamps = d_st;
         g_stamp_waves = waves;

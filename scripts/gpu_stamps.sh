@@ -12,7 +12,7 @@ sim.prepare(16384)
 for _ in range(2):
     sim.launch(0)
     sim.sync()
-out = (ctypes.c_uint64 * 12)()
+out = (ctypes.c_uint64 * 16)()
 runtime.lib().bftsim_debug_stamps(out)
 names = ["t_step", "classify", "event_step", "deliver_pp", "deliver_pc", "deliver_blk", "resolve", "loop/other", "#phases", "#pp", "#pc", "#blk"]
 cnt = (8, 9, 10, 11)

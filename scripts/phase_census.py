@@ -20,11 +20,15 @@ PATHS = {0: "GENERAL", 1: "BLK", 2: "PC", 3: "NONE", 4: "PP", 5: "RC"}
 
 def census(cfg, n):
     E.run(cfg, 0, n)
+    E.run(cfg, 0, n)
     keys = np.zeros(4096, np.uint32); cnt = np.zeros(4096, np.uint64)
     m = L.emu_census(keys.ctypes.data, cnt.ctypes.data, 4096)
     tot = int(cnt[:m].sum())
     rows = sorted(zip(cnt[:m], keys[:m]), reverse=True)
-    print(f"== {cfg.name}: {tot} segment-phases")
+    r = E.run(cfg, 0, n)
+    views = int(r["views"].sum())
+    print(f"== {cfg.name}: {tot // 2} segment-phases for {views} instance-rounds ({tot / 2 / max(views, 1):.2f} per "
+          f"instance-round)")
     for c, k in rows[:14]:
         kinds = "+".join(n for i, n in enumerate(KN) if k >> i & 1) or "-"
         nu = "".join(x for i, x in ((7, "pr"), (8, "cm"), (9, "blk")) if k >> i & 1)
