@@ -292,14 +292,20 @@ BFT_FN uint32_t delivery_offset(uint64_t seed, uint32_t n, uint32_t inst, uint32
     return offset_from_parts(seed, n, offset_tick_part(offset_inst_part(seed, inst), tick), phase, recv);
 }
 
-// N-bit delivery mask of receiver `recv` for (tick, phase); self always delivered.
-template <int NW>
+// N-bit delivery mask of receiver `recv` for (tick, phase); self always delivered. Only the bits of the
+// senders in `present` are meaningful: the Philox draw of an 8-sender block with no sender present is
+// skipped (its bits stay 0), which leaves every delivered message unchanged (SPEC.md §3 fixes the draw of
+// each (receiver, block), not the order of the draws).
+// SKIP = false computes every block (the skip is a branch in the loop; for small segments, where one or
+// two blocks cover the instance, it only costs registers)
+template <int NW, bool SKIP = true>
 BFT_FN Bits<NW> deliver_mask(uint64_t seed, uint32_t n, uint32_t thr16, uint32_t inst, uint32_t tick,
-                             uint32_t phase, uint32_t recv) {
+                             uint32_t phase, uint32_t recv, const Bits<NW>& present) {
     Bits<NW> all = Bits<NW>::low(n);
     if (thr16 == 0) return all;
     Bits<NW> m = Bits<NW>::zero();
     for (uint32_t j = 0; 8 * j < n; ++j) {
+        if (SKIP && ((present.word((int)(j >> 3)) >> (8u * (j & 7u))) & 0xffull) == 0) continue;
         uint32_t w[4];
         philox(seed, inst, tick, (phase << 24) | (recv << 8) | j, DOM_DROP, w);
         uint64_t byte = 0;

@@ -753,7 +753,8 @@ struct Fast64 {
                     miner_step_p();   // a no-op for lanes without a queued event (miner_step_p guards the mining)
                     F64_STAMP(2);
                     if (path != P_NONE) {
-                        const uint64_t mk = LOSSY ? deliver_mask<1>(seed(), N, P.thr16, inst, (uint32_t)tick, p, me).w[0]
+                        const uint64_t mk = LOSSY ? deliver_mask<1>(seed(), N, P.thr16, inst, (uint32_t)tick, p, me,
+                                                                    Bits<1>::from(kpp | kpr | kcm | kblk)).w[0]
                                                   : ~0ull;
                         if (path == P_PC) {
                             const uint32_t off = offset_from_parts(seed(), N, off_tick, p, me);

@@ -129,6 +129,37 @@ struct GroupHip {
         return r;
     }
     __device__ void sync() { __syncthreads(); par ^= 1u; }
+    // batched collectives (one barrier each): K ballots; K words each written by at most one lane
+    // (wr[k]; an unwritten word reads as stale data, which the caller must not use)
+    __device__ uint64_t* big() const { return slot + 8 + par * 64u; }
+    template <int K> __device__ void ballot_k(const bool (&p)[K], Bits<NW> (&out)[K]) {
+        static_assert(K * NW <= 64, "batched ballot area");
+        uint64_t* s = big();
+        uint64_t b[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) b[k] = __ballot(p[k]);
+        if (__lane_id() == 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) s[k * NW + (threadIdx.x >> 6)] = b[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+            for (int w = 0; w < NW; ++w) out[k].w[w] = s[k * NW + w];
+        par ^= 1u;
+    }
+    template <int K> __device__ void gather_k(const bool (&wr)[K], const uint32_t (&v)[K], uint32_t (&out)[K]) {
+        static_assert(K <= 128, "batched gather area");
+        uint32_t* s = (uint32_t*)big();
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (wr[k]) s[k] = v[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < K; ++k) out[k] = s[k];
+        par ^= 1u;
+    }
     __device__ static uint64_t clock() { return __builtin_amdgcn_s_memtime(); }
     __device__ static uint32_t gload(const uint32_t* p) {
         return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -87,7 +87,10 @@ struct Layout {
     static_assert(L * CMT_STRIDE <= L * REC_WORDS, "commit hand-off must fit in the record area");
     static_assert(HIST_BINS * 4 <= 528, "histogram area");
     static constexpr uint32_t GRP_OFF = SEG_OFF + 256;
-    static constexpr uint32_t CHASH_OFF = SEG_OFF + 512;
+    // group collectives (S > 64): 2 parities x 4 words, then the batched ballots / gathers of summarize,
+    // 2 parities x GRP_BIG words (bft_hip.h GroupHip)
+    static constexpr uint32_t GRP_BYTES = S > 64 ? 64u + 2u * 8u * 64u : 256u;
+    static constexpr uint32_t CHASH_OFF = GRP_OFF + GRP_BYTES;
     static constexpr uint32_t SCR_OFF = CHASH_OFF + L * 32;
     static constexpr uint32_t BYTES_POW2 = CHASH_OFF;
     static constexpr uint32_t BYTES_SEED = S > 64 ? SCR_OFF : SCR_OFF + 64 * LANE_HASH_BUF;
@@ -1142,7 +1145,58 @@ struct Sim {
         else return wv.shfl(v, seg_base + j);
     }
 
+    // S > 64 (one instance per workgroup): the same summary with three batched collectives (one barrier
+    // each) instead of one barrier per ballot and per leader value: the kinds and digest-variant masks,
+    // the leaders' message fields, the uniformity checks
+    BFT_FN void summarize_group(PhaseSummary& ps) {
+        const uint32_t f = nx.f;
+        const bool pp = (f & F_PP) != 0, pr = (f & F_PR) != 0, cm = (f & F_CM) != 0, bk = (f & F_BLK) != 0,
+                   rc = (f & F_RC) != 0, prw = (f & F_PR_W) != 0, cmw = (f & F_CM_W) != 0;
+        const bool pv1 = blk_var(nx.pr_d) == 1, cv1 = blk_var(nx.cm_d) == 1;
+        const bool pred[13] = {pp, pr, cm, (f & F_OCM) != 0, rc, (f & F_SYNC) != 0, bk, (bool)(pr & prw),
+                               (bool)(pr & !prw & !pv1), (bool)(pr & !prw & pv1), (bool)(cm & cmw),
+                               (bool)(cm & !cmw & !cv1), (bool)(cm & !cmw & cv1)};
+        M bl[13];
+        wv.template ballot_k<13>(pred, bl);
+        ps.k_pp = bl[0]; ps.k_pr = bl[1]; ps.k_cm = bl[2]; ps.k_ocm = bl[3]; ps.k_rc = bl[4]; ps.k_sync = bl[5];
+        ps.k_blk = bl[6]; ps.pr_w = bl[7]; ps.pr_v0 = bl[8]; ps.pr_v1 = bl[9]; ps.cm_w = bl[10]; ps.cm_v0 = bl[11];
+        ps.cm_v1 = bl[12];
+        // the first sender of each kind publishes its message fields
+        const uint32_t jpp = ps.k_pp.any() ? ps.k_pp.ctz_nz() : S, jpr = ps.k_pr.any() ? ps.k_pr.ctz_nz() : S,
+                       jcm = ps.k_cm.any() ? ps.k_cm.ctz_nz() : S, jbk = ps.k_blk.any() ? ps.k_blk.ctz_nz() : S,
+                       jrc = ps.k_rc.any() ? ps.k_rc.ctz_nz() : S;
+        const uint64_t pcls = nx.pr_d & BLK_HP_MASK, ccls = nx.cm_d & BLK_HP_MASK;
+        const bool lpp = me == jpp, lpr = me == jpr, lcm = me == jcm, lbk = me == jbk, lrc = me == jrc;
+        const bool wr[17] = {lpp, lpp, lpp, lpp, lpp, lpr, lpr, lpr, lpr, lcm, lcm, lcm, lcm, lbk, lbk, lrc, lrc};
+        const uint32_t val[17] = {nx.pp_h, nx.pp_r, (uint32_t)nx.pp_b, (uint32_t)(nx.pp_b >> 32), f & F_PP_EQ,
+                                  nx.pr_h, nx.pr_r, (uint32_t)pcls, (uint32_t)(pcls >> 32),
+                                  nx.cm_h, nx.cm_r, (uint32_t)ccls, (uint32_t)(ccls >> 32),
+                                  nx.blk_lo, nx.blk_hi, nx.rc_h, nx.rc_r};
+        uint32_t g[17];
+        wv.template gather_k<17>(wr, val, g);
+        const bool any_pp = ps.k_pp.any(), any_pr = ps.k_pr.any(), any_cm = ps.k_cm.any(), any_bk = ps.k_blk.any(),
+                   any_rc = ps.k_rc.any();
+        ps.pp_src = any_pp ? jpp : 0u;
+        ps.pp_h = any_pp ? g[0] : 0u; ps.pp_r = any_pp ? g[1] : 0u;
+        ps.pp_b = any_pp ? ((uint64_t)g[2] | ((uint64_t)g[3] << 32)) : 0ull; ps.pp_eq = any_pp ? g[4] : 0u;
+        ps.pr_h = any_pr ? g[5] : 0u; ps.pr_r = any_pr ? g[6] : 0u;
+        ps.pr_cls = any_pr ? ((uint64_t)g[7] | ((uint64_t)g[8] << 32)) : 0ull;
+        ps.cm_h = any_cm ? g[9] : 0u; ps.cm_r = any_cm ? g[10] : 0u;
+        ps.cm_cls = any_cm ? ((uint64_t)g[11] | ((uint64_t)g[12] << 32)) : 0ull;
+        ps.blk_lo = any_bk ? g[13] : 0u; ps.blk_hi = any_bk ? g[14] : 0u;
+        ps.rc_h = any_rc ? g[15] : 0u; ps.rc_r = any_rc ? g[16] : 0u;
+        // uniformity against the leaders
+        const bool mm[4] = {(bool)(pr & ((nx.pr_h != ps.pr_h) | (nx.pr_r != ps.pr_r) | (pcls != ps.pr_cls))),
+                            (bool)(cm & ((nx.cm_h != ps.cm_h) | (nx.cm_r != ps.cm_r) | (ccls != ps.cm_cls))),
+                            (bool)(bk & ((nx.blk_lo != ps.blk_lo) | (nx.blk_hi != ps.blk_hi))),
+                            (bool)(rc & ((nx.rc_h != ps.rc_h) | (nx.rc_r != ps.rc_r)))};
+        M mb[4];
+        wv.template ballot_k<4>(mm, mb);
+        ps.u_pr = mb[0].none(); ps.u_cm = mb[1].none(); ps.u_blk = mb[2].none(); ps.u_rc = mb[3].none();
+    }
+
     BFT_FN void summarize(PhaseSummary& ps) {
+        if constexpr (S > 64) { summarize_group(ps); return; }
         const uint32_t f = nx.f;
         ps.k_pp = seg_bits(ballot((f & F_PP) != 0));
         ps.k_pr = seg_bits(ballot((f & F_PR) != 0));
@@ -1506,7 +1560,12 @@ struct Sim {
                 BFT_STAMP(2);
                 if (act & seg_pending) {
                     miner_step();                             // event step
-                    M mk = deliver_mask<NW>(P.seed, nval(), P.thr16, inst, (uint32_t)tick, p, me);
+                    // the draws of the senders in flight only (a Preprepare phase: one block of 8)
+                    const M present = path == PATH_PP ? M::bit(ps.pp_src)
+                                    : (ps.k_pp | ps.k_pr | ps.k_cm | ps.k_ocm | ps.k_rc | ps.k_sync | ps.k_blk);
+                    M mk = path == PATH_NONE ? M::zero()
+                                             : deliver_mask<NW, (S >= 64)>(P.seed, nval(), P.thr16, inst, (uint32_t)tick, p,
+                                                                             me, present);
                     uint32_t off = (path == PATH_GENERAL || path == PATH_PC || path == PATH_RC)
                                        ? offset_from_parts(P.seed, nval(), off_tick, p, me) : 0u;
                     BFT_STAMP(5);

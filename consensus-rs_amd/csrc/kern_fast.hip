@@ -11,7 +11,7 @@ namespace bft {
 #define BFT_FAST_WAVES_PER_SIMD 6   // measured best of 4..8 (profiles/r02: 4 → 3.86e8, 5 → 3.97e8, 6 → 4.17e8, 7 → 3.69e8)
 #endif
 #ifndef BFT_FAST_SEEDED_WAVES_PER_SIMD
-#define BFT_FAST_SEEDED_WAVES_PER_SIMD 5   // the in-kernel wave hash needs registers: 6 spills SGPRs to scratch
+#define BFT_FAST_SEEDED_WAVES_PER_SIMD 4   // the in-kernel wave hash needs registers: 5 spills to scratch (gpurun r03c: 4 waves +6 %)
 #endif
 template <bool LOSSY, bool SEEDED>
 __global__ __launch_bounds__(64, SEEDED ? BFT_FAST_SEEDED_WAVES_PER_SIMD : BFT_FAST_WAVES_PER_SIMD)

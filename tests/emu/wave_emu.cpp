@@ -143,6 +143,13 @@ struct EmuGroup {
     uint32_t grp_or(uint32_t v) { return (uint32_t)collective(7, v); }
     uint64_t grp_sum64(uint32_t v) { return collective(8, v); }
     void sync() { collective(3, 0); }
+    template <int K> void ballot_k(const bool (&p)[K], bft::Bits<NW> (&out)[K]) {
+        for (int k = 0; k < K; ++k) out[k] = ballot(p[k]);
+    }
+    // one gather per word: the value of the (unique) writing lane, 0 if none
+    template <int K> void gather_k(const bool (&wr)[K], const uint32_t (&v)[K], uint32_t (&out)[K]) {
+        for (int k = 0; k < K; ++k) out[k] = (uint32_t)collective(9, (uint64_t)v[k] | ((uint64_t)(wr[k] ? 1u : 0u) << 32));
+    }
     static uint64_t clock() { return 0; }
     static uint32_t gload(const uint32_t* p) { return *p; }
     static void gstore(uint32_t* p, uint32_t v) { *p = v; }
@@ -249,6 +256,14 @@ int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds, int
             for (int l = 1; l < nl; ++l)
                 if ((uint32_t)(s.arg[l] >> 32) != j) { fprintf(stderr, "emu: non-uniform bcast source\n"); return -1; }
             for (int l = 0; l < nl; ++l) s.res[l] = (uint32_t)s.arg[j];
+        } else if (op == 9) {                 // gather: the writing lane's value (more than one: abort)
+            int wl = -1;
+            for (int l = 0; l < nl; ++l)
+                if (s.arg[l] >> 32) {
+                    if (wl >= 0) { fprintf(stderr, "emu: two writers of one gathered word\n"); return -1; }
+                    wl = l;
+                }
+            for (int l = 0; l < nl; ++l) s.res[l] = wl >= 0 ? (uint32_t)s.arg[wl] : 0u;
         } else if (op >= 6 && op <= 8) {
             uint64_t r = 0;
             for (int l = 0; l < nl; ++l) {
