@@ -178,7 +178,7 @@ BFT_FN bool rd_bytes_var(S& s, uint32_t t, uint32_t max, uint8_t* out, uint32_t&
 }
 template <class S>
 BFT_FN bool rd_tx(S& s, bftwire_tx& t) {
-    uint32_t n, tag, len;
+    uint32_t n, tag;
     if (!rd_arr(s, n) || n != 7) return false;
     if (!rd_uint(s, t.nonce) || !rd_uint(s, t.price) || !rd_uint(s, t.gas_limit)) return false;
     if (!s.get(tag)) return false;

@@ -9,11 +9,23 @@
 
 namespace bft {
 
-template <bool NEED_SEED, int MODE, uint32_t S>
 #ifndef BFT_WAVES_PER_SIMD
 #define BFT_WAVES_PER_SIMD 3   // register budget of the one-wave kernels (LDS allows ~2.75 per SIMD)
 #endif
-__global__ __launch_bounds__(S > 64 ? S : 64, S > 64 ? 1 : BFT_WAVES_PER_SIMD) void bft_consensus_kernel(Params p) {
+// workgroups per CU of the segment kernels (S = 128 / 256 lanes per instance). With one the S = 256
+// body got 256 VGPRs + 46 AGPRs, one wave per SIMD, and a CU waited on one instance's barriers;
+// two per CU spill 168 B/lane but run cfg4 N = 256 1.65x faster (profiles/r03/ab_cfg4)
+#ifndef BFT_WG_PER_CU_256
+#define BFT_WG_PER_CU_256 2
+#endif
+#ifndef BFT_WG_PER_CU_128
+#define BFT_WG_PER_CU_128 4
+#endif
+template <uint32_t S>
+constexpr int min_blocks_per_cu() { return S == 256 ? BFT_WG_PER_CU_256 : S == 128 ? BFT_WG_PER_CU_128 : BFT_WAVES_PER_SIMD; }
+
+template <bool NEED_SEED, int MODE, uint32_t S>
+__global__ __launch_bounds__(S > 64 ? S : 64, min_blocks_per_cu<S>()) void bft_consensus_kernel(Params p) {
     extern __shared__ uint8_t lds[];
     if constexpr (S > 64) {
         Sim<GroupHip<(int)(S / 64)>, NEED_SEED, S, MODE> sim(p, lds, blockIdx.x);

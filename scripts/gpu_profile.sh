@@ -2,13 +2,13 @@
 # Measurement pass of one workload (through gpurun): bench line with the CPU baseline, rocprofv3 kernel
 # stats, and separate PMC passes (FETCH_SIZE, WRITE_SIZE, SQ) — counters never share a pass with
 # traces other than --kernel-trace/--stats. Summary: <out>/pmc_summary.json (scripts/pmc_summary.py).
-# usage: scripts/gpu_profile.sh [workload] [extra bench args...]   (outputs under gpurun_out/prof/<workload>)
+# usage: [NAME=dir] scripts/gpu_profile.sh [workload] [extra bench args...]   (outputs under gpurun_out/prof/<NAME or workload>)
 set -o pipefail
 W=${1:-cfg3}; shift
 X="$*"
 export PYTHONUNBUFFERED=1
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-R=gpurun_out/prof/$W
+R=gpurun_out/prof/${NAME:-$W}
 mkdir -p $R
 S=${STEPS:-10}; PS=${PSTEPS:-3}; WU=${WARMUP:-2}; PWU=${PWARMUP:-1}
 lscpu | grep -E "Model name|^CPU\(s\)" > $R/host_cpu.txt; nproc > $R/host_nproc.txt
