@@ -380,6 +380,18 @@ def main():
                 "hbm": {"algorithmic_bytes": algo_bytes, "achieved_GBps": algo_bytes / (ms / 1e3) / 1e9,
                         "peak_GBps": HBM_PEAK / 1e9, "frac": algo_bytes / (ms / 1e3) / HBM_PEAK},
                 "kernel_ms": {"bft_consensus_kernel": cms, "bft_hash_kernel": hms},
+                # both kernels' fractions, whichever is dominant, and the whole step against the full
+                # per-instance-round model (consensus + one header hash per committed height). The hash
+                # pass's own time is exclusive only with --no-pipeline (pipelined, it runs beside the
+                # next launches' consensus kernels and its event time is stretched wall time)
+                "per_kernel": {
+                    "bft_consensus_kernel": {"ops": c_ops, "ms": cms,
+                                             "frac": c_ops / (cms / 1e3) / VALU_PEAK if cms > 0 else None},
+                    "bft_hash_kernel": {"ops": h_ops, "ms": hms, "exclusive": not pipelined,
+                                        "frac": h_ops / (hms / 1e3) / VALU_PEAK if hms > 0 and h_ops else None},
+                },
+                "step": {"ops": c_ops + h_ops, "ms": ms_step,
+                         "frac": (c_ops + h_ops) / (ms_step / 1e3) / VALU_PEAK},
                 "ops_model": "consensus 4*N*(3*ceil(N/64)+8) lane-ops per instance-round; "
                              "hash 14976 lane-ops per header (SURVEY.md 8d)",
             },

@@ -149,6 +149,20 @@ struct GroupHip {
             for (int w = 0; w < NW; ++w) out[k].w[w] = s[k * NW + w];
         par ^= 1u;
     }
+    // the phase summary's K ballots into the stable LDS area summary() ([K][NW], one barrier): read by
+    // every lane until the next phase (Sim::kmask), no register copies
+    __device__ uint64_t* summary() const { return slot + 8 + 2u * 64u; }
+    template <int K> __device__ void ballot_k_store(const bool (&p)[K], uint64_t* dst) {
+        uint64_t b[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) b[k] = __ballot(p[k]);
+        if (__lane_id() == 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) dst[k * NW + (threadIdx.x >> 6)] = b[k];
+        }
+        __syncthreads();
+        par ^= 1u;
+    }
     template <int K> __device__ void gather_k(const bool (&wr)[K], const uint32_t (&v)[K], uint32_t (&out)[K]) {
         static_assert(K <= 128, "batched gather area");
         uint32_t* s = (uint32_t*)big();

@@ -88,8 +88,8 @@ struct Layout {
     static_assert(HIST_BINS * 4 <= 528, "histogram area");
     static constexpr uint32_t GRP_OFF = SEG_OFF + 256;
     // group collectives (S > 64): 2 parities x 4 words, then the batched ballots / gathers of summarize,
-    // 2 parities x GRP_BIG words (bft_hip.h GroupHip)
-    static constexpr uint32_t GRP_BYTES = S > 64 ? 64u + 2u * 8u * 64u : 256u;
+    // 2 parities x 64 words, then the phase summary's 13 sender masks (bft_hip.h GroupHip::summary)
+    static constexpr uint32_t GRP_BYTES = S > 64 ? 64u + 2u * 8u * 64u + 13u * 8u * (uint32_t)NW : 256u;
     static constexpr uint32_t CHASH_OFF = GRP_OFF + GRP_BYTES;
     static constexpr uint32_t SCR_OFF = CHASH_OFF + L * 32;
     static constexpr uint32_t BYTES_POW2 = CHASH_OFF;
@@ -1105,8 +1105,15 @@ struct Sim {
 
     // ---------------------------------------------------------------- phase fast paths
     // Segment-wide summary of one phase's messages. All masks use segment-local sender bits.
+    // For S > 64 (one instance per workgroup) the 13 sender masks stay in LDS (GroupHip::summary(),
+    // read where a path needs them: kmask) instead of 13 x NW 64-bit registers per lane; the kinds
+    // present are the scalar bits `kinds`.
+    enum : uint32_t { KM_PP = 0, KM_PR, KM_CM, KM_OCM, KM_RC, KM_SYNC, KM_BLK, KM_PR_W, KM_PR_V0, KM_PR_V1,
+                      KM_CM_W, KM_CM_V0, KM_CM_V1, KM_COUNT };
+    static constexpr uint32_t KB_PP1 = 1u << 7;   // kinds: bit k = mask k nonempty (k < 7); KB_PP1: one Preprepare
     struct PhaseSummary {
-        M k_pp, k_pr, k_cm, k_ocm, k_rc, k_sync, k_blk;
+        uint32_t kinds;                                   // S > 64 only
+        M k_pp, k_pr, k_cm, k_ocm, k_rc, k_sync, k_blk;   // S <= 64 only
         M pr_v0, pr_v1, pr_w, cm_v0, cm_v1, cm_w;
         uint32_t pr_h, pr_r, cm_h, cm_r, blk_lo, blk_hi;
         uint64_t pr_cls, cm_cls;              // (height, proposer) class of the digests
@@ -1124,10 +1131,21 @@ struct Sim {
     enum : uint32_t { PATH_GENERAL = 0, PATH_BLK = 1, PATH_PC = 2, PATH_NONE = 3, PATH_PP = 4, PATH_RC = 5 };
     BFT_FN uint32_t classify(const PhaseSummary& ps) const {
         if (!P.fast) return PATH_GENERAL;
-        if ((ps.k_ocm | ps.k_sync).any()) return PATH_GENERAL;
-        const bool pc = ps.k_pr.any() || ps.k_cm.any(), blk = ps.k_blk.any(), pp = ps.k_pp.any();
-        if (ps.k_rc.any()) return (!pp && !pc && !blk && ps.u_rc) ? PATH_RC : PATH_GENERAL;
-        if (pp) return (!pc && !blk && ps.k_pp.popc() == 1u) ? PATH_PP : PATH_GENERAL;
+        if constexpr (S <= 64) {                      // the masks are registers: test them directly
+            if ((ps.k_ocm | ps.k_sync).any()) return PATH_GENERAL;
+            const bool pc = ps.k_pr.any() || ps.k_cm.any(), blk = ps.k_blk.any(), pp = ps.k_pp.any();
+            if (ps.k_rc.any()) return (!pp && !pc && !blk && ps.u_rc) ? PATH_RC : PATH_GENERAL;
+            if (pp) return (!pc && !blk && ps.k_pp.popc() == 1u) ? PATH_PP : PATH_GENERAL;
+            if (!pc) return blk ? (ps.u_blk ? PATH_BLK : PATH_GENERAL) : PATH_NONE;
+            if (!blk && ps.u_pr && ps.u_cm) return PATH_PC;
+            return PATH_GENERAL;
+        }
+        const uint32_t K = ps.kinds;
+        if (K & ((1u << KM_OCM) | (1u << KM_SYNC))) return PATH_GENERAL;
+        const bool pc = (K & ((1u << KM_PR) | (1u << KM_CM))) != 0, blk = (K & (1u << KM_BLK)) != 0,
+                   pp = (K & (1u << KM_PP)) != 0;
+        if (K & (1u << KM_RC)) return (!pp && !pc && !blk && ps.u_rc) ? PATH_RC : PATH_GENERAL;
+        if (pp) return (!pc && !blk && (K & KB_PP1) != 0) ? PATH_PP : PATH_GENERAL;
         if (!pc) return blk ? (ps.u_blk ? PATH_BLK : PATH_GENERAL) : PATH_NONE;
         if (!blk && ps.u_pr && ps.u_cm) return PATH_PC;
         return PATH_GENERAL;
@@ -1145,6 +1163,29 @@ struct Sim {
         else return wv.shfl(v, seg_base + j);
     }
 
+    // sender mask `k` (KM_*) of the phase: a register of the summary (S <= 64) or the LDS copy (S > 64)
+    template <uint32_t k>
+    BFT_FN M kmask(const PhaseSummary& ps) const {
+        if constexpr (S > 64) {
+            M r;
+            const uint64_t* src = wv.summary() + k * (uint32_t)NW;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) r.w[w] = src[w];
+            return r;
+        } else {
+            static_assert(k < KM_COUNT, "mask index");
+            return k == KM_PP ? ps.k_pp : k == KM_PR ? ps.k_pr : k == KM_CM ? ps.k_cm : k == KM_OCM ? ps.k_ocm
+                 : k == KM_RC ? ps.k_rc : k == KM_SYNC ? ps.k_sync : k == KM_BLK ? ps.k_blk
+                 : k == KM_PR_W ? ps.pr_w : k == KM_PR_V0 ? ps.pr_v0 : k == KM_PR_V1 ? ps.pr_v1
+                 : k == KM_CM_W ? ps.cm_w : k == KM_CM_V0 ? ps.cm_v0 : ps.cm_v1;
+        }
+    }
+    // every sender with a message of any kind in flight
+    BFT_FN M kmask_any(const PhaseSummary& ps) const {
+        return kmask<KM_PP>(ps) | kmask<KM_PR>(ps) | kmask<KM_CM>(ps) | kmask<KM_OCM>(ps) | kmask<KM_RC>(ps) |
+               kmask<KM_SYNC>(ps) | kmask<KM_BLK>(ps);
+    }
+
     // S > 64 (one instance per workgroup): the same summary with three batched collectives (one barrier
     // each) instead of one barrier per ballot and per leader value: the kinds and digest-variant masks,
     // the leaders' message fields, the uniformity checks
@@ -1156,15 +1197,18 @@ struct Sim {
         const bool pred[13] = {pp, pr, cm, (f & F_OCM) != 0, rc, (f & F_SYNC) != 0, bk, (bool)(pr & prw),
                                (bool)(pr & !prw & !pv1), (bool)(pr & !prw & pv1), (bool)(cm & cmw),
                                (bool)(cm & !cmw & !cv1), (bool)(cm & !cmw & cv1)};
-        M bl[13];
-        wv.template ballot_k<13>(pred, bl);
-        ps.k_pp = bl[0]; ps.k_pr = bl[1]; ps.k_cm = bl[2]; ps.k_ocm = bl[3]; ps.k_rc = bl[4]; ps.k_sync = bl[5];
-        ps.k_blk = bl[6]; ps.pr_w = bl[7]; ps.pr_v0 = bl[8]; ps.pr_v1 = bl[9]; ps.cm_w = bl[10]; ps.cm_v0 = bl[11];
-        ps.cm_v1 = bl[12];
+        static_assert(KM_PP == 0 && KM_BLK == 6 && KM_CM_V1 == 12, "pred order = KM_* order");
+        wv.template ballot_k_store<13>(pred, wv.summary());
         // the first sender of each kind publishes its message fields
-        const uint32_t jpp = ps.k_pp.any() ? ps.k_pp.ctz_nz() : S, jpr = ps.k_pr.any() ? ps.k_pr.ctz_nz() : S,
-                       jcm = ps.k_cm.any() ? ps.k_cm.ctz_nz() : S, jbk = ps.k_blk.any() ? ps.k_blk.ctz_nz() : S,
-                       jrc = ps.k_rc.any() ? ps.k_rc.ctz_nz() : S;
+        const M kpp = kmask<KM_PP>(ps), kpr = kmask<KM_PR>(ps), kcm = kmask<KM_CM>(ps), kbk = kmask<KM_BLK>(ps),
+                krc = kmask<KM_RC>(ps);
+        ps.kinds = (kpp.any() ? 1u << KM_PP : 0u) | (kpr.any() ? 1u << KM_PR : 0u) | (kcm.any() ? 1u << KM_CM : 0u) |
+                   (kmask<KM_OCM>(ps).any() ? 1u << KM_OCM : 0u) | (krc.any() ? 1u << KM_RC : 0u) |
+                   (kmask<KM_SYNC>(ps).any() ? 1u << KM_SYNC : 0u) | (kbk.any() ? 1u << KM_BLK : 0u) |
+                   (kpp.popc() == 1u ? KB_PP1 : 0u);
+        const uint32_t jpp = kpp.any() ? kpp.ctz_nz() : S, jpr = kpr.any() ? kpr.ctz_nz() : S,
+                       jcm = kcm.any() ? kcm.ctz_nz() : S, jbk = kbk.any() ? kbk.ctz_nz() : S,
+                       jrc = krc.any() ? krc.ctz_nz() : S;
         const uint64_t pcls = nx.pr_d & BLK_HP_MASK, ccls = nx.cm_d & BLK_HP_MASK;
         const bool lpp = me == jpp, lpr = me == jpr, lcm = me == jcm, lbk = me == jbk, lrc = me == jrc;
         const bool wr[17] = {lpp, lpp, lpp, lpp, lpp, lpr, lpr, lpr, lpr, lcm, lcm, lcm, lcm, lbk, lbk, lrc, lrc};
@@ -1174,8 +1218,7 @@ struct Sim {
                                   nx.blk_lo, nx.blk_hi, nx.rc_h, nx.rc_r};
         uint32_t g[17];
         wv.template gather_k<17>(wr, val, g);
-        const bool any_pp = ps.k_pp.any(), any_pr = ps.k_pr.any(), any_cm = ps.k_cm.any(), any_bk = ps.k_blk.any(),
-                   any_rc = ps.k_rc.any();
+        const bool any_pp = kpp.any(), any_pr = kpr.any(), any_cm = kcm.any(), any_bk = kbk.any(), any_rc = krc.any();
         ps.pp_src = any_pp ? jpp : 0u;
         ps.pp_h = any_pp ? g[0] : 0u; ps.pp_r = any_pp ? g[1] : 0u;
         ps.pp_b = any_pp ? ((uint64_t)g[2] | ((uint64_t)g[3] << 32)) : 0ull; ps.pp_eq = any_pp ? g[4] : 0u;
@@ -1313,7 +1356,7 @@ struct Sim {
     // receiver's delivery order with prefix masks instead of one message at a time.
     BFT_FN void deliver_prepare_commit(const PhaseSummary& ps, const M& mk, uint32_t off) {
         M PRacc = M::zero(), CMacc = M::zero();
-        M prd = mk & ps.k_pr, cmd = mk & ps.k_cm;
+        M prd = mk & kmask<KM_PR>(ps), cmd = mk & kmask<KM_CM>(ps);
         if (prd.any()) {
             int res = check_message(2, ps.pr_h);
             if (res != 0) { if (res == 2) note_future_block(ps.pr_h); }
@@ -1322,7 +1365,7 @@ struct Sim {
         if (cmd.any()) {
             int res = check_message(3, ps.cm_h);
             if (res != 0) { if (res == 2) note_future_block(ps.cm_h); }
-            else if (ps.cm_h == h && ps.cm_r == r) CMacc = cmd & class_match(ps.cm_cls, ps.cm_v0, ps.cm_v1, ps.cm_w, pp);
+            else if (ps.cm_h == h && ps.cm_r == r) CMacc = cmd & class_match(ps.cm_cls, kmask<KM_CM_V0>(ps), kmask<KM_CM_V1>(ps), kmask<KM_CM_W>(ps), pp);
         }
         if (PRacc.none() && CMacc.none()) return;
         const uint32_t q = qval();
@@ -1335,7 +1378,7 @@ struct Sim {
         // one (|prep ∪ commit| only grows); commits of the last prepare's sender come after it.
         const bool trigB = PR.any() & ((U0 | PR | (CM & low(lastPR))).popc() > q);
         M lm = M::zero();
-        if (blk_valid(lock) && PR.any()) lm = rot(PRacc & class_match(ps.pr_cls, ps.pr_v0, ps.pr_v1, ps.pr_w, lock), off);
+        if (blk_valid(lock) && PR.any()) lm = rot(PRacc & class_match(ps.pr_cls, kmask<KM_PR_V0>(ps), kmask<KM_PR_V1>(ps), kmask<KM_PR_W>(ps), lock), off);
         const bool trig = trigB | lm.any();
         // commit quorum events (commit.rs:75-80) exist iff the final count is over q
         const bool cexists = CM.any() & ((C0 | CM).popc() > q);
@@ -1346,7 +1389,7 @@ struct Sim {
                 lastT = lastPR;                                 // every prepare from tB on
             } else {
                 // lock-match triggers only: the first one locks pp, later ones match pp
-                M mpp = rot(PRacc & class_match(ps.pr_cls, ps.pr_v0, ps.pr_v1, ps.pr_w, pp), off);
+                M mpp = rot(PRacc & class_match(ps.pr_cls, kmask<KM_PR_V0>(ps), kmask<KM_PR_V1>(ps), kmask<KM_PR_W>(ps), pp), off);
                 M T = (mpp & ~low(t1)) | M::bit(t1);
                 lastT = T.hibit();
             }
@@ -1386,7 +1429,7 @@ struct Sim {
     // set of R); it is found as a prefix count, as the prepare quorum of deliver_prepare_commit.
     BFT_FN void deliver_round_change(const PhaseSummary& ps, const M& mk, uint32_t off) {
         if (core_dead) return;                        // deliver_from: a panicked Core handles nothing
-        const M D = mk & ps.k_rc;
+        const M D = mk & kmask<KM_RC>(ps);
         if (D.none()) return;
         const uint32_t R = ps.rc_r;
         const int res = check_message(MT_ROUND_CHANGE, ps.rc_h);
@@ -1437,7 +1480,7 @@ struct Sim {
             return;
         }
         if (path == PATH_BLK) {                       // block gossip with one range
-            if ((mk & ps.k_blk & ~M::bit(me)).any()) handle_blocks(ps.blk_lo, ps.blk_hi);
+            if ((mk & kmask<KM_BLK>(ps) & ~M::bit(me)).any()) handle_blocks(ps.blk_lo, ps.blk_hi);
             BFT_STAMP(8);
             return;
         }
@@ -1448,7 +1491,7 @@ struct Sim {
         }
         // general path: every delivered non-empty sender, in rotated order, one at a time
         if (EXT && P.backlog_replay) replay_backlog();   // the stored messages first (SPEC.md §10)
-        M any = ps.k_pp | ps.k_pr | ps.k_cm | ps.k_ocm | ps.k_rc | ps.k_sync | ps.k_blk;
+        M any = kmask_any(ps);
         M c = rot(mk & any, off);
         while (c.any()) {
             uint32_t pos = c.ctz_nz();
@@ -1562,7 +1605,7 @@ struct Sim {
                     miner_step();                             // event step
                     // the draws of the senders in flight only (a Preprepare phase: one block of 8)
                     const M present = path == PATH_PP ? M::bit(ps.pp_src)
-                                    : (ps.k_pp | ps.k_pr | ps.k_cm | ps.k_ocm | ps.k_rc | ps.k_sync | ps.k_blk);
+                                    : kmask_any(ps);
                     M mk = path == PATH_NONE ? M::zero()
                                              : deliver_mask<NW, (S >= 64)>(P.seed, nval(), P.thr16, inst, (uint32_t)tick, p,
                                                                              me, present);

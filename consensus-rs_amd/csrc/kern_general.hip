@@ -12,14 +12,16 @@ namespace bft {
 #ifndef BFT_WAVES_PER_SIMD
 #define BFT_WAVES_PER_SIMD 3   // register budget of the one-wave kernels (LDS allows ~2.75 per SIMD)
 #endif
-// workgroups per CU of the segment kernels (S = 128 / 256 lanes per instance). With one the S = 256
-// body got 256 VGPRs + 46 AGPRs, one wave per SIMD, and a CU waited on one instance's barriers;
-// two per CU spill 168 B/lane but run cfg4 N = 256 1.65x faster (profiles/r03/ab_cfg4)
+// occupancy target of the segment kernels (S = 128 / 256 lanes per instance; the launch bound's second
+// argument, which the compiler turns into waves per SIMD). With 1 the S = 256 body got 256 VGPRs + 46
+// AGPRs, one wave per SIMD, and a CU waited on one instance's barriers; 2 runs cfg4 N = 256 1.65x
+// faster. S = 128: 2 (208 VGPRs, no spills) runs 1.63x faster than 4 (128 VGPRs, 376 B/lane spills).
+// (profiles/r03/ab_occupancy)
 #ifndef BFT_WG_PER_CU_256
 #define BFT_WG_PER_CU_256 2
 #endif
 #ifndef BFT_WG_PER_CU_128
-#define BFT_WG_PER_CU_128 4
+#define BFT_WG_PER_CU_128 2
 #endif
 template <uint32_t S>
 constexpr int min_blocks_per_cu() { return S == 256 ? BFT_WG_PER_CU_256 : S == 128 ? BFT_WG_PER_CU_128 : BFT_WAVES_PER_SIMD; }

@@ -21,9 +21,11 @@ static std::map<uint32_t, uint64_t> g_census;
 #define BFT_PHASE_CENSUS(ps, path, me)                                                                     \
     do {                                                                                                   \
         if ((me) == 0) {                                                                                   \
-            uint32_t k_ = (ps.k_pp.any() ? 1u : 0u) | (ps.k_pr.any() ? 2u : 0u) | (ps.k_cm.any() ? 4u : 0u) | \
-                          (ps.k_ocm.any() ? 8u : 0u) | (ps.k_rc.any() ? 16u : 0u) | (ps.k_sync.any() ? 32u : 0u) | \
-                          (ps.k_blk.any() ? 64u : 0u) | (ps.u_pr ? 0 : 128u) | (ps.u_cm ? 0 : 256u) |           \
+            uint32_t k_ = (S > 64 ? (ps.kinds & 127u)                                                       \
+                                  : ((ps.k_pp.any() ? 1u : 0u) | (ps.k_pr.any() ? 2u : 0u) | (ps.k_cm.any() ? 4u : 0u) | \
+                                     (ps.k_ocm.any() ? 8u : 0u) | (ps.k_rc.any() ? 16u : 0u) |               \
+                                     (ps.k_sync.any() ? 32u : 0u) | (ps.k_blk.any() ? 64u : 0u))) |          \
+                          (ps.u_pr ? 0 : 128u) | (ps.u_cm ? 0 : 256u) |                                     \
                           (ps.u_blk ? 0 : 512u) | ((uint32_t)(path) << 12);                                   \
             g_census[k_] += 1;                                                                             \
         }                                                                                                  \
@@ -130,7 +132,9 @@ struct EmuWave {
 // the workgroup flavour (S = 64*NW lanes): same collectives as GroupHip in bftsim.hip
 template <int NW>
 struct EmuGroup {
-    void init(uint8_t*) {}
+    uint64_t* slot = nullptr;    // the LDS group area (Layout::GRP_OFF), as GroupHip
+    void init(uint8_t* p) { slot = (uint64_t*)p; }
+    uint64_t* summary() const { return slot + 8 + 2 * 64; }
     static uint32_t lane() { return (uint32_t)g->cur; }
     bft::Bits<NW> ballot(bool p) {
         collective(1, p ? 1 : 0);
@@ -145,6 +149,14 @@ struct EmuGroup {
     void sync() { collective(3, 0); }
     template <int K> void ballot_k(const bool (&p)[K], bft::Bits<NW> (&out)[K]) {
         for (int k = 0; k < K; ++k) out[k] = ballot(p[k]);
+    }
+    template <int K> void ballot_k_store(const bool (&p)[K], uint64_t* dst) {
+        bft::Bits<NW> r[K];
+        for (int k = 0; k < K; ++k) r[k] = ballot(p[k]);
+        if (lane() == 0)
+            for (int k = 0; k < K; ++k)
+                for (int w = 0; w < NW; ++w) dst[k * NW + w] = r[k].w[w];
+        sync();
     }
     // one gather per word: the value of the (unique) writing lane, 0 if none
     template <int K> void gather_k(const bool (&wr)[K], const uint32_t (&v)[K], uint32_t (&out)[K]) {
