@@ -55,7 +55,10 @@ __global__ __launch_bounds__(64) void sig_sign_kernel(const Aff* gtab, const uin
 }
 
 // mode 0: recover (pub nullable, addr); mode 1: verify_address against addr_in
-__global__ __launch_bounds__(64) void sig_recover_kernel(const Aff* gtab, const uint8_t* dig, const uint8_t* sig,
+#ifndef SIG_RECOVER_WAVES
+#define SIG_RECOVER_WAVES 2
+#endif
+__global__ __launch_bounds__(64, SIG_RECOVER_WAVES) void sig_recover_kernel(const Aff* gtab, const uint8_t* dig, const uint8_t* sig,
                                                          uint64_t n, uint8_t* pub, uint8_t* addr,
                                                          const uint8_t* addr_in, uint8_t* ok) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -504,8 +504,39 @@ SECP_FN void split_lambda(const U256& k, U256& r1, U256& r2) {
     r2 = sc_add(sc_mul(c1, c_mb1()), sc_mul(c2, c_mb2()));
     r1 = sc_add(k, sc_neg(sc_mul(r2, c_lambda())));
 }
-// k * P: GLV split, then signed 4-bit digits of both 128-bit halves (k' = k + 0x88..8, 32 nibbles) in
-// one doubling chain; table 1P..8P (Jacobian), the lambda table derived on the fly as (beta X, +-Y, Z)
+// Radix-8 signed digits of a GLV half k (|k| < 2^128): k' = k + 4 * (8^43 - 1) / 7 < 2^130, then
+// k = top * 2^129 + sum_{i < 43} d_i 8^i with d_i = ((k' >> 3i) & 7) - 4 in [-4, 3] and top = k' >> 129
+SECP_FN uint32_t r8_digit(const U256& kp, uint32_t i) {        // (k' >> 3i) & 7, i < 43
+    const uint32_t b = 3u * i, w = b >> 5, o = b & 31u;
+    const uint32_t lo = kp.v[w] >> o;
+    const uint32_t hi = (o > 29u && w < 7u) ? (kp.v[w + 1] << (32u - o)) : 0u;
+    return (lo | hi) & 7u;
+}
+SECP_FN U256 r8_bias() {                                       // 4 * (8^43 - 1) / 7 = 0b100100...100 (43 x '100')
+    U256 r = u_zero();
+    for (uint32_t i = 0; i < 43; ++i) {
+        const uint32_t b = 3u * i + 2u;
+        r.v[b >> 5] |= 1u << (b & 31u);
+    }
+    return r;
+}
+// entry j (0..3, lane-varying) of the affine table by selects: a dynamic index into a register array
+// would put the whole table in scratch memory (round 2: 944 B/lane for an 8-point Jacobian table)
+SECP_FN Aff aff_select4(const Aff& t0, const Aff& t1, const Aff& t2, const Aff& t3, uint32_t j) {
+    Aff r;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t x01 = (j & 1u) ? t1.x.v[k] : t0.x.v[k], x23 = (j & 1u) ? t3.x.v[k] : t2.x.v[k];
+        const uint32_t y01 = (j & 1u) ? t1.y.v[k] : t0.y.v[k], y23 = (j & 1u) ? t3.y.v[k] : t2.y.v[k];
+        r.x.v[k] = (j & 2u) ? x23 : x01;
+        r.y.v[k] = (j & 2u) ? y23 : y01;
+    }
+    return r;
+}
+// k * P: GLV split, then radix-8 signed digits of both 128-bit halves in one doubling chain (129
+// doublings, <= 86 mixed additions). The table 1q..4q is made affine with one shared inversion
+// (Montgomery's trick), so every addition is mixed (7M + 4S) and the table is 64 registers selected
+// by value, not a scratch-memory array; the lambda table is derived on the fly as (beta x, +-y).
 SECP_FN Jac mul_var(const U256& k, const Aff& p) {
     U256 k1, k2;
     split_lambda(k, k1, k2);
@@ -515,36 +546,50 @@ SECP_FN Jac mul_var(const U256& k, const Aff& p) {
     Aff q = p;
     if (n1) q.y = fe_neg(q.y);
     const bool flip2 = n1 != n2;                 // lambda table = lambda * (i q), negated when the signs differ
-    Jac tbl[8];
-    tbl[0] = jac_from_aff(q);
-    for (int i = 1; i < 8; ++i) tbl[i] = jac_add_aff(tbl[i - 1], q);
-    U256 eights = u_zero(), k1p, k2p;
-    for (int i = 0; i < 4; ++i) eights.v[i] = 0x88888888u;
-    u_add(k1p, k1, eights);
-    u_add(k2p, k2, eights);
+    Aff t0 = q, t1, t2, t3;
+    {
+        const Jac j1 = jac_dbl(jac_from_aff(q));                 // 2q, 3q, 4q (never infinity: prime order)
+        const Jac j2 = jac_add_aff(j1, q);
+        const Jac j3 = jac_dbl(j1);
+        const U256 c12 = fe_mul(j1.z, j2.z), c123 = fe_mul(c12, j3.z);
+        U256 inv = fe_inv(c123);
+        const U256 z3 = fe_mul(inv, c12);                         // 1 / z3
+        inv = fe_mul(inv, j3.z);                                  // 1 / (z1 z2)
+        const U256 z2 = fe_mul(inv, j1.z);
+        const U256 z1 = fe_mul(inv, j2.z);
+        const U256 z1s = fe_sqr(z1), z2s = fe_sqr(z2), z3s = fe_sqr(z3);
+        t1.x = fe_mul(j1.x, z1s); t1.y = fe_mul(j1.y, fe_mul(z1s, z1));
+        t2.x = fe_mul(j2.x, z2s); t2.y = fe_mul(j2.y, fe_mul(z2s, z2));
+        t3.x = fe_mul(j3.x, z3s); t3.y = fe_mul(j3.y, fe_mul(z3s, z3));
+    }
+    const U256 bias = r8_bias();
+    U256 k1p, k2p;
+    u_add(k1p, k1, bias);
+    u_add(k2p, k2, bias);
     const U256 beta = c_beta();
     Jac acc = jac_inf();
-    if (k1p.v[4] & 1u) acc = jac_add(acc, tbl[0]);
-    if (k2p.v[4] & 1u) {
-        Jac t = tbl[0];
+    if ((k1p.v[4] >> 1) & 1u) acc = jac_add_aff(acc, t0);       // bit 129: top = 1
+    if ((k2p.v[4] >> 1) & 1u) {
+        Aff t = t0;
         t.x = fe_mul(t.x, beta);
         if (flip2) t.y = fe_neg(t.y);
-        acc = jac_add(acc, t);
+        acc = jac_add_aff(acc, t);
     }
-    for (int w = 31; w >= 0; --w) {
-        if (!acc.inf) { acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); }
-        const int d1 = (int)u_nibble(k1p, (uint32_t)w) - 8;
+#pragma unroll 1
+    for (int w = 42; w >= 0; --w) {
+        if (!acc.inf) { acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); }
+        const int d1 = (int)r8_digit(k1p, (uint32_t)w) - 4;
         if (d1 != 0) {
-            Jac t = tbl[(d1 > 0 ? d1 : -d1) - 1];
+            Aff t = aff_select4(t0, t1, t2, t3, (uint32_t)((d1 > 0 ? d1 : -d1) - 1));
             if (d1 < 0) t.y = fe_neg(t.y);
-            acc = jac_add(acc, t);
+            acc = jac_add_aff(acc, t);
         }
-        const int d2 = (int)u_nibble(k2p, (uint32_t)w) - 8;
+        const int d2 = (int)r8_digit(k2p, (uint32_t)w) - 4;
         if (d2 != 0) {
-            Jac t = tbl[(d2 > 0 ? d2 : -d2) - 1];
+            Aff t = aff_select4(t0, t1, t2, t3, (uint32_t)((d2 > 0 ? d2 : -d2) - 1));
             t.x = fe_mul(t.x, beta);
             if ((d2 < 0) != flip2) t.y = fe_neg(t.y);
-            acc = jac_add(acc, t);
+            acc = jac_add_aff(acc, t);
         }
     }
     return acc;
