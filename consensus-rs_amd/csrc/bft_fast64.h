@@ -60,7 +60,7 @@ struct Fast64 {
                               L_PENDV = 256u, L_CMT = 512u, L_PROP = 1024u,   // L_PROP: proposer is set (= 0)
                               L_OBX = 2048u,   // FLAG_OUTBOX of this lane (a second message of a kind in one phase)
                               L_SYNCP = 4096u; // W_SYNC (the delayed sync check's height) is nonzero
-    enum : uint32_t { P_GENERAL = 0, P_BLK = 1, P_PC = 2, P_PP = 3, P_NONE = 4 };
+    enum : uint32_t { P_GENERAL = 0, P_BLK = 1, P_PC = 2, P_PP = 3, P_NONE = 4, P_CANON = 5 };
 
     const Params& P;
     uint8_t* lds;
@@ -396,11 +396,10 @@ struct Fast64 {
 
     // ------------------------------------------------------------------ handlers
     // HandlePreprepare::handle (preprepare.rs:45-126) of the phase's single Preprepare (uniform src, view)
-    BFT_FN void handle_preprepare_p(bool c, uint32_t src, uint32_t vh, uint64_t b, bool equiv) {
-        if (equiv) {                                             // SPEC.md §6: variant 1 to SPLIT receivers
-            const uint64_t sm = split_mask(vh);
-            b |= ((me != src) & (((sm >> me) & 1ull) != 0)) ? (1ull << 33) : 0ull;
-        }
+    // sm: the SPLIT bits of view (vh, 0) if the proposer equivocates, else 0 (split_mask)
+    BFT_FN void handle_preprepare_p(bool c, uint32_t src, uint32_t vh, uint64_t b, uint64_t sm) {
+        // SPEC.md §6: variant 1 to SPLIT receivers
+        b |= ((me != src) & (((sm >> me) & 1ull) != 0)) ? (1ull << 33) : 0ull;
         // check_message (core.rs:366-399) of a Preprepare of height vh (uniform): Unknown for 0, OK at h,
         // FutureBlock above h (falls through), OldMessage below
         const bool vok = vh != 0;
@@ -611,6 +610,67 @@ struct Fast64 {
         return 0;
     }
 
+    // ------------------------------------------------------------------ the canonical height, composed
+    // Lossless schedule. When the honest round-0 proposer's Preprepare (view (H, 0); validator 0 with
+    // big-endian seeds, seed(tip) mod 64 with little-endian ones) is the only message in flight and every validator waits for it in the state
+    // start_new_zero_round left (core.rs:441-470: AcceptRequest, unlocked, chain tip H - 1, nothing
+    // queued for the miner), the next four phases have one outcome, and this applies it directly:
+    //   PP  — everyone accepts (preprepare.rs:87-106): pp = b, Preprepared, send_prepare; the Byzantine
+    //         validators also commit at once (SPEC.md §6);
+    //   PC1 — 64 Prepares > Q (prepare.rs:59-63): lock_hash, Prepared, send_commit (the Byzantine ones'
+    //         Commits are outbound-cache hits, backend.rs:141-148); their ≤ Q early Commits fire nothing;
+    //   PC2 — the honest Commits complete 64 > Q (commit.rs:63-82): Committed, Core::commit →
+    //         insert_block (chain.rs:45-71), Blocks out, NewHeader queued;
+    //   BLK — the fused block-gossip phase of `run` (ChainError::Exists for everyone) → the miner step.
+    // The preconditions make each phase's closed form (handle_preprepare_p, deliver_pc,
+    // resolve_commits, the fused phase) take exactly this branch; `macro_ok` (set once per instance)
+    // adds every validator running and at most Q Byzantine ones (their early Commits never reach the
+    // commit quorum in PC1). Bit-identical by construction; checked by the emulator suite and fuzzer.
+    bool macro_ok;
+    // It runs in place of the PP phase's classification; the PP phase's event step is skipped, being a
+    // no-op (nothing queued for the miner), and the phase's resolve_commits and fused block phase then
+    // run unchanged, so the single call sites of record_canon / hash_pending stay single.
+    // j: the Preprepare's sender, fj its flags, H its height, sm as in handle_preprepare_p
+    BFT_FN bool canonical_step(uint32_t j, uint32_t fj, uint32_t H) {
+        if ((canon_h + 1u != H) | (H >= P.hcap)) return false;
+        // an equivocating proposer's variant 1 goes to the SPLIT receivers (SPEC.md §5, handle_preprepare_p);
+        // one draw, every lane the same: held in SGPRs
+        uint64_t v1m = 0;
+        if (fj & F_PP_EQ) {
+            const uint64_t d = split_mask(H);
+            v1m = ((uint64_t)uni((uint32_t)d) | ((uint64_t)uni((uint32_t)(d >> 32)) << 32)) & ~(1ull << j);
+        }
+        // PC2: a validator commits iff the Byzantine wildcards and the honest Commits of its own variant
+        // exceed Q; exactly one variant may commit (both: a fork, neither: round changes — the phase loop)
+        const uint64_t hon = ~byz_mask;
+        const bool k0 = popc(byz_mask | (hon & ~v1m)) > Q, k1 = popc(byz_mask | (hon & v1m)) > Q;
+        if (k0 == k1) return false;
+        const bool var = ((v1m >> me) & 1ull) != 0;
+        const uint64_t b = blk_make(H, j, var ? 1u : 0u, pp_T_out);
+        const uint32_t d32 = blk_d32(b);
+        uint32_t* c1 = cache_p(2);                                 // Prepare {h, d32}
+        uint32_t* c2 = cache_p(4);                                 // Commit {h, d32}
+        const bool hit1 = (c1[64] == d32) & (c1[0] == H), hit2 = (c2[64] == d32) & (c2[0] == H);   // d32 != 0
+        const bool ok = (h == H) & (st() == ST_ACCEPT_REQUEST) & ((fl & (L_LOCK | L_DEAD | L_PROP)) == L_PROP) &
+                        (last + 1u == H) & (miner_event() == 0u) & (nxf == (me == j ? fj : 0u)) &
+                        (!SEEDED | (prop_l == j)) & !hit1 & !hit2;
+        if (ballot(!ok) != 0) return false;
+        const bool fires = var == k1;
+        pp = b;
+        prep = ~0ull;                                            // every validator's Prepare
+        comm = byz_mask | (hon & (var ? v1m : ~v1m));           // early Byzantine (PP) + matching honest (PC1)
+        fl = (fl & ~L_ST) | (fires ? (ST_COMMITTED | L_CMT) : ST_PREPARED) | L_LOCK;
+        c1[0] = H; c1[64] = d32;
+        c2[0] = H; c2[64] = d32;
+        last = fires ? H : last;                                 // insert_block, Blocks [H, H] out
+        last_T = fires ? (int32_t)pp_T_out : last_T;
+        nx_blo = fires ? H : nx_blo;
+        nx_bhi = fires ? H : nx_bhi;
+        miner_queue = (fires & (H > miner_queue)) ? H : miner_queue;
+        nxf = fires ? (uint32_t)F_BLK : 0u;
+        return true;
+    }
+
     // ------------------------------------------------------------------ hand-over to the full kernel
     // the full kernel's save layout (bft_wave.h BFT_STATE_32 / BFT_STATE_64, then prep, comm, the 12
     // cache words, the bool bits, tick, phase); every implied field is expanded here
@@ -674,6 +734,7 @@ struct Fast64 {
         st_t = wv.clock();
 #endif
         if (P.byz_count > 0) init_byzantine();
+        macro_ok = !LOSSY && ballot(has(L_RUN)) == ~0ull && popc(byz_mask) <= Q;
         uint32_t* lat = (uint32_t*)(lds + F64Layout::LAT_OFF);
         for (uint32_t b = me; b < 65u; b += 64u) lat[b] = 0;
         wv.sync();
@@ -699,56 +760,67 @@ struct Fast64 {
                     nxf = 0;
                     break;
                 }
-                // what is in flight, by kind (segment = wave). The classification is branch-free: every
-                // kind's first sender is read whether or not the kind is present, so no per-path values
-                // are merged at control-flow joins (those merges cost a copy of every live value).
-                const uint32_t f = nxf;
-                const bool pr = (f & F_PR) != 0, cm = (f & F_CM) != 0;
-                const uint64_t kpp = ballot((f & F_PP) != 0), kpr = ballot(pr), kcm = ballot(cm);
-                const uint64_t kblk = ballot((f & F_BLK) != 0);
-                const uint64_t kcold = ballot((f & (F_OCM | F_RC | F_SYNC)) != 0);
-                // the only Preprepare sender of the FAST kernel is the round-0 proposer (send_preprepare_cand_p):
-                // validator 0 with big-endian seeds (kpp is 0 or 1); with SEEDED the proposer of the senders'
-                // height, and two senders (validators at different heights) take the general path
-                const uint32_t j = SEEDED ? ff1(kpp) : 0u, jp = ff1(kpr), jc = ff1(kcm), jb = ff1(kblk);
-                const uint64_t cls = pp & BLK_HP_MASK;
+                // the Preprepare in flight: its sender j (the round-0 proposer: validator 0 with big-endian
+                // seeds; with SEEDED the first sender, two senders take the general path), its flags and
+                // height; the SPLIT draw once per phase for an equivocating sender (SPEC.md §5)
+                const uint64_t kpp = ballot((nxf & F_PP) != 0);
+                const uint32_t j = SEEDED ? ff1(kpp) : 0u;
+                const uint32_t fj = uni(rl(nxf, j)), pp_h = uni(rl(h, j));
+                const uint32_t pp_eq = kpp ? (fj & F_PP_EQ) : 0u;
+                // the round-0 proposer's Preprepare alone in flight, every validator waiting for it: the
+                // height's PP and two Prepare/Commit phases at once (canonical_step)
+                const bool canon = !LOSSY && macro_ok && (p + 3u < P.phase_cap) && (kpp == (1ull << j)) &&
+                                   ((fj & ~(uint32_t)F_PP_EQ) == F_PP) && canonical_step(j, fj, pp_h);
+                uint32_t path = P_CANON, blo = 0, bhi = 0;
+                uint64_t kpr = 0, kcm = 0, kblk = 0;
                 PC c;
-                c.kpr = kpr; c.kcm = kcm;
-                const uint32_t hp = uni(rl(h, jp)), hc = uni(rl(h, jc));
-                c.pr_h = kpr ? hp : 0u;
-                c.cm_h = kcm ? hc : 0u;
-                c.pr_cls = rl64(cls, jp);
-                c.cm_cls = rl64(cls, jc);
-                c.v1 = ballot(blk_var(pp) != 0);
-                const uint32_t pp_h = uni(rl(h, j));
-                const uint32_t pp_T = pp_T_out;
-                const uint32_t pp_eq = uni(rl(f & F_PP_EQ, j));
-                const uint32_t blo = uni(rl(nx_blo, jb)), bhi = uni(rl(nx_bhi, jb));
-                uint32_t path;
-                if (kcold | (SEEDED ? (kpp & (kpp - 1ull)) : 0ull)) path = P_GENERAL;
-                else if (kpp) path = (kpr | kcm | kblk) == 0 ? P_PP : P_GENERAL;
-                else if (kpr | kcm) path = kblk ? P_GENERAL : P_PC;
-                else path = kblk ? P_BLK : P_NONE;
-                // a PC phase needs one view and digest class per kind, a BLK phase one block range
-                // (integer form: a nonzero XOR marks a mismatch, one compare per lane)
-                const uint32_t cls_lo = (uint32_t)cls, cls_hi = (uint32_t)(cls >> 32);
-                const uint32_t bad_pr = (h ^ c.pr_h) | (cls_lo ^ (uint32_t)c.pr_cls) | (cls_hi ^ (uint32_t)(c.pr_cls >> 32));
-                const uint32_t bad_cm = (h ^ c.cm_h) | (cls_lo ^ (uint32_t)c.cm_cls) | (cls_hi ^ (uint32_t)(c.cm_cls >> 32));
-                const uint32_t bad_pc = (pr ? bad_pr : 0u) | (cm ? bad_cm : 0u);
-                const uint32_t bad_blk = (f & F_BLK) ? ((nx_blo ^ blo) | (nx_bhi ^ bhi)) : 0u;
-                const uint32_t bad = path == P_PC ? bad_pc : (path == P_BLK ? bad_blk : 0u);
-                if (ballot(bad != 0) != 0) path = P_GENERAL;
-                if (path == P_GENERAL) {                          // hand the instance to the full kernel
-                    save_state(p);
-                    if (me == 0) P.resume_flags[inst_local] = 1u;
-                    bailed = true;
-                    seg_done = true;
-                    break;
+                if (!canon) {
+                    // what is in flight, by kind (segment = wave). The classification is branch-free: every
+                    // kind's first sender is read whether or not the kind is present, so no per-path values
+                    // are merged at control-flow joins (those merges cost a copy of every live value).
+                    const uint32_t f = nxf;
+                    const bool pr = (f & F_PR) != 0, cm = (f & F_CM) != 0;
+                    kpr = ballot(pr); kcm = ballot(cm);
+                    kblk = ballot((f & F_BLK) != 0);
+                    const uint64_t kcold = ballot((f & (F_OCM | F_RC | F_SYNC)) != 0);
+                    const uint32_t jp = ff1(kpr), jc = ff1(kcm), jb = ff1(kblk);
+                    const uint64_t cls = pp & BLK_HP_MASK;
+                    c.kpr = kpr; c.kcm = kcm;
+                    const uint32_t hp = uni(rl(h, jp)), hc = uni(rl(h, jc));
+                    c.pr_h = kpr ? hp : 0u;
+                    c.cm_h = kcm ? hc : 0u;
+                    c.pr_cls = rl64(cls, jp);
+                    c.cm_cls = rl64(cls, jc);
+                    c.v1 = ballot(blk_var(pp) != 0);
+                    blo = uni(rl(nx_blo, jb)); bhi = uni(rl(nx_bhi, jb));
+                    if (kcold | (SEEDED ? (kpp & (kpp - 1ull)) : 0ull)) path = P_GENERAL;
+                    else if (kpp) path = (kpr | kcm | kblk) == 0 ? P_PP : P_GENERAL;
+                    else if (kpr | kcm) path = kblk ? P_GENERAL : P_PC;
+                    else path = kblk ? P_BLK : P_NONE;
+                    // a PC phase needs one view and digest class per kind, a BLK phase one block range
+                    // (integer form: a nonzero XOR marks a mismatch, one compare per lane)
+                    const uint32_t cls_lo = (uint32_t)cls, cls_hi = (uint32_t)(cls >> 32);
+                    const uint32_t bad_pr = (h ^ c.pr_h) | (cls_lo ^ (uint32_t)c.pr_cls) | (cls_hi ^ (uint32_t)(c.pr_cls >> 32));
+                    const uint32_t bad_cm = (h ^ c.cm_h) | (cls_lo ^ (uint32_t)c.cm_cls) | (cls_hi ^ (uint32_t)(c.cm_cls >> 32));
+                    const uint32_t bad_pc = (pr ? bad_pr : 0u) | (cm ? bad_cm : 0u);
+                    const uint32_t bad_blk = (f & F_BLK) ? ((nx_blo ^ blo) | (nx_bhi ^ bhi)) : 0u;
+                    const uint32_t bad = path == P_PC ? bad_pc : (path == P_BLK ? bad_blk : 0u);
+                    if (ballot(bad != 0) != 0) path = P_GENERAL;
+                    if (path == P_GENERAL) {                          // hand the instance to the full kernel
+                        save_state(p);
+                        if (me == 0) P.resume_flags[inst_local] = 1u;
+                        bailed = true;
+                        seg_done = true;
+                        break;
+                    }
                 }
-                nxf = 0;
                 F64_STAMP(1);
                 F64_COUNT(8);
-                if (act) {
+                if (canon) {                                       // PP, PC1, PC2 of the canonical height, applied
+                    p += 2u;
+                    F64_COUNT(8); F64_COUNT(8); F64_COUNT(9); F64_COUNT(10); F64_COUNT(10); F64_COUNT(12);
+                } else if (act) {
+                    nxf = 0;
                     // event step: Minner's NewHeader handler, for the validators with queued chain events
                     miner_step_p();   // a no-op for lanes without a queued event (miner_step_p guards the mining)
                     F64_STAMP(2);
@@ -763,7 +835,7 @@ struct Fast64 {
                             F64_COUNT(10);
                         } else if (path == P_PP) {
                             handle_preprepare_p(has(L_RUN) & (((mk >> j) & 1ull) != 0) & !has(L_DEAD), j, pp_h,
-                                                blk_make(pp_h, j, 0, pp_T), pp_eq != 0);
+                                                blk_make(pp_h, j, 0, pp_T_out), pp_eq ? split_mask(pp_h) : 0ull);
                             F64_STAMP(3);
                             F64_COUNT(9);
                         } else {                                  // P_BLK
@@ -782,7 +854,7 @@ struct Fast64 {
                 // validator already has xc, handle_blocks_p is ChainError::Exists for all of them
                 // (core.rs:75-82) and that phase reduces to its event step. Same phase index, same
                 // miner step: bit-identical, without a second classification per height.
-                if ((path == P_PC) & (xc != 0) & act & (p + 1 < P.phase_cap)) {
+                if (((path == P_PC) | (path == P_CANON)) & (xc != 0) & act & (p + 1 < P.phase_cap)) {
                     if (ballot(((nxf & ~F_BLK) != 0) | (has(L_RUN) & (last < xc))) == 0) {
                         ++p;
                         nxf = 0;

@@ -3,11 +3,11 @@
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 env BFTSIM_TESTING=1 BFTSIM_LIB=consensus-rs_amd/build/libbftsim_stamps.so python - <<'PY' > gpurun_out/stamps.txt 2>&1
-import ctypes, sys
+import ctypes, dataclasses, os, sys
 sys.path.insert(0, "consensus-rs_amd")
 from bftsim import runtime
 from bftsim.configs import cfg3
-sim = runtime.Simulator(cfg3())
+sim = runtime.Simulator(dataclasses.replace(cfg3(), byz_count=int(os.environ.get('BYZ', '21'))))
 sim.prepare(16384)
 for _ in range(2):
     sim.launch(0)
