@@ -45,8 +45,11 @@ hipError_t launch_fast(dim3 grid, hipStream_t s, const Params& p) {
 // Keccak state word, the odd lane the high half. A 64-bit rotation is one v_alignbit_b32 of this
 // lane's half and the partner's (exchanged with one DPP quad_perm swap); theta parities, chi and iota
 // are half-local. Per lane and round ~125 VALU instead of ~205 for a whole state in one lane, and
-// twice the waves for the chip (the chains are sequential in height, so per-chain issue latency,
-// not throughput, bounds this kernel).
+// twice the waves for the chip. The chains are sequential in height and a lone wave issues one VALU
+// per ~4 cycles, so the pass is bound by its per-chain issue latency: the pair halves it. (A whole
+// state per lane has ~27 % fewer vector instructions per header; it was the large-shard choice while
+// the consensus kernel took longer than its 2.25 ms latency, and lost 18 % once it did not:
+// profiles/r03/ab_hash.)
 #if defined(__HIP_DEVICE_COMPILE__)
 __device__ inline uint32_t pair_swap(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
@@ -136,42 +139,8 @@ __global__ __launch_bounds__(64) void bft_hash_pair_kernel(Params p) {
     }
 #endif
 }
-// one lane per instance, the whole Keccak state in that lane (32-bit halves): ~27 % fewer vector
-// instructions per header than the lane pair, at twice the chain latency. Used for large shards, where
-// the pass shares the GPU with the next launches' consensus kernels and instruction count is what it
-// costs them (profiles/r02/ab_s2: +1 % at 16,384 instances per GPU); small shards are bound by the
-// chain latency and keep the lane pair.
-__global__ __launch_bounds__(64) void bft_hash_lane_kernel(Params p) {
-    __shared__ __attribute__((aligned(16))) uint64_t bufs[64 * HDR_WORDS];
-    const uint32_t il = blockIdx.x * 64u + threadIdx.x;
-    if (il >= p.n_instances) return;
-    const uint32_t inst = p.first_instance + il;
-    const uint32_t ch = p.committed_height[il];
-    uint32_t prev[8];
-    for (int i = 0; i < 8; ++i)
-        prev[i] = (uint32_t)p.genesis_hash[4 * i] | ((uint32_t)p.genesis_hash[4 * i + 1] << 8) |
-                  ((uint32_t)p.genesis_hash[4 * i + 2] << 16) | ((uint32_t)p.genesis_hash[4 * i + 3] << 24);
-    uint8_t* buf = (uint8_t*)(bufs + threadIdx.x * HDR_WORDS);
-    for (uint32_t x = 1; x <= ch; ++x) {
-        const uint32_t* row = p.rec + ((uint64_t)il * p.rows + x) * 4;
-        const uint32_t w1 = row[1];
-        const uint32_t prop = w1 & 0xffffu, var = (w1 >> 16) & 1u, T = row[2];
-        const uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)T + 1ull);
-        uint32_t out[8];
-        lane_block_hash(buf, prev, p.addresses + 20u * prop, p.seed, inst, x, prop, var, time, out);
-        uint4* dst = (uint4*)(p.hash + ((uint64_t)il * p.rows + x) * 32);
-        dst[0] = make_uint4(out[0], out[1], out[2], out[3]);
-        dst[1] = make_uint4(out[4], out[5], out[6], out[7]);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) prev[i] = out[i];
-    }
-}
-constexpr uint32_t HASH_LANE_MIN_INSTANCES = 8192;
 hipError_t launch_hash(dim3 grid, hipStream_t s, const Params& p) {
-    if (p.n_instances >= HASH_LANE_MIN_INSTANCES)
-        hipLaunchKernelGGL(bft_hash_lane_kernel, dim3((p.n_instances + 63u) / 64u), dim3(64), 0, s, p);
-    else
-        hipLaunchKernelGGL(bft_hash_pair_kernel, grid, dim3(64), 0, s, p);
+    hipLaunchKernelGGL(bft_hash_pair_kernel, grid, dim3(64), 0, s, p);
     return hipGetLastError();
 }
 
