@@ -70,6 +70,8 @@ def lib():
         L.bftsim_set_fast.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.bftsim_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
         L.bftsim_set_window.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        if hasattr(L, "bftsim_set_rcs_capacity"):     # (absent from A/B builds of earlier rounds)
+            L.bftsim_set_rcs_capacity.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         L.bftsim_fetch_summary.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5
         L.bftsim_two_thirds_majority.restype = ctypes.c_uint32
         L.bftsim_seed_from_hash.restype = ctypes.c_uint32
@@ -147,6 +149,11 @@ class Simulator:
     def set_window(self, window: int):
         """Keep a ring of `window` canonical rows per instance (0: every height); see bftsim.h."""
         _check(self.h, lib().bftsim_set_window(self.h, window), "bftsim_set_window")
+
+    def set_rcs_capacity(self, rounds: int):
+        """RoundChangeSet rounds kept per validator (bftsim_set_rcs_capacity); run() re-runs an
+        overflowing batch at twice the capacity."""
+        _check(self.h, lib().bftsim_set_rcs_capacity(self.h, rounds), "bftsim_set_rcs_capacity")
 
     def fetch_summary(self, n: int, tips: bool = True):
         out = dict(committed_height=np.zeros(n, np.uint64), flags=np.zeros(n, np.uint32),

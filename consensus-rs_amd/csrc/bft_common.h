@@ -55,7 +55,7 @@ struct Params {
     uint64_t* hist;                   // [130] summed rounds-to-commit (65) + commit-latency (65) bins
     uint32_t window_mask;             // 0: rec/hash rows for every height; else ring of window_mask+1 rows
     uint32_t rows;                    // rec/hash rows per instance (hcap, or the ring size)
-    uint32_t* rcs;                    // RoundChangeSet tables: per wave / workgroup rcs_words(seg) words
+    uint32_t* rcs;                    // RoundChangeSet tables: per wave / workgroup rcs_words(seg, rcs_k) words
     uint32_t q;                       // floor(2N/3) (two_thirds_majority, validator.rs:149-154)
     uint32_t nmask;                   // N-1 when N is a power of two (x mod N = x & nmask), else 0
     // FAST launches (bft_wave.h): instances that need the general path are saved and resumed
@@ -76,7 +76,13 @@ struct Params {
     uint64_t forged[4];               // validators signing with a key that is not theirs
     uint32_t* vsnap;                  // [n_inst][seg][8] each lane's commit set at its last Core commit
     uint32_t* votes;                  // [n_inst][rows][8] the canonical committer's commit set per height
+    // block-hash pass (kern_fast.hip): header suffix rows of heights [sfx_x0, sfx_x0 + sfx_rows)
+    uint32_t* sfx;                    // [n_inst][sfx_rows][SFX_DWORDS]
+    uint32_t sfx_x0, sfx_rows;
+    uint32_t rcs_k;                   // RoundChangeSet rounds per validator (bftsim_set_rcs_capacity)
+    uint32_t pad5;
 };
+constexpr uint32_t RCS_DEFAULT_K = 16, RCS_MAX_K = 4096;
 // one logged broadcast: {tick, phase | code << 8 | sender << 16, height, round, block id lo, hi,
 // flags (MLOG_*), 0}; code = MessageType 1..4 (Preprepare .. RoundChange)
 constexpr uint32_t MLOG_WORDS = 8;
@@ -497,16 +503,27 @@ constexpr uint32_t HDR_WORDS = LANE_HASH_BUF / 8;
 // host_header_bytes() (bft_host.h), which the tests compare against the msgpack package.
 struct HdrWriter {
     uint64_t* wb;        // HDR_WORDS words, 8-aligned
+    uint32_t* sb;        // or: dword k of the stream at sb[k * stride] (the block-hash pass's suffix rows)
+    uint32_t stride;
     uint64_t acc;
     uint32_t fill;       // bytes in acc, 0..7
     uint32_t wi;         // next word index
-    BFT_FN explicit HdrWriter(uint64_t* w) : wb(w), acc(0), fill(0), wi(0) {}
+    BFT_FN explicit HdrWriter(uint64_t* w) : wb(w), sb(nullptr), stride(0), acc(0), fill(0), wi(0) {}
+    BFT_FN HdrWriter(uint32_t* s, uint32_t st) : wb(nullptr), sb(s), stride(st), acc(0), fill(0), wi(0) {}
+    BFT_FN void store(uint32_t i, uint64_t v) {
+        if (stride) {
+            sb[(uint64_t)(2u * i) * stride] = (uint32_t)v;
+            sb[(uint64_t)(2u * i + 1u) * stride] = (uint32_t)(v >> 32);
+        } else {
+            wb[i] = v;
+        }
+    }
     BFT_FN void put(uint64_t v, uint32_t n) {            // 1 <= n <= 8, v < 2^(8n)
         const uint32_t sh = 8u * fill;
         const uint64_t lo = acc | (v << sh);
         const uint32_t nf = fill + n;
         if (nf >= 8u) {
-            wb[wi++] = lo;
+            store(wi++, lo);
             acc = sh ? (v >> (64u - sh)) : 0ull;
             fill = nf - 8u;
         } else {
@@ -574,12 +591,15 @@ struct HdrWriter {
 };
 
 // The fields of the header of block (x, prop, var) with parent hash `prev` (8 LE words) at `time`.
-// Field order = Header declaration order (types/block.rs:16-36).
-BFT_FN void header_fields(HdrWriter& w, const uint32_t prev[8], const uint8_t* addr20, uint64_t seed,
-                          uint32_t inst, uint32_t h, uint32_t prop, uint32_t var, uint64_t time) {
+// Field order = Header declaration order (types/block.rs:16-36). Only prev_hash chains from height to
+// height: header_prefix is that field (with the array header), header_suffix_fields everything after it.
+BFT_FN void header_prefix_fields(HdrWriter& w, const uint32_t prev[8]) {
     w.put(0x2000dc9dull, 4);                           // array(13); prev_hash: array16(32)
 #pragma unroll
     for (int i = 0; i < 8; ++i) w.put_hash_word(prev[i]);
+}
+BFT_FN void header_suffix_fields(HdrWriter& w, const uint8_t* addr20, uint64_t seed, uint32_t inst, uint32_t h,
+                                 uint32_t prop, uint32_t var, uint64_t time) {
     w.put_address(addr20);                             // proposer
     w.put(0x2000dcull, 3);                             // root = EMPTY_HASH
     for (int i = 0; i < 4; ++i) w.put(0, 8);
@@ -596,6 +616,68 @@ BFT_FN void header_fields(HdrWriter& w, const uint32_t prev[8], const uint8_t* a
     w.put_uint(time);
     w.put(0x2065736e696f439bull, 8);                   // extra = "Coinse base" (minner/mod.rs:113)
     w.put(0xc065736162ull, 5);                         //   ... + votes: None
+}
+BFT_FN void header_fields(HdrWriter& w, const uint32_t prev[8], const uint8_t* addr20, uint64_t seed,
+                          uint32_t inst, uint32_t h, uint32_t prop, uint32_t var, uint64_t time) {
+    header_prefix_fields(w, prev);
+    header_suffix_fields(w, addr20, seed, inst, h, prop, var, time);
+}
+
+// ---- the header spliced from its two parts (the block-hash pass of kern_fast.hip) ----
+// Suffix row, per (instance, height), written by a pass over every height at once: the suffix bytes
+// (at most 212: address 44, root 35, tx_hash ≤ 67, receipt 35, height ≤ 5, time ≤ 9, the rest 21),
+// then the Keccak domain byte 0x01, zero-filled; dword SFX_LEN_DW holds the suffix length. Host rows
+// (header_suffix) are SFX_DWORDS contiguous dwords; on the device the rows are dword-major across the
+// launch's instances (header_suffix_strided), so that the writes and the chains' reads coalesce.
+constexpr uint32_t SFX_DWORDS = 64, SFX_BODY_DW = 60, SFX_LEN_DW = 63, SFX_DEV_LEN_DW = 60, SFX_DEV_DW = 61;
+// Splice buffer (dwords): SFX_PAD zero dwords, the suffix body, zeros up to the last dword a 3-block
+// message reads. The prefix is 36..68 bytes, so a message dword w is read at byte 4w - len_p + 72.
+constexpr uint32_t SFX_PAD = 18, SFX_BUF = 112, PFX_WORDS = 9;
+BFT_FN uint32_t header_suffix(uint64_t* wb, const uint8_t* addr20, uint64_t seed, uint32_t inst, uint32_t h,
+                              uint32_t prop, uint32_t var, uint64_t time) {   // wb: SFX_DWORDS / 2 words
+    HdrWriter w(wb);
+    header_suffix_fields(w, addr20, seed, inst, h, prop, var, time);
+    const uint32_t len = 8u * w.wi + w.fill;
+    wb[w.wi++] = w.acc | (0x01ull << (8u * w.fill));
+    while (w.wi < SFX_DWORDS / 2u - 1u) wb[w.wi++] = 0;
+    wb[SFX_DWORDS / 2u - 1u] = (uint64_t)len << 32;    // dword SFX_LEN_DW
+    return len;
+}
+// the device layout: dword k of the row at sb[k * stride] (stride = the launch's instance count)
+BFT_FN uint32_t header_suffix_strided(uint32_t* sb, uint32_t stride, const uint8_t* addr20, uint64_t seed,
+                                      uint32_t inst, uint32_t h, uint32_t prop, uint32_t var, uint64_t time) {
+    HdrWriter w(sb, stride);
+    header_suffix_fields(w, addr20, seed, inst, h, prop, var, time);
+    const uint32_t len = 8u * w.wi + w.fill;
+    w.store(w.wi++, w.acc | (0x01ull << (8u * w.fill)));
+    while (w.wi < SFX_BODY_DW / 2u) w.store(w.wi++, 0);
+    sb[(uint64_t)SFX_DEV_LEN_DW * stride] = len;
+    return len;
+}
+BFT_FN uint32_t header_prefix(uint64_t* wb, const uint32_t prev[8]) {     // wb: PFX_WORDS words
+    HdrWriter w(wb);
+    header_prefix_fields(w, prev);
+    const uint32_t len = 8u * w.wi + w.fill;
+    wb[w.wi++] = w.acc;
+    while (w.wi < PFX_WORDS) wb[w.wi++] = 0;
+    return len;
+}
+BFT_FN uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32_t r) {      // ({hi, lo} >> 8r)[31:0], r < 4
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbyte(hi, lo, r);
+#else
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * r));
+#endif
+}
+// rate blocks of a spliced header: ceil((len_p + len_s + 1) / 136)
+BFT_FN uint32_t splice_blocks(uint32_t len_p, uint32_t len_s) { return (len_p + len_s + 136u) / 136u; }
+// message dword w of the padded header: `sx` = splice buffer + ((72 - len_p) >> 2), r = (72 - len_p) & 3,
+// `pw` = the prefix as dwords (zero past len_p); nb rate blocks (the final 0x80 at dword 34 nb - 1)
+BFT_FN uint32_t splice_word(const uint32_t* sx, uint32_t r, const uint32_t* pw, uint32_t w, uint32_t nb) {
+    uint32_t v = align_bytes(sx[w + 1u], sx[w], r);
+    if (w < 2u * PFX_WORDS) v |= pw[w];
+    if (w == 34u * nb - 1u) v ^= 0x80000000u;
+    return v;
 }
 // the header into wb, padded for Keccak; returns the number of rate blocks (2 or 3)
 BFT_FN uint32_t header_words(uint64_t* wb, const uint32_t prev[8], const uint8_t* addr20, uint64_t seed,
@@ -634,6 +716,30 @@ BFT_FN void lane_block_hash(uint8_t* buf, const uint32_t prev[8], const uint8_t*
 #pragma unroll
     for (int i = 0; i < 4; ++i) { out[2 * i] = (uint32_t)a[i]; out[2 * i + 1] = (uint32_t)(a[i] >> 32); }
 }
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+// The same hash through the two-kernel block-hash pass's splice (host: the CPU emulator's post-pass).
+// sfx: the height's suffix row (SFX_DWORDS dwords, header_suffix).
+inline void spliced_block_hash(const uint32_t* sfx, const uint32_t prev[8], uint32_t out[8]) {
+    uint32_t buf[SFX_BUF] = {};
+    for (uint32_t i = 0; i < SFX_BODY_DW; ++i) buf[SFX_PAD + i] = sfx[i];
+    uint64_t pfx[PFX_WORDS];
+    const uint32_t lp = header_prefix(pfx, prev);
+    uint32_t pw[2 * PFX_WORDS];
+    for (uint32_t i = 0; i < PFX_WORDS; ++i) { pw[2 * i] = (uint32_t)pfx[i]; pw[2 * i + 1] = (uint32_t)(pfx[i] >> 32); }
+    const uint32_t c = 72u - lp, nb = splice_blocks(lp, sfx[SFX_LEN_DW]);
+    const uint32_t* sx = buf + (c >> 2);
+    uint64_t a[25] = {};
+    for (uint32_t blk = 0; blk < nb; ++blk) {
+        for (uint32_t i = 0; i < 17; ++i) {
+            const uint32_t w = 34u * blk + 2u * i;
+            a[i] ^= (uint64_t)splice_word(sx, c & 3u, pw, w, nb) | ((uint64_t)splice_word(sx, c & 3u, pw, w + 1u, nb) << 32);
+        }
+        keccak_f1600(a);
+    }
+    for (int i = 0; i < 4; ++i) { out[2 * i] = (uint32_t)a[i]; out[2 * i + 1] = (uint32_t)(a[i] >> 32); }
+}
+#endif
 
 // randon_seed (validator.rs:39-48): U128::from(hash[0..8] ++ 0^8) mod n. `le` selects how the
 // 16-byte buffer is read (bftsim.h BFTSIM_SEED_*): big-endian (BE64(hash[0..8]) * 2^64) mod n, or

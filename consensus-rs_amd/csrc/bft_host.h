@@ -92,6 +92,7 @@ inline Params params_from_config(const bftsim_config& c, uint32_t seg, uint32_t 
     p.fast = p.backlog_replay ? 0u : 1u;             // replay mode: one message at a time (SPEC.md §10)
     p.q = (2u * c.n) / 3u;
     p.nmask = (c.n & (c.n - 1)) == 0 ? c.n - 1 : 0;
+    p.rcs_k = RCS_DEFAULT_K;
     return p;
 }
 

@@ -74,14 +74,13 @@ template <uint32_t S>
 struct Layout {
     static constexpr uint32_t L = S > 64 ? S : 64;
     static constexpr int NW = S > 64 ? (int)(S / 64) : 1;
-    static constexpr int K = 16;                      // RoundChangeSet rounds kept per validator
     static constexpr uint32_t CMT_STRIDE = 8;          // words per lane of the commit hand-off
     static constexpr uint32_t REC_OFF = 0;
     static constexpr uint32_t RC_OFF = REC_OFF + L * (uint32_t)REC_WORDS * 4;
     static constexpr uint32_t CMT_OFF = REC_OFF;
     static constexpr uint32_t CACHE_OFF = RC_OFF;
     static constexpr uint32_t HIST_OFF = CACHE_OFF + 12u * L * 4u;
-    static constexpr uint32_t RCS_WORDS = (uint32_t)K * (1u + 2u * NW) * L;    // global, per wave
+    static constexpr uint32_t RCS_WORDS_PER_ROUND = (1u + 2u * NW) * L;   // global, per wave and round
     static constexpr uint32_t BL_WORDS = S * 5u * L;  // replay mode: backlog slots, global, per wave
     static constexpr uint32_t SEG_OFF = HIST_OFF + 528;
     static_assert(L * CMT_STRIDE <= L * REC_WORDS, "commit hand-off must fit in the record area");
@@ -96,8 +95,11 @@ struct Layout {
     static constexpr uint32_t BYTES_SEED = S > 64 ? SCR_OFF : SCR_OFF + 64 * LANE_HASH_BUF;
     static constexpr uint32_t bytes(bool need_seed) { return need_seed ? BYTES_SEED : BYTES_POW2; }
 };
-BFT_FN uint32_t rcs_words(uint32_t seg) {
-    return seg == 256 ? Layout<256>::RCS_WORDS : seg == 128 ? Layout<128>::RCS_WORDS : Layout<64>::RCS_WORDS;
+// RoundChangeSet table words per wave / workgroup for k rounds per validator (a runtime capacity:
+// bftsim_set_rcs_capacity; bftsim_run re-runs an overflowing batch at a larger one)
+BFT_FN uint64_t rcs_words(uint32_t seg, uint32_t k) {
+    return (uint64_t)k * (seg == 256 ? Layout<256>::RCS_WORDS_PER_ROUND : seg == 128 ? Layout<128>::RCS_WORDS_PER_ROUND
+                                                                         : Layout<64>::RCS_WORDS_PER_ROUND);
 }
 BFT_FN uint32_t backlog_words(uint32_t seg) {      // per wave (S <= 64) or workgroup
     return seg == 256 ? Layout<256>::BL_WORDS : seg == 128 ? Layout<128>::BL_WORDS : seg == 64 ? Layout<64>::BL_WORDS
@@ -132,7 +134,6 @@ struct Sim {
     static_assert(MODE != MODE_RESUME || S == 64, "hand-over modes are for one instance per wave");
     using LY = Layout<S>;
     static constexpr int NW = LY::NW;
-    static constexpr int RCS_K = LY::K;
     static constexpr uint32_t LDS_REC_OFF = LY::REC_OFF, LDS_RC_OFF = LY::RC_OFF, LDS_CMT_OFF = LY::CMT_OFF,
                               LDS_HIST_OFF = LY::HIST_OFF, LDS_CACHE_OFF = LY::CACHE_OFF,
                               LDS_SEG_OFF = LY::SEG_OFF, LDS_CHASH_OFF = LY::CHASH_OFF, LDS_SCR_OFF = LY::SCR_OFF;
@@ -176,6 +177,7 @@ struct Sim {
     bool hash_defer, in_pc;
     uint32_t lane_flags;
     uint32_t* rcs_base;      // this wave's RoundChangeSet table (global)
+    uint32_t rcs_k;          // its capacity in rounds (Params::rcs_k)
     uint32_t* bl_base;       // this wave's backlog slots (global, replay mode)
     uint32_t mlog_cnt;       // real-crypto mode: messages logged so far by this instance (segment-uniform)
 #ifdef BFT_STAMPS
@@ -224,7 +226,8 @@ struct Sim {
         mlog_cnt = 0;
         lane_flags = 0;
         off_inst = offset_inst_part(p.seed, inst);
-        rcs_base = p.rcs + (uint64_t)wave_global * LY::RCS_WORDS;
+        rcs_k = p.rcs_k;
+        rcs_base = p.rcs + (uint64_t)wave_global * rcs_k * LY::RCS_WORDS_PER_ROUND;
         bl_base = p.backlog ? p.backlog + (uint64_t)wave_global * LY::BL_WORDS : nullptr;
         off_tick = 0;
     }
@@ -584,7 +587,7 @@ struct Sim {
     // RoundChangeSet table (global, lane-private), SoA [k][lane]: coalesced per wave
     BFT_FN uint32_t* rc_round_p(uint32_t k) const { return rcs_base + k * LY::L + lane; }
     BFT_FN uint32_t* rc_word_p(uint32_t k, uint32_t j) const {
-        return rcs_base + (RCS_K + k * 2u * NW + j) * LY::L + lane;
+        return rcs_base + (rcs_k + k * 2u * NW + j) * LY::L + lane;
     }
     BFT_FN M rc_set_at(uint32_t k) const {
         M m;
@@ -611,7 +614,7 @@ struct Sim {
         uint32_t pos = 0;
         while (pos < n_rcs && *rc_round_p(pos) < round) ++pos;
         if (pos == n_rcs || *rc_round_p(pos) != round) {
-            if (n_rcs == (uint32_t)RCS_K) { lane_flags |= FLAG_RCS_OVERFLOW; return -1; }
+            if (n_rcs == rcs_k) { lane_flags |= FLAG_RCS_OVERFLOW; return -1; }
             for (uint32_t i = n_rcs; i > pos; --i) {
                 *rc_round_p(i) = *rc_round_p(i - 1);
                 for (uint32_t j = 0; j < 2u * NW; ++j) *rc_word_p(i, j) = *rc_word_p(i - 1, j);

@@ -384,6 +384,7 @@ struct bftsim {
     uint32_t* d_save = nullptr;       // FAST launches: [SAVE_WORDS][cap_inst * 64] saved lane state
     int fast = 1;                     // FAST kernel + resume for N = 64 (bftsim_set_fast(h, 0): full kernel)
     uint32_t window = 0;              // 0: full per-height rows; else ring of `window` rows
+    uint32_t rcs_k = bft::RCS_DEFAULT_K;   // RoundChangeSet rounds per validator (bftsim_set_rcs_capacity)
     uint64_t* d_trace = nullptr;
     uint64_t* h_trace = nullptr;
     uint32_t trace_ticks = 0;
@@ -397,16 +398,18 @@ struct bftsim {
     struct RowSet {
         uint32_t* ch = nullptr; uint32_t* flags = nullptr; uint32_t* ticks = nullptr; uint64_t* views = nullptr;
         uint32_t* rec = nullptr; uint8_t* hash = nullptr;
+        uint32_t* sfx = nullptr;      // header suffix rows of the hash pass (sfx_rows per instance)
         hipStream_t hs = nullptr;     // the set's hash stream
         hipEvent_t done = nullptr;    // hash pass of the last launch that used the set
         bool busy = false;
     } sets[MAX_SETS];
     int pipeline = 0;                 // number of row-table sets (0: no pipelining)
+    uint32_t sfx_rows = 0;            // heights per hash-pass chunk (0: no hash pass)
     uint32_t n_sets = 0, cur_set = 0;
     hipStream_t hs = nullptr;         // the hash stream of the last pipelined launch
     // per-launch kernel timing: a ring of event quadruples, read by bftsim_kernel_ms_sum
     static constexpr uint32_t RING = 64;
-    struct LaunchEv { hipEvent_t c0, c1, h0, h1; bool has_hash, pending; } ring[RING] = {};
+    struct LaunchEv { hipEvent_t c0, c1, h0, h1, sx; bool has_hash, pending; } ring[RING] = {};
     uint32_t ring_head = 0;
     double acc_c = 0, acc_h = 0;
     uint32_t acc_n = 0;
@@ -432,8 +435,8 @@ static void free_bufs(bftsim* h) {
     for (uint32_t k = 0; k < h->n_sets; ++k) {
         bftsim::RowSet& r = h->sets[k];
         (void)hipFree(r.ch); (void)hipFree(r.flags); (void)hipFree(r.ticks); (void)hipFree(r.views);
-        (void)hipFree(r.rec); (void)hipFree(r.hash);
-        r.ch = r.flags = r.ticks = nullptr; r.views = nullptr; r.rec = nullptr; r.hash = nullptr;
+        (void)hipFree(r.rec); (void)hipFree(r.hash); (void)hipFree(r.sfx);
+        r.ch = r.flags = r.ticks = nullptr; r.views = nullptr; r.rec = nullptr; r.hash = nullptr; r.sfx = nullptr;
     }
     (void)hipFree(h->d_trace); (void)hipFree(h->d_tips); (void)hipFree(h->d_rcs);
     h->d_rcs = nullptr;
@@ -630,6 +633,7 @@ int bftsim_create(const bftsim_config* cfg, int hip_device, bftsim_t** out) {
     for (uint32_t i = 0; i < bftsim::RING; ++i) {
         HIPCHECK(h, hipEventCreate(&h->ring[i].c0)); HIPCHECK(h, hipEventCreate(&h->ring[i].c1));
         HIPCHECK(h, hipEventCreate(&h->ring[i].h0)); HIPCHECK(h, hipEventCreate(&h->ring[i].h1));
+        HIPCHECK(h, hipEventCreateWithFlags(&h->ring[i].sx, hipEventDisableTiming));
     }
     for (uint32_t i = 0; i < bftsim::MAX_SETS; ++i)
         HIPCHECK(h, hipEventCreateWithFlags(&h->sets[i].done, hipEventDisableTiming));
@@ -650,6 +654,7 @@ void bftsim_destroy(bftsim_t* h) {
         if (h->ring[i].c1) (void)hipEventDestroy(h->ring[i].c1);
         if (h->ring[i].h0) (void)hipEventDestroy(h->ring[i].h0);
         if (h->ring[i].h1) (void)hipEventDestroy(h->ring[i].h1);
+        if (h->ring[i].sx) (void)hipEventDestroy(h->ring[i].sx);
     }
     for (uint32_t i = 0; i < bftsim::MAX_SETS; ++i) {
         if (h->sets[i].done) (void)hipEventDestroy(h->sets[i].done);
@@ -657,6 +662,11 @@ void bftsim_destroy(bftsim_t* h) {
     }
     delete h;
 }
+
+static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n);
+#ifndef BFT_SFX_ON_LAUNCH_STREAM
+#define BFT_SFX_ON_LAUNCH_STREAM 1    // A/B switch (scripts/gpu_r03k.sh)
+#endif
 
 int bftsim_prepare(bftsim_t* h, uint64_t n) {
     if (!h || n == 0 || n > (1ull << 31)) return fail(h, BFTSIM_EINVAL, "bad instance count");
@@ -674,7 +684,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
     {
         uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg;
         uint64_t blocks = (n + per_block - 1) / per_block;
-        HIPCHECK(h, hipMalloc(&h->d_rcs, blocks * bft::rcs_words(h->seg) * 4));
+        HIPCHECK(h, hipMalloc(&h->d_rcs, blocks * bft::rcs_words(h->seg, h->rcs_k) * 4));
         if (h->crypto) {
             HIPCHECK(h, hipMalloc(&h->d_mlog, n * (uint64_t)h->mlog_cap * bft::MLOG_WORDS * 4));
             HIPCHECK(h, hipMalloc(&h->d_mlog_n, n * 4));
@@ -703,6 +713,18 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         HIPCHECK(h, hipMalloc(&r.hash, n * h->hcap * 32));
         h->n_sets = k + 1;
     }
+    // the hash pass's suffix rows (runs without in-kernel hashes): every height in one chunk up to 2 GiB
+    // per set, fewer heights per chunk beyond
+    h->sfx_rows = 0;
+    if (!make_params(h, 0, 1).need_seed) {
+        const uint64_t per_row = n * bft::SFX_DEV_DW * 4ull;
+        uint64_t rows = (2ull << 30) / per_row;
+        if (rows < 1) rows = 1;
+        if (rows > h->cfg.heights) rows = h->cfg.heights;
+        if (rows * n >= (1ull << 32)) rows = ((1ull << 32) - 1) / n;
+        h->sfx_rows = (uint32_t)rows;
+        for (uint32_t k = 0; k < h->n_sets; ++k) HIPCHECK(h, hipMalloc(&h->sets[k].sfx, rows * per_row));
+    }
     h->cap_inst = n;
     h->n_req = n;
     return BFTSIM_OK;
@@ -717,6 +739,17 @@ int bftsim_set_window(bftsim_t* h, uint32_t window) {
     h->hcap = window ? window : h->cfg.heights + 64;
     (void)hipSetDevice(h->device);
     free_bufs(h);                                   // row tables are re-sized by the next prepare
+    return BFTSIM_OK;
+}
+
+int bftsim_set_rcs_capacity(bftsim_t* h, uint32_t rounds) {
+    if (!h) return BFTSIM_EINVAL;
+    if (rounds < 1 || rounds > bft::RCS_MAX_K) return fail(h, BFTSIM_EINVAL, "RoundChangeSet capacity must be 1..4096");
+    if (rounds == h->rcs_k) return BFTSIM_OK;
+    if (h->last_stream || h->hs) if (int rc = sync_all(h)) return rc;
+    h->rcs_k = rounds;
+    (void)hipSetDevice(h->device);
+    free_bufs(h);                                   // the tables are re-sized by the next prepare
     return BFTSIM_OK;
 }
 
@@ -747,6 +780,7 @@ static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
     p.trace_ticks = h->trace_ticks;
     p.hist = h->d_hist;
     p.rcs = h->d_rcs;
+    p.rcs_k = h->rcs_k;
     p.backlog = h->d_backlog;
     if (h->crypto && h->d_mlog) {
         p.mlog = h->d_mlog;
@@ -845,9 +879,25 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     ev.pending = true;
     if (!p.need_seed) {
         hipStream_t t = pipe ? h->sets[h->cur_set].hs : s;
-        if (pipe) HIPCHECK(h, hipStreamWaitEvent(t, ev.c1, 0));
-        HIPCHECK(h, hipEventRecord(ev.h0, t));
-        HIPCHECK(h, bft::launch_hash(dim3((uint32_t)((n + 31) / 32)), t, p));
+        uint32_t* sfx = h->sets[pipe ? h->cur_set : 0].sfx;
+        const uint32_t H = h->cfg.heights, K = h->sfx_rows;
+        if (K >= H && BFT_SFX_ON_LAUNCH_STREAM) {
+            // one chunk: the suffix rows on the launch stream, right behind the consensus kernel (a short
+            // full-chip pass), the chains on the set's hash stream
+            HIPCHECK(h, hipEventRecord(ev.h0, s));
+            HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, 1, K, sfx, s, p));
+            HIPCHECK(h, hipEventRecord(ev.sx, s));
+            if (pipe) HIPCHECK(h, hipStreamWaitEvent(t, ev.sx, 0));
+            HIPCHECK(h, bft::launch_hash_chain((uint32_t)n, 1, K, sfx, t, p));
+        } else {
+            // chunks of K heights share the suffix rows: suffix and chain kernels in order on one stream
+            if (pipe) HIPCHECK(h, hipStreamWaitEvent(t, ev.c1, 0));
+            HIPCHECK(h, hipEventRecord(ev.h0, t));
+            for (uint32_t x0 = 1; x0 <= H; x0 += K) {
+                HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, x0, K, sfx, t, p));
+                HIPCHECK(h, bft::launch_hash_chain((uint32_t)n, x0, K, sfx, t, p));
+            }
+        }
         HIPCHECK(h, hipEventRecord(ev.h1, t));
         if (pipe) {
             HIPCHECK(h, hipEventRecord(h->sets[h->cur_set].done, t));
@@ -974,10 +1024,20 @@ int bftsim_export_headers(bftsim_t* h, uint8_t* hdr, uint32_t* hdr_len) {
 }
 
 int bftsim_run(bftsim_t* h, uint64_t first, uint64_t n, bftsim_result* out) {
-    int rc = bftsim_prepare(h, n);
-    if (rc) return rc;
-    if ((rc = bftsim_launch(h, first, nullptr))) return rc;
-    return bftsim_fetch(h, out);
+    if (!h || !out) return BFTSIM_EINVAL;
+    for (;;) {
+        int rc = bftsim_prepare(h, n);
+        if (rc) return rc;
+        if ((rc = bftsim_launch(h, first, nullptr))) return rc;
+        if ((rc = bftsim_fetch(h, out))) return rc;
+        // the RoundChangeSet is unbounded in the reference (round_change_set.rs:11-35): an overflowing
+        // batch is run again at twice the capacity
+        bool over = false;
+        for (uint64_t i = 0; i < n && !over; ++i) over = (out->flags[i] & BFTSIM_FLAG_RCS_OVERFLOW) != 0;
+        if (!over || h->rcs_k >= bft::RCS_MAX_K) return BFTSIM_OK;
+        const uint32_t k = 2u * h->rcs_k;
+        if ((rc = bftsim_set_rcs_capacity(h, k < bft::RCS_MAX_K ? k : bft::RCS_MAX_K))) return rc;
+    }
 }
 
 int bftsim_fetch_summary(bftsim_t* h, uint64_t* committed_height, uint32_t* flags, uint32_t* ticks,

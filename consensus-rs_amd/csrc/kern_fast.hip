@@ -99,33 +99,90 @@ __device__ inline void keccak_f1600_pair(uint32_t X[25], uint32_t odd) {
 
 #endif
 
-__global__ __launch_bounds__(64) void bft_hash_pair_kernel(Params p) {
+// The pass is split in two kernels so that the sequential chains carry only what chains: prev_hash.
+// 1. bft_hash_suffix_kernel, one thread per (instance, height): the header bytes after prev_hash
+//    (proposer address, the seeded tx_hash's two Philox draws, height, time, ...) into a suffix row
+//    (bft_common.h header_suffix). Fully parallel: it fills the chip and overlaps the consensus waves.
+// 2. bft_hash_chain_kernel, a lane pair per instance: per height, encode prev_hash (36..68 bytes), splice
+//    the suffix behind it with one v_alignbyte per message dword (splice_word; the suffix row is in LDS,
+//    loaded one height ahead), absorb, permute. Both lanes used to run the whole encoder.
+__global__ __launch_bounds__(256) void bft_hash_suffix_kernel(Params p) {
+    const uint32_t K = p.sfx_rows;
+    const uint32_t n = p.n_instances;
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;  // n * rows < 2^32 (bftsim.hip)
+    const uint32_t j = t / n, il = t - j * n;           // consecutive threads: consecutive instances
+    if (j >= K) return;
+    const uint32_t x = p.sfx_x0 + j;
+    if (x > p.committed_height[il]) return;
+    const uint4 row = *(const uint4*)(p.rec + ((uint64_t)il * p.rows + x) * 4);
+    const uint32_t prop = row.y & 0xffffu, var = (row.y >> 16) & 1u;
+    const uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)row.z + 1ull);
+    header_suffix_strided(p.sfx + (uint64_t)j * SFX_DEV_DW * n + il, n, p.addresses + 20u * prop, p.seed,
+                          p.first_instance + il, x, prop, var, time);
+}
+
+__global__ __launch_bounds__(64) void bft_hash_chain_kernel(Params p) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    __shared__ __attribute__((aligned(16))) uint64_t bufs[64 * HDR_WORDS];
-    const uint32_t odd = threadIdx.x & 1u;
-    const uint32_t il = blockIdx.x * 32u + (threadIdx.x >> 1);
+    __shared__ __attribute__((aligned(16))) uint32_t sbuf[32 * SFX_BUF];      // splice buffer per pair
+    __shared__ __attribute__((aligned(16))) uint64_t pbuf[64 * PFX_WORDS];    // prefix per lane
+    const uint32_t odd = threadIdx.x & 1u, pair = threadIdx.x >> 1;
+    const uint32_t il = blockIdx.x * 32u + pair;
     if (il >= p.n_instances) return;                  // both lanes of a pair leave together
-    const uint32_t inst = p.first_instance + il;
+    const uint32_t K = p.sfx_rows, x0 = p.sfx_x0;
     const uint32_t ch = p.committed_height[il];
+    const uint32_t x1 = ch < x0 + K - 1u ? ch : x0 + K - 1u;
+    if (x1 < x0) return;
+    uint32_t* sb = sbuf + pair * SFX_BUF;
+    for (uint32_t i = odd; i < SFX_PAD; i += 2u) sb[i] = 0;
+    for (uint32_t i = SFX_PAD + SFX_BODY_DW + odd; i < SFX_BUF; i += 2u) sb[i] = 0;
+    // the parent of x0: genesis, or the previous chunk's last hash (same stream, already written)
+    const uint8_t* ph = x0 == 1u ? p.genesis_hash : p.hash + ((uint64_t)il * p.rows + x0 - 1u) * 32;
     uint32_t prev[8];
     for (int i = 0; i < 8; ++i)
-        prev[i] = (uint32_t)p.genesis_hash[4 * i] | ((uint32_t)p.genesis_hash[4 * i + 1] << 8) |
-                  ((uint32_t)p.genesis_hash[4 * i + 2] << 16) | ((uint32_t)p.genesis_hash[4 * i + 3] << 24);
-    uint64_t* wb = bufs + threadIdx.x * HDR_WORDS;     // each lane encodes its own copy (no exchange)
-    const uint32_t* wh = (const uint32_t*)wb + odd;   // this lane's halves of the message words
-    for (uint32_t x = 1; x <= ch; ++x) {
-        const uint32_t* row = p.rec + ((uint64_t)il * p.rows + x) * 4;
-        const uint32_t w1 = row[1];
-        const uint32_t prop = w1 & 0xffffu, var = (w1 >> 16) & 1u, T = row[2];
-        const uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)T + 1ull);
-        const uint32_t nb = header_words(wb, prev, p.addresses + 20u * prop, p.seed, inst, x, prop, var, time);
+        prev[i] = (uint32_t)ph[4 * i] | ((uint32_t)ph[4 * i + 1] << 8) | ((uint32_t)ph[4 * i + 2] << 16) |
+                  ((uint32_t)ph[4 * i + 3] << 24);
+    // this lane's half of the suffix body of the next height, and its length
+    constexpr uint32_t HALF = SFX_BODY_DW / 2u;
+    const uint32_t n = p.n_instances;
+    const uint64_t rstride = (uint64_t)SFX_DEV_DW * n;   // suffix rows: [height][dword][instance]
+    const uint32_t* srow = p.sfx + il + (uint64_t)odd * HALF * n;
+    uint32_t s[HALF], slen;
+#pragma unroll
+    for (uint32_t i = 0; i < HALF; ++i) s[i] = srow[(uint64_t)i * n];
+    slen = p.sfx[il + (uint64_t)SFX_DEV_LEN_DW * n];
+    uint64_t* pb = pbuf + threadIdx.x * PFX_WORDS;
+    const uint32_t* pw = (const uint32_t*)pb + odd;
+    for (uint32_t x = x0; x <= x1; ++x) {
+#pragma unroll
+        for (uint32_t i = 0; i < HALF; ++i) sb[SFX_PAD + odd * HALF + i] = s[i];
+        const uint32_t len_s = slen;
+        if (x < x1) {                                 // prefetch height x + 1
+            const uint64_t ro = (uint64_t)(x + 1u - x0) * rstride;
+#pragma unroll
+            for (uint32_t i = 0; i < HALF; ++i) s[i] = srow[ro + (uint64_t)i * n];
+            slen = p.sfx[il + ro + (uint64_t)SFX_DEV_LEN_DW * n];
+        }
+        const uint32_t len_p = header_prefix(pb, prev);
+        __syncthreads();                              // the pair's suffix halves and this lane's prefix
+        const uint32_t c = 72u - len_p, r = c & 3u, nb = splice_blocks(len_p, len_s);
+        const uint32_t* sx = sb + (c >> 2) + odd;    // dword w = 2i + odd of each block
         uint32_t X[25];
 #pragma unroll
         for (int i = 0; i < 25; ++i) X[i] = 0;
-#pragma unroll 1
-        for (uint32_t blk = 0; blk < nb; ++blk) {
 #pragma unroll
-            for (int i = 0; i < 17; ++i) X[i] ^= wh[2 * (17u * blk + i)];
+        for (uint32_t i = 0; i < 17; ++i) {           // block 0: the prefix lies here
+            uint32_t v = align_bytes(sx[2u * i + 1u], sx[2u * i], r);
+            if (i < PFX_WORDS) v |= pw[2u * i];
+            X[i] ^= v;
+        }
+        if (odd & (nb == 1u)) X[16] ^= 0x80000000u;
+        keccak_f1600_pair(X, odd);
+#pragma unroll 1
+        for (uint32_t blk = 1; blk < nb; ++blk) {
+            const uint32_t* sxb = sx + 34u * blk;
+#pragma unroll
+            for (uint32_t i = 0; i < 17; ++i) X[i] ^= align_bytes(sxb[2u * i + 1u], sxb[2u * i], r);
+            if (odd & (blk + 1u == nb)) X[16] ^= 0x80000000u;
             keccak_f1600_pair(X, odd);
         }
         uint32_t* dst = (uint32_t*)(p.hash + ((uint64_t)il * p.rows + x) * 32);
@@ -136,11 +193,24 @@ __global__ __launch_bounds__(64) void bft_hash_pair_kernel(Params p) {
             prev[2 * i] = odd ? o : X[i];
             prev[2 * i + 1] = odd ? X[i] : o;
         }
+        __syncthreads();                              // splice buffer read before the next height's write
     }
 #endif
 }
-hipError_t launch_hash(dim3 grid, hipStream_t s, const Params& p) {
-    hipLaunchKernelGGL(bft_hash_pair_kernel, grid, dim3(64), 0, s, p);
+
+// heights [x0, x0 + rows) of the block-hash pass: the suffix rows, then the chains
+hipError_t launch_hash_suffix(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, hipStream_t s, Params p) {
+    p.sfx = sfx;
+    p.sfx_rows = rows;
+    p.sfx_x0 = x0;
+    hipLaunchKernelGGL(bft_hash_suffix_kernel, dim3((uint32_t)(((uint64_t)n * rows + 255u) / 256u)), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, hipStream_t s, Params p) {
+    p.sfx = sfx;
+    p.sfx_rows = rows;
+    p.sfx_x0 = x0;
+    hipLaunchKernelGGL(bft_hash_chain_kernel, dim3((n + 31u) / 32u), dim3(64), 0, s, p);
     return hipGetLastError();
 }
 

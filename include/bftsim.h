@@ -40,7 +40,7 @@ extern "C" {
 #define BFTSIM_FLAG_CORE_PANIC 4u    /* a Core panicked (core.rs:540 unwrap on no request) */
 #define BFTSIM_FLAG_OUTBOX 8u        /* a second message of one kind in one phase was dropped */
 #define BFTSIM_FLAG_TIMEOUT 16u      /* max_ticks reached before `heights` */
-#define BFTSIM_FLAG_RCS_OVERFLOW 32u /* more round-change rounds than the GPU table holds */
+#define BFTSIM_FLAG_RCS_OVERFLOW 32u /* more round-change rounds than the set's capacity (bftsim_set_rcs_capacity) */
 #define BFTSIM_FLAG_WINDOW 64u       /* windowed run: a lookup older than the row ring (result unpinned) */
 
 /* Conventions the reference leaves to unvendored crates (SPEC.md §1, §7): they are
@@ -154,6 +154,12 @@ int bftsim_set_trace(bftsim_t *h, uint64_t *host_out, uint32_t trace_ticks);
  * read bftsim_fetch_summary and the histograms of bftsim_stats_get. A lookup older than the ring
  * (a validator lagging > window heights) sets BFTSIM_FLAG_WINDOW. */
 int bftsim_set_window(bftsim_t *h, uint32_t window);
+/* RoundChangeSet capacity: distinct round-change rounds each validator keeps between two resets of its
+ * set (the reference's HashMap<u64, MessageManage>, round_change_set.rs:11-35, is unbounded).
+ * 1..4096, default 16. A validator needing more sets BFTSIM_FLAG_RCS_OVERFLOW on its instance;
+ * bftsim_run then re-runs the batch at twice the capacity until no instance overflows (instances are
+ * independent and deterministic, so the others are unchanged). Takes effect at the next bftsim_prepare. */
+int bftsim_set_rcs_capacity(bftsim_t *h, uint32_t rounds);
 /* per-instance outputs of the last launch (any pointer may be NULL); tip_hash[i*32..] = hash of
  * the block at committed_height[i] (the genesis hash at 0), which commits to the whole chain */
 int bftsim_fetch_summary(bftsim_t *h, uint64_t *committed_height, uint32_t *flags, uint32_t *ticks,

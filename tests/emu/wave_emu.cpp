@@ -328,7 +328,8 @@ extern "C" int emu_run_stream(const bftsim_config* cfg, uint64_t first, uint64_t
     uint32_t per_wave = seg > 64 ? 1 : 64 / seg;
     uint32_t waves = (uint32_t)((n + per_wave - 1) / per_wave);
     std::vector<uint8_t> lds(bft::lds_bytes(seg, true));
-    std::vector<uint32_t> rcs((size_t)waves * bft::rcs_words(seg), 0xcdcdcdcdu);
+    if (const char* e = getenv("BFT_EMU_RCS_K")) P.rcs_k = (uint32_t)atoi(e);   // RoundChangeSet capacity
+    std::vector<uint32_t> rcs((size_t)waves * bft::rcs_words(seg, P.rcs_k), 0xcdcdcdcdu);
     P.rcs = rcs.data();
     std::vector<uint32_t> backlog(P.backlog_replay ? (size_t)waves * bft::backlog_words(seg) : 0, 0);
     P.backlog = P.backlog_replay ? backlog.data() : nullptr;
@@ -387,7 +388,8 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
     uint32_t per_wave = seg > 64 ? 1 : 64 / seg;
     uint32_t waves = (uint32_t)((n + per_wave - 1) / per_wave);
     std::vector<uint8_t> lds(bft::lds_bytes(seg, P.need_seed != 0));
-    std::vector<uint32_t> rcs((size_t)waves * bft::rcs_words(seg), 0xcdcdcdcdu);
+    if (const char* e = getenv("BFT_EMU_RCS_K")) P.rcs_k = (uint32_t)atoi(e);   // RoundChangeSet capacity
+    std::vector<uint32_t> rcs((size_t)waves * bft::rcs_words(seg, P.rcs_k), 0xcdcdcdcdu);
     P.rcs = rcs.data();
     std::vector<uint32_t> backlog(P.backlog_replay ? (size_t)waves * bft::backlog_words(seg) : 0, 0);
     P.backlog = P.backlog_replay ? backlog.data() : nullptr;
@@ -418,9 +420,10 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
         for (uint64_t i = 0; i < n; ++i) nb += resume[i];
         fprintf(stderr, "emu: FAST handed over %llu of %llu instances\n", (unsigned long long)nb, (unsigned long long)n);
     }
-    // the hash post-pass (bft_hash_pair_kernel computes the same Keccak-256 chain, two lanes per state)
+    // the hash post-pass, as kern_fast.hip splits it: every height's header suffix first
+    // (bft_hash_suffix_kernel), then the chain, splicing prev_hash in front (bft_hash_chain_kernel)
     if (!P.need_seed) {
-        alignas(16) uint8_t buf[bft::LANE_HASH_BUF];
+        uint32_t sfx[bft::SFX_DWORDS];
         for (uint64_t il = 0; il < n; ++il) {
             uint32_t prev[8];
             for (int i = 0; i < 8; ++i)
@@ -431,8 +434,9 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
                 uint32_t prop = row[1] & 0xffffu, var = (row[1] >> 16) & 1u;
                 uint64_t time = cfg->genesis_time + (uint64_t)cfg->block_period * ((uint64_t)row[2] + 1ull);
                 uint32_t out[8];
-                bft::lane_block_hash(buf, prev, cfg->addresses + 20u * prop, cfg->seed, (uint32_t)(first + il), x,
-                                     prop, var, time, out);
+                bft::header_suffix((uint64_t*)sfx, cfg->addresses + 20u * prop, cfg->seed, (uint32_t)(first + il), x,
+                                   prop, var, time);
+                bft::spliced_block_hash(sfx, prev, out);
                 memcpy(&hs[(il * hcap + x) * 32], out, 32);
                 for (int i = 0; i < 8; ++i) prev[i] = out[i];
             }
@@ -457,4 +461,37 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
         }
     }
     return 0;
+}
+
+// The splice of the block-hash pass against the one-piece encoder: `trials` random headers (random parent
+// hashes, proposers, variants, heights and times), including parents with every byte >= 128 or < 128 (the
+// longest and shortest prefixes) and heights / times at MessagePack width boundaries. Returns mismatches.
+extern "C" int emu_splice_check(uint32_t trials, uint64_t seed) {
+    uint64_t s = seed | 1ull;
+    auto rnd = [&]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
+    std::vector<uint8_t> addr(64 * 20);
+    for (auto& b : addr) b = (uint8_t)rnd();
+    int bad = 0;
+    alignas(16) uint8_t buf[bft::LANE_HASH_BUF];
+    uint32_t sfx[bft::SFX_DWORDS];
+    const uint64_t times[] = {0ull, 127ull, 128ull, 255ull, 256ull, 65535ull, 65536ull, 4294967295ull, 4294967296ull, ~0ull};
+    const uint32_t heights[] = {1u, 127u, 128u, 255u, 256u, 65535u, 65536u, 4294967295u};
+    for (uint32_t t = 0; t < trials; ++t) {
+        uint32_t prev[8];
+        for (int i = 0; i < 8; ++i) {
+            uint32_t v = (uint32_t)rnd();
+            if (t % 4 == 1) v |= 0x80808080u;
+            if (t % 4 == 2) v &= 0x7f7f7f7fu;
+            prev[i] = v;
+        }
+        const uint32_t prop = (uint32_t)(rnd() % 64), var = (uint32_t)(rnd() & 1), inst = (uint32_t)rnd();
+        const uint32_t h = (t % 3 == 0) ? heights[rnd() % 8] : (uint32_t)rnd();
+        const uint64_t time = (t % 3 == 1) ? times[rnd() % 10] : rnd();
+        uint32_t a[8], b[8];
+        bft::lane_block_hash(buf, prev, addr.data() + 20u * prop, s, inst, h, prop, var, time, a);
+        bft::header_suffix((uint64_t*)sfx, addr.data() + 20u * prop, s, inst, h, prop, var, time);
+        bft::spliced_block_hash(sfx, prev, b);
+        if (memcmp(a, b, 32) != 0) ++bad;
+    }
+    return bad;
 }

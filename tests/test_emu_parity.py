@@ -118,3 +118,40 @@ def test_full_kernel_alone_n64(name, mk, monkeypatch):
     monkeypatch.setenv("BFT_EMU_FAST", "0")
     cfg = mk()
     assert_same(O.run(cfg, 0, 2), E.run(cfg, 0, 2), name + " full kernel")
+
+
+def test_block_hash_splice_matches_one_piece_encoder():
+    """The block-hash pass encodes every height's header suffix in one parallel kernel and splices
+    prev_hash in front in the chain (kern_fast.hip, bft_common.h header_suffix / splice_word). The
+    splice equals the one-piece encoder of the header (SPEC.md §7) for random headers, including parents
+    of all-high and all-low bytes (prefix 68 and 36 bytes, so 2- and 3-block messages) and heights /
+    times at every MessagePack width boundary."""
+    import ctypes
+    lib = E.lib()
+    lib.emu_splice_check.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
+    assert lib.emu_splice_check(20000, 12345) == 0
+    assert lib.emu_splice_check(20000, 987654321) == 0
+
+
+def test_roundchangeset_capacity_overflow_is_flagged_and_local(monkeypatch):
+    """The GPU RoundChangeSet holds a runtime number of rounds per validator (Params::rcs_k,
+    bftsim_set_rcs_capacity); the reference's is an unbounded HashMap (round_change_set.rs:11-35). A
+    validator that needs more sets BFTSIM_FLAG_RCS_OVERFLOW on its instance; every instance that did not
+    overflow is exactly the oracle's (instances are independent), and at a capacity that suffices the
+    whole batch is (bftsim_run re-runs an overflowing batch at twice the capacity)."""
+    cfg = BftConfig(n=16, heights=30, seed=4, proposer_crash_ppm=300_000, name="cfg4-n16")
+    ref = O.run(cfg, 0, 32)
+    monkeypatch.setenv("BFT_EMU_RCS_K", "1")
+    got = E.run(cfg, 0, 32)
+    over = (got["flags"] & 32) != 0
+    assert over.any() and not over.all()
+    keep = ~over
+    for k in ("committed_height", "ticks", "views", "flags"):
+        assert (got[k][keep] == ref[k][keep]).all(), k
+    for k in ("round", "proposer", "variant", "time_tick", "block_hash"):
+        assert (got[k][keep] == ref[k][keep]).all(), k
+    cfg7 = BftConfig(n=7, heights=30, seed=8, drop_ppm=300_000)
+    monkeypatch.setenv("BFT_EMU_RCS_K", "2")
+    assert ((E.run(cfg7, 0, 16)["flags"] & 32) != 0).all()
+    monkeypatch.setenv("BFT_EMU_RCS_K", "8")
+    assert_same(O.run(cfg7, 0, 16), E.run(cfg7, 0, 16), "n7-drop30 rcs_k=8")

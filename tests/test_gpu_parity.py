@@ -105,3 +105,21 @@ def test_gpu_full_kernel_alone_n64(name, mk, n, monkeypatch):
     finally:
         sim.close()
     assert_same(O.run(cfg, 0, n), got, name + " full kernel")
+
+
+@pytest.mark.gpu
+def test_gpu_roundchangeset_capacity_grows_until_no_overflow():
+    """A RoundChangeSet capacity of one round overflows on a lossy N=7 batch and a crash-storm N=16
+    batch; bftsim_run re-runs at twice the capacity until no instance overflows (the reference's map is
+    unbounded, round_change_set.rs:11-35), and the outputs are the oracle's."""
+    from bftsim.runtime import Simulator
+    for cfg, n in ((BftConfig(n=7, heights=30, seed=8, drop_ppm=300_000), 64),
+                   (BftConfig(n=16, heights=30, seed=4, proposer_crash_ppm=300_000, name="cfg4-n16"), 64)):
+        sim = Simulator(cfg)
+        try:
+            sim.set_rcs_capacity(1)
+            got = sim.run(0, n)
+        finally:
+            sim.close()
+        assert not ((got["flags"] & 32) != 0).any()
+        assert_same(O.run(cfg, 0, n), got, f"{cfg.name} rcs capacity 1 -> grown")

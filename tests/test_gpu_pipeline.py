@@ -60,7 +60,7 @@ def test_pipeline_toggle_and_sizes():
 
 def test_timed_mode_full_size():
     """The exact mode bench.py times: cfg3 at 16,384 instances, pipeline depth 3 (so the hash pass is
-    bft_hash_pair_kernel on its set's stream under the ring), repeated launches of the same instances;
+    the block-hash pass (bft_hash_suffix_kernel + bft_hash_chain_kernel) on its set's stream under the ring), repeated launches of the same instances;
     the last launch's results against the oracle over every instance."""
     from bftsim.configs import INSTANCES
     cfg = cfg3()
