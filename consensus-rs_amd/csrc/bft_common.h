@@ -662,6 +662,57 @@ BFT_FN uint32_t header_prefix(uint64_t* wb, const uint32_t prev[8]) {     // wb:
     while (w.wi < PFX_WORDS) wb[w.wi++] = 0;
     return len;
 }
+// The prefix for the chains, branch-free: each prev_hash word's MessagePack expansion (a byte >= 128
+// becomes 0xcc b) is two v_perm_b32 of {0xcccccccc, w} with selectors from a 16-entry table indexed by
+// the word's four high bits, and the expansions are appended to the stream with an unconditional store
+// per word (the divergent `put` of HdrWriter costs both of its paths). Same bytes as header_prefix.
+struct PfxSel { uint32_t lo, hi; };
+BFT_FN constexpr PfxSel pfx_sel(uint32_t idx) {               // output byte k: 4 = 0xcc, i = byte i, 12 = 0
+    uint32_t out[8] = {12, 12, 12, 12, 12, 12, 12, 12};
+    uint32_t pos = 0;
+    for (uint32_t i = 0; i < 4; ++i) {
+        if ((idx >> i) & 1u) out[pos++] = 4;
+        out[pos++] = i;
+    }
+    return PfxSel{out[0] | out[1] << 8 | out[2] << 16 | out[3] << 24, out[4] | out[5] << 8 | out[6] << 16 | out[7] << 24};
+}
+BFT_FN uint32_t perm_bytes(uint32_t s0, uint32_t s1, uint32_t sel) {   // v_perm_b32 (selectors 0..7, 12)
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_perm(s0, s1, sel);
+#else
+    const uint64_t v = ((uint64_t)s0 << 32) | s1;
+    uint32_t d = 0;
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t q = (sel >> (8 * k)) & 0xffu;
+        d |= (q < 8 ? (uint32_t)((v >> (8 * q)) & 0xffu) : 0u) << (8 * k);
+    }
+    return d;
+#endif
+}
+// `tbl`: pfx_sel(0..15) (LDS on the device); wb: PFX_WORDS + 4 words. Returns the prefix length.
+BFT_FN uint32_t header_prefix_perm(uint64_t* wb, const uint32_t prev[8], const PfxSel* tbl) {
+    uint64_t acc = 0x2000dc9dull;                     // array(13); prev_hash: array16(32)
+    uint32_t fill = 4, wi = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t w = prev[i];
+        const uint32_t idx = ((((w >> 7) & 0x01010101u) * 0x10204080u) >> 28);   // the four high bits
+        const PfxSel sel = tbl[idx];
+        const uint64_t v = (uint64_t)perm_bytes(0xccccccccu, w, sel.lo) | ((uint64_t)perm_bytes(0xccccccccu, w, sel.hi) << 32);
+        const uint32_t n = 4u + (uint32_t)__builtin_popcount(idx);
+        const uint32_t sh = 8u * fill, nf = fill + n;
+        const uint64_t lo = acc | (v << sh);
+        wb[wi] = lo;                                  // rewritten until the word is complete
+        const bool full = nf >= 8u;
+        acc = full ? (sh ? v >> (64u - sh) : 0ull) : lo;
+        wi += full ? 1u : 0u;
+        fill = full ? nf - 8u : nf;
+    }
+    wb[wi] = acc;
+#pragma unroll
+    for (uint32_t k = 1; k <= 4; ++k) wb[wi + k] = 0;   // wi >= 4: words past the prefix up to PFX_WORDS
+    return 8u * wi + fill;
+}
 BFT_FN uint32_t align_bytes(uint32_t hi, uint32_t lo, uint32_t r) {      // ({hi, lo} >> 8r)[31:0], r < 4
 #if defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_alignbyte(hi, lo, r);
@@ -721,10 +772,15 @@ BFT_FN void lane_block_hash(uint8_t* buf, const uint32_t prev[8], const uint8_t*
 // The same hash through the two-kernel block-hash pass's splice (host: the CPU emulator's post-pass).
 // sfx: the height's suffix row (SFX_DWORDS dwords, header_suffix).
 inline void spliced_block_hash(const uint32_t* sfx, const uint32_t prev[8], uint32_t out[8]) {
+    for (int i = 0; i < 8; ++i) out[i] = 0;
     uint32_t buf[SFX_BUF] = {};
     for (uint32_t i = 0; i < SFX_BODY_DW; ++i) buf[SFX_PAD + i] = sfx[i];
-    uint64_t pfx[PFX_WORDS];
-    const uint32_t lp = header_prefix(pfx, prev);
+    uint64_t pfx[PFX_WORDS + 4], ref[PFX_WORDS];
+    PfxSel tbl[16];
+    for (uint32_t i = 0; i < 16; ++i) tbl[i] = pfx_sel(i);
+    const uint32_t lp = header_prefix_perm(pfx, prev, tbl);
+    if (header_prefix(ref, prev) != lp) return;      // leaves `out` unset: the checks fail loudly
+    for (uint32_t i = 0; i < PFX_WORDS; ++i) if (ref[i] != pfx[i]) return;
     uint32_t pw[2 * PFX_WORDS];
     for (uint32_t i = 0; i < PFX_WORDS; ++i) { pw[2 * i] = (uint32_t)pfx[i]; pw[2 * i + 1] = (uint32_t)(pfx[i] >> 32); }
     const uint32_t c = 72u - lp, nb = splice_blocks(lp, sfx[SFX_LEN_DW]);

@@ -664,9 +664,6 @@ void bftsim_destroy(bftsim_t* h) {
 }
 
 static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n);
-#ifndef BFT_SFX_ON_LAUNCH_STREAM
-#define BFT_SFX_ON_LAUNCH_STREAM 1    // A/B switch (scripts/gpu_r03k.sh)
-#endif
 
 int bftsim_prepare(bftsim_t* h, uint64_t n) {
     if (!h || n == 0 || n > (1ull << 31)) return fail(h, BFTSIM_EINVAL, "bad instance count");
@@ -881,7 +878,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         hipStream_t t = pipe ? h->sets[h->cur_set].hs : s;
         uint32_t* sfx = h->sets[pipe ? h->cur_set : 0].sfx;
         const uint32_t H = h->cfg.heights, K = h->sfx_rows;
-        if (K >= H && BFT_SFX_ON_LAUNCH_STREAM) {
+        if (K >= H && BFT_SFX_MODE == 0) {
             // one chunk: the suffix rows on the launch stream, right behind the consensus kernel (a short
             // full-chip pass), the chains on the set's hash stream
             HIPCHECK(h, hipEventRecord(ev.h0, s));

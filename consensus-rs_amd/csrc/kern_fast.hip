@@ -106,28 +106,52 @@ __device__ inline void keccak_f1600_pair(uint32_t X[25], uint32_t odd) {
 // 2. bft_hash_chain_kernel, a lane pair per instance: per height, encode prev_hash (36..68 bytes), splice
 //    the suffix behind it with one v_alignbyte per message dword (splice_word; the suffix row is in LDS,
 //    loaded one height ahead), absorb, permute. Both lanes used to run the whole encoder.
-__global__ __launch_bounds__(256) void bft_hash_suffix_kernel(Params p) {
-    const uint32_t K = p.sfx_rows;
-    const uint32_t n = p.n_instances;
-    const uint32_t t = blockIdx.x * 256u + threadIdx.x;  // n * rows < 2^32 (bftsim.hip)
-    const uint32_t j = t / n, il = t - j * n;           // consecutive threads: consecutive instances
-    if (j >= K) return;
-    const uint32_t x = p.sfx_x0 + j;
-    if (x > p.committed_height[il]) return;
+__device__ inline void suffix_row(const Params& p, uint32_t il, uint32_t j) {
+    const uint32_t n = p.n_instances, x = p.sfx_x0 + j;
     const uint4 row = *(const uint4*)(p.rec + ((uint64_t)il * p.rows + x) * 4);
     const uint32_t prop = row.y & 0xffffu, var = (row.y >> 16) & 1u;
     const uint64_t time = p.genesis_time + (uint64_t)p.block_period * ((uint64_t)row.z + 1ull);
     header_suffix_strided(p.sfx + (uint64_t)j * SFX_DEV_DW * n + il, n, p.addresses + 20u * prop, p.seed,
                           p.first_instance + il, x, prop, var, time);
 }
+__global__ __launch_bounds__(256) void bft_hash_suffix_kernel(Params p) {
+    const uint32_t K = p.sfx_rows;
+    const uint32_t n = p.n_instances;
+#if BFT_SFX_MODE == 2
+    // a thread per instance over its heights: few waves, beside the consensus kernels on the hash stream
+    const uint32_t il = blockIdx.x * 256u + threadIdx.x;
+    if (il >= n) return;
+    const uint32_t ch = p.committed_height[il];
+    for (uint32_t j = 0; j < K && p.sfx_x0 + j <= ch; ++j) suffix_row(p, il, j);
+#else
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;  // n * rows < 2^32 (bftsim.hip)
+    const uint32_t j = t / n, il = t - j * n;           // consecutive threads: consecutive instances
+    if (j >= K) return;
+    if (p.sfx_x0 + j > p.committed_height[il]) return;
+    suffix_row(p, il, j);
+#endif
+}
+
+__constant__ PfxSel PFX_TBL[16] = {pfx_sel(0), pfx_sel(1), pfx_sel(2), pfx_sel(3), pfx_sel(4), pfx_sel(5),
+                                   pfx_sel(6), pfx_sel(7), pfx_sel(8), pfx_sel(9), pfx_sel(10), pfx_sel(11),
+                                   pfx_sel(12), pfx_sel(13), pfx_sel(14), pfx_sel(15)};
 
 __global__ __launch_bounds__(64) void bft_hash_chain_kernel(Params p) {
 #if defined(__HIP_DEVICE_COMPILE__)
     __shared__ __attribute__((aligned(16))) uint32_t sbuf[32 * SFX_BUF];      // splice buffer per pair
-    __shared__ __attribute__((aligned(16))) uint64_t pbuf[64 * PFX_WORDS];    // prefix per lane
+    __shared__ __attribute__((aligned(16))) uint64_t pbuf[64 * (PFX_WORDS + 4)];   // prefix per lane
+    __shared__ PfxSel ptbl[16];                                                 // header_prefix_perm
+    if (threadIdx.x < 16) ptbl[threadIdx.x] = PFX_TBL[threadIdx.x];
+    __syncthreads();
     const uint32_t odd = threadIdx.x & 1u, pair = threadIdx.x >> 1;
     const uint32_t il = blockIdx.x * 32u + pair;
     if (il >= p.n_instances) return;                  // both lanes of a pair leave together
+#ifndef BFT_CHAIN_PRIO_BELOW
+#define BFT_CHAIN_PRIO_BELOW 6144   // gpurun r03mn: 2,048 per GPU 1.63e8 -> 2.0e8, 4,096 2.94e8 -> 3.38e8, 8,192 unchanged
+#endif
+    // small shards are bound by the chains' issue latency, not by the consensus kernels beside them: the
+    // chains outrank them (large shards: the consensus kernels are the critical path and keep priority 2)
+    if (p.n_instances < BFT_CHAIN_PRIO_BELOW) __builtin_amdgcn_s_setprio(3);
     const uint32_t K = p.sfx_rows, x0 = p.sfx_x0;
     const uint32_t ch = p.committed_height[il];
     const uint32_t x1 = ch < x0 + K - 1u ? ch : x0 + K - 1u;
@@ -150,7 +174,7 @@ __global__ __launch_bounds__(64) void bft_hash_chain_kernel(Params p) {
 #pragma unroll
     for (uint32_t i = 0; i < HALF; ++i) s[i] = srow[(uint64_t)i * n];
     slen = p.sfx[il + (uint64_t)SFX_DEV_LEN_DW * n];
-    uint64_t* pb = pbuf + threadIdx.x * PFX_WORDS;
+    uint64_t* pb = pbuf + threadIdx.x * (PFX_WORDS + 4);
     const uint32_t* pw = (const uint32_t*)pb + odd;
     for (uint32_t x = x0; x <= x1; ++x) {
 #pragma unroll
@@ -162,7 +186,7 @@ __global__ __launch_bounds__(64) void bft_hash_chain_kernel(Params p) {
             for (uint32_t i = 0; i < HALF; ++i) s[i] = srow[ro + (uint64_t)i * n];
             slen = p.sfx[il + ro + (uint64_t)SFX_DEV_LEN_DW * n];
         }
-        const uint32_t len_p = header_prefix(pb, prev);
+        const uint32_t len_p = header_prefix_perm(pb, prev, ptbl);
         __syncthreads();                              // the pair's suffix halves and this lane's prefix
         const uint32_t c = 72u - len_p, r = c & 3u, nb = splice_blocks(len_p, len_s);
         const uint32_t* sx = sb + (c >> 2) + odd;    // dword w = 2i + odd of each block
@@ -203,7 +227,11 @@ hipError_t launch_hash_suffix(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* 
     p.sfx = sfx;
     p.sfx_rows = rows;
     p.sfx_x0 = x0;
+#if BFT_SFX_MODE == 2
+    hipLaunchKernelGGL(bft_hash_suffix_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, p);
+#else
     hipLaunchKernelGGL(bft_hash_suffix_kernel, dim3((uint32_t)(((uint64_t)n * rows + 255u) / 256u)), dim3(256), 0, s, p);
+#endif
     return hipGetLastError();
 }
 hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, hipStream_t s, Params p) {
