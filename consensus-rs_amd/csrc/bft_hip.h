@@ -201,14 +201,11 @@ inline hipError_t launch_general(bool need_seed, bool ext, uint32_t seg, dim3 gr
     return ext ? launch_general_0_1(seg, grid, lds, s, p) : launch_general_0_0(seg, grid, lds, s, p);
 }
 hipError_t launch_fast(dim3 grid, hipStream_t s, const Params& p);               // kern_fast.hip
-// suffix kernel placement (A/B switch): 0 = a thread per (instance, height) on the launch stream,
-// 1 = the same on the row-table set's hash stream, 2 = a thread per instance on the hash stream
-#ifndef BFT_SFX_MODE
-#define BFT_SFX_MODE 0
-#endif
 // block-hash pass of heights [x0, x0 + rows) for n instances (kern_fast.hip): the header suffix rows,
 // then the prev_hash chains that splice them
-hipError_t launch_hash_suffix(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, hipStream_t s, Params p);
+// (loop: a thread per instance over its heights instead of a thread per (instance, height))
+hipError_t launch_hash_suffix(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, bool loop, hipStream_t s,
+                              Params p);
 hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, hipStream_t s, Params p);
 hipError_t launch_resume(dim3 grid, size_t lds, hipStream_t s, const Params& p);  // kern_resume.hip
 

@@ -718,6 +718,10 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         uint64_t rows = (2ull << 30) / per_row;
         if (rows < 1) rows = 1;
         if (rows > h->cfg.heights) rows = h->cfg.heights;
+        // tests only (BFTSIM_TESTING=1): fewer heights per chunk, so that small batches take the chunked path
+        const char* tst = getenv("BFTSIM_TESTING");
+        const char* cap = getenv("BFTSIM_SFX_ROWS");
+        if (tst && cap && strcmp(tst, "1") == 0 && atoi(cap) > 0 && (uint64_t)atoi(cap) < rows) rows = (uint64_t)atoi(cap);
         if (rows * n >= (1ull << 32)) rows = ((1ull << 32) - 1) / n;
         h->sfx_rows = (uint32_t)rows;
         for (uint32_t k = 0; k < h->n_sets; ++k) HIPCHECK(h, hipMalloc(&h->sets[k].sfx, rows * per_row));
@@ -878,11 +882,17 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         hipStream_t t = pipe ? h->sets[h->cur_set].hs : s;
         uint32_t* sfx = h->sets[pipe ? h->cur_set : 0].sfx;
         const uint32_t H = h->cfg.heights, K = h->sfx_rows;
-        if (K >= H && BFT_SFX_MODE == 0) {
-            // one chunk: the suffix rows on the launch stream, right behind the consensus kernel (a short
-            // full-chip pass), the chains on the set's hash stream
+        // Where the suffix rows go depends on how long the consensus kernel runs against the chains
+        // (A/B, profiles/r03/ab_sfx): the N = 64 FAST kernel (~1.9 ms at 16,384 instances) is shorter than
+        // the chains, so a full-chip pass by a thread per (instance, height) runs on the launch stream
+        // right behind it (on a hash stream its waves take the next consensus kernel's slots: cfg3 6.3e8
+        // instead of 7.6e8; a thread per instance there lengthens the ring: 6.4e8). The general kernels
+        // (many instances per wave, or a workgroup per instance) run far longer than the chains: a
+        // thread per instance on the hash stream hides the rows entirely (cfg2 6.8e8 -> 7.9e8).
+        const bool on_launch = fast;
+        if (K >= H && on_launch) {
             HIPCHECK(h, hipEventRecord(ev.h0, s));
-            HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, 1, K, sfx, s, p));
+            HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, 1, K, sfx, false, s, p));
             HIPCHECK(h, hipEventRecord(ev.sx, s));
             if (pipe) HIPCHECK(h, hipStreamWaitEvent(t, ev.sx, 0));
             HIPCHECK(h, bft::launch_hash_chain((uint32_t)n, 1, K, sfx, t, p));
@@ -891,7 +901,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
             if (pipe) HIPCHECK(h, hipStreamWaitEvent(t, ev.c1, 0));
             HIPCHECK(h, hipEventRecord(ev.h0, t));
             for (uint32_t x0 = 1; x0 <= H; x0 += K) {
-                HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, x0, K, sfx, t, p));
+                HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, x0, K, sfx, !on_launch, t, p));
                 HIPCHECK(h, bft::launch_hash_chain((uint32_t)n, x0, K, sfx, t, p));
             }
         }

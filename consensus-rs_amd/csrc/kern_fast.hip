@@ -117,19 +117,19 @@ __device__ inline void suffix_row(const Params& p, uint32_t il, uint32_t j) {
 __global__ __launch_bounds__(256) void bft_hash_suffix_kernel(Params p) {
     const uint32_t K = p.sfx_rows;
     const uint32_t n = p.n_instances;
-#if BFT_SFX_MODE == 2
-    // a thread per instance over its heights: few waves, beside the consensus kernels on the hash stream
-    const uint32_t il = blockIdx.x * 256u + threadIdx.x;
-    if (il >= n) return;
-    const uint32_t ch = p.committed_height[il];
-    for (uint32_t j = 0; j < K && p.sfx_x0 + j <= ch; ++j) suffix_row(p, il, j);
-#else
     const uint32_t t = blockIdx.x * 256u + threadIdx.x;  // n * rows < 2^32 (bftsim.hip)
     const uint32_t j = t / n, il = t - j * n;           // consecutive threads: consecutive instances
     if (j >= K) return;
     if (p.sfx_x0 + j > p.committed_height[il]) return;
     suffix_row(p, il, j);
-#endif
+}
+// the same rows with a thread per instance over its heights: few waves, run on the hash stream beside
+// the consensus kernels (large shards; launch_hash_suffix)
+__global__ __launch_bounds__(256) void bft_hash_suffix_loop_kernel(Params p) {
+    const uint32_t il = blockIdx.x * 256u + threadIdx.x;
+    if (il >= p.n_instances) return;
+    const uint32_t ch = p.committed_height[il];
+    for (uint32_t j = 0; j < p.sfx_rows && p.sfx_x0 + j <= ch; ++j) suffix_row(p, il, j);
 }
 
 __constant__ PfxSel PFX_TBL[16] = {pfx_sel(0), pfx_sel(1), pfx_sel(2), pfx_sel(3), pfx_sel(4), pfx_sel(5),
@@ -223,15 +223,13 @@ __global__ __launch_bounds__(64) void bft_hash_chain_kernel(Params p) {
 }
 
 // heights [x0, x0 + rows) of the block-hash pass: the suffix rows, then the chains
-hipError_t launch_hash_suffix(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, hipStream_t s, Params p) {
+hipError_t launch_hash_suffix(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, bool loop, hipStream_t s,
+                              Params p) {
     p.sfx = sfx;
     p.sfx_rows = rows;
     p.sfx_x0 = x0;
-#if BFT_SFX_MODE == 2
-    hipLaunchKernelGGL(bft_hash_suffix_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, p);
-#else
-    hipLaunchKernelGGL(bft_hash_suffix_kernel, dim3((uint32_t)(((uint64_t)n * rows + 255u) / 256u)), dim3(256), 0, s, p);
-#endif
+    if (loop) hipLaunchKernelGGL(bft_hash_suffix_loop_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(bft_hash_suffix_kernel, dim3((uint32_t)(((uint64_t)n * rows + 255u) / 256u)), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, hipStream_t s, Params p) {

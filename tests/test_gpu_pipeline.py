@@ -79,3 +79,29 @@ def test_timed_mode_full_size():
     ref = O.run(cfg, 0, n, threads=16)
     assert_same(ref, got, "cfg3 16384 pipelined x5")
     assert st["views"] == int(ref["views"].sum()) == n * 100
+
+
+@pytest.mark.gpu
+def test_chunked_hash_pass(monkeypatch):
+    """Heights hashed in chunks (the suffix rows of every height would exceed the 2 GiB per row-table set
+    for large batches): chunks of 7 and 1 heights, each chunk's chains starting from the previous chunk's
+    last hash, pipelined and not, against the oracle."""
+    from bftsim.configs import cfg2
+    monkeypatch.setenv("BFTSIM_TESTING", "1")
+    for cfg, rows, depth in ((cfg3(heights=30), "7", 0), (cfg3(heights=30), "7", 3), (cfg3(heights=30), "1", 3),
+                             (cfg2(heights=30), "7", 0), (cfg2(heights=30), "1", 3)):
+        # cfg3: the FAST kernel (suffix rows by a thread per (instance, height)); cfg2: the general kernel
+        # (a thread per instance over the chunk's heights)
+        monkeypatch.setenv("BFTSIM_SFX_ROWS", rows)
+        if True:
+            sim = _sim(cfg)
+            try:
+                if depth:
+                    sim.set_pipeline(True, depth)
+                sim.prepare(96)
+                for _ in range(2):
+                    sim.launch(0)
+                got = sim.fetch()
+            finally:
+                sim.close()
+            assert_same(O.run(cfg, 0, 96), got, f"chunk rows {rows} depth {depth}")
