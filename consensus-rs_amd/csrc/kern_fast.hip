@@ -1,5 +1,5 @@
 // kern_fast.hip — the N = 64 FAST consensus kernel (bft_fast64.h) and the block-hash pass
-// (bft_hash_pair_kernel) of the benchmark workload.
+// (bft_hash_suffix_kernel / bft_hash_suffix_loop_kernel + bft_hash_chain_kernel) of the benchmark workload.
 #include "bft_hip.h"
 #include "bft_fast64.h"
 
@@ -102,7 +102,8 @@ __device__ inline void keccak_f1600_pair(uint32_t X[25], uint32_t odd) {
 // The pass is split in two kernels so that the sequential chains carry only what chains: prev_hash.
 // 1. bft_hash_suffix_kernel, one thread per (instance, height): the header bytes after prev_hash
 //    (proposer address, the seeded tx_hash's two Philox draws, height, time, ...) into a suffix row
-//    (bft_common.h header_suffix). Fully parallel: it fills the chip and overlaps the consensus waves.
+//    (bft_common.h header_suffix_strided). Fully parallel: a short full-chip pass (bftsim.hip decides
+//    where it runs; beside long general kernels, bft_hash_suffix_loop_kernel: a thread per instance).
 // 2. bft_hash_chain_kernel, a lane pair per instance: per height, encode prev_hash (36..68 bytes), splice
 //    the suffix behind it with one v_alignbyte per message dword (splice_word; the suffix row is in LDS,
 //    loaded one height ahead), absorb, permute. Both lanes used to run the whole encoder.
