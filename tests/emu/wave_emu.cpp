@@ -492,6 +492,13 @@ extern "C" int emu_splice_check(uint32_t trials, uint64_t seed) {
         bft::header_suffix((uint64_t*)sfx, addr.data() + 20u * prop, s, inst, h, prop, var, time);
         bft::spliced_block_hash(sfx, prev, b);
         if (memcmp(a, b, 32) != 0) ++bad;
+        // the device layout (dword k of the row at k * stride): the same body and length
+        uint32_t strided[bft::SFX_DEV_DW * 3];
+        for (auto& v : strided) v = 0xdeadbeefu;
+        const uint32_t ls = bft::header_suffix_strided(strided + 1, 3, addr.data() + 20u * prop, s, inst, h, prop, var, time);
+        bool same = ls == sfx[bft::SFX_LEN_DW] && strided[1 + 3 * bft::SFX_DEV_LEN_DW] == ls;
+        for (uint32_t k = 0; k < bft::SFX_BODY_DW; ++k) same = same && strided[1 + 3 * k] == sfx[k];
+        if (!same) ++bad;
     }
     return bad;
 }

@@ -123,7 +123,8 @@ def test_full_kernel_alone_n64(name, mk, monkeypatch):
 def test_block_hash_splice_matches_one_piece_encoder():
     """The block-hash pass encodes every height's header suffix in one parallel kernel and splices
     prev_hash in front in the chain (kern_fast.hip, bft_common.h header_suffix / splice_word). The
-    splice equals the one-piece encoder of the header (SPEC.md §7) for random headers, including parents
+    splice equals the one-piece encoder of the header (SPEC.md §7) for random headers (and the device
+    rows, dword-major across instances, hold the same dwords), including parents
     of all-high and all-low bytes (prefix 68 and 36 bytes, so 2- and 3-block messages) and heights /
     times at every MessagePack width boundary."""
     import ctypes
