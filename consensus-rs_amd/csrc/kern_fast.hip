@@ -147,12 +147,6 @@ __global__ __launch_bounds__(64) void bft_hash_chain_kernel(Params p) {
     const uint32_t odd = threadIdx.x & 1u, pair = threadIdx.x >> 1;
     const uint32_t il = blockIdx.x * 32u + pair;
     if (il >= p.n_instances) return;                  // both lanes of a pair leave together
-#ifndef BFT_CHAIN_PRIO_BELOW
-#define BFT_CHAIN_PRIO_BELOW 6144   // gpurun r03mn: 2,048 per GPU 1.63e8 -> 2.0e8, 4,096 2.94e8 -> 3.38e8, 8,192 unchanged
-#endif
-    // small shards are bound by the chains' issue latency, not by the consensus kernels beside them: the
-    // chains outrank them (large shards: the consensus kernels are the critical path and keep priority 2)
-    if (p.n_instances < BFT_CHAIN_PRIO_BELOW) __builtin_amdgcn_s_setprio(3);
     const uint32_t K = p.sfx_rows, x0 = p.sfx_x0;
     const uint32_t ch = p.committed_height[il];
     const uint32_t x1 = ch < x0 + K - 1u ? ch : x0 + K - 1u;
