@@ -175,6 +175,65 @@ def host_cpu() -> str:
     return f"{model} ({usable_cpus()} usable CPUs)"
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` without an external launcher (no WORLD_SIZE in the environment): start N rank processes of
+    this same command, one per GPU, the way torch.distributed.run would (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT), and wait for them. This process never imports
+    torch or touches HIP: the ranks are fresh children, not an exec of a process that initialised the GPU.
+    Rank 0 writes the one JSON line on this process's stdout; the other ranks' stdout goes to stderr. If any
+    rank fails, the others are stopped (they may be blocked in a collective with it) and its exit code is
+    returned. The reference's counterpart is its multi-process cluster launch (build.sh:7-13)."""
+    import signal
+    port = _free_port()
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), BFTSIM_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen(cmd, env=env, stdout=None if r == 0 else sys.stderr.fileno()))
+    if os.environ.get("BFTSIM_TESTING") == "1" and os.environ.get("BFTSIM_BENCH_STUB_DIR"):
+        with open(os.path.join(os.environ["BFTSIM_BENCH_STUB_DIR"], "parent.json"), "w") as f:
+            json.dump({"pids": [p.pid for p in procs], "gpu_modules": sorted(
+                m for m in sys.modules if m == "torch" or m.startswith("torch.") or m.startswith("bftsim"))}, f)
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:                       # peers may wait forever in a collective with it
+                    q.send_signal(signal.SIGTERM)
+        if live:
+            time.sleep(0.05)
+    return rc
+
+
+def stub_rank(args) -> None:
+    """BFTSIM_TESTING stub of a rank (tests/test_bench_launcher.py): records its environment, prints the
+    JSON line shape of rank 0 with n_gpus from WORLD_SIZE; touches no GPU."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+    with open(os.path.join(os.environ["BFTSIM_BENCH_STUB_DIR"], f"rank{rank}.json"), "w") as f:
+        json.dump({k: os.environ.get(k) for k in keys} | {"pid": os.getpid(), "ppid": os.getppid()}, f)
+    if os.environ.get("BFTSIM_BENCH_STUB_FAIL") == str(rank):
+        sys.exit(3)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": 0.0, "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "data": "stub"}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -200,10 +259,19 @@ def main():
                          "cfg2-byz = 1, cfg5-byz = 2)")
     ap.add_argument("--seed-order", choices=("be", "le"), default="be",
                     help="U128 byte order of randon_seed (validator.rs:39-48; include/bftsim.h BFTSIM_SEED_*)")
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
-                    help="weak: --instances per GPU; strong: --instances in total, split over the ranks "
-                         "(BASELINE configs[2]: 16,384 sharded over 1/2/4/8 GPUs)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default=None,
+                    help="weak: --instances per GPU; strong: --instances in total, split over the ranks. Default: "
+                         "strong for cfg3 (BASELINE configs[2]: 16,384 sharded over 1/2/4/8 GPUs; at N > 1 the "
+                         "weak number, 16,384 per GPU, is measured too and reported in config.weak), weak for the "
+                         "other workloads")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))           # before anything touches the GPU
+    if os.environ.get("BFTSIM_TESTING") == "1" and os.environ.get("BFTSIM_BENCH_STUB_DIR"):
+        return stub_rank(args)
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']} from the launcher; "
+              "using WORLD_SIZE", file=sys.stderr)
     if args.workload == "sig":
         return main_sig(args)
     if args.workload == "wire":
@@ -251,6 +319,8 @@ def main():
         cfg = dataclasses.replace(cfg, seed_byte_order=1, name=cfg.name + "-le")
     sim = Simulator(cfg, device=local)
     pipelined = not c5 and not args.no_pipeline
+    if args.scaling is None:
+        args.scaling = "strong" if wl == "cfg3" else "weak"
     if args.scaling == "strong":
         from bftsim.distributed import strong_shard
         first, I = strong_shard(rank, world, args.instances)
@@ -262,6 +332,22 @@ def main():
         sim.set_window(args.window)
     sim.prepare(I)
     stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def timed_steps(first_id):
+        """K launches between two barriers + device synchronisations; the max over ranks (s)"""
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            sim.launch(first_id, stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        tmax = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        return float(tmax.item())
 
     for _ in range(args.warmup):
         sim.launch(first, stream)
@@ -285,27 +371,31 @@ def main():
     views_all, heights_all = tot["views"], tot["committed_heights"]
     safety_all, timeout_all = tot["flagged"][0], tot["flagged"][4]
 
-    if world > 1:
-        dist.barrier()
     torch.cuda.synchronize(dev)
     sim.kernel_ms_sum()                   # drop the warmup launches
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        sim.launch(first, stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    tmax = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    dt = float(tmax.item())
+    dt = timed_steps(first)
 
     ms_step = 1000.0 * dt / args.steps
     value = views_all * args.steps / dt
     cms_sum, hms_sum, nl = sim.kernel_ms_sum()    # HIP events around every launch of the timed region
     cms = cms_sum / max(nl, 1)
     hms = hms_sum / max(nl, 1)
+
+    # the weak counterpart of a multi-GPU strong headline: --instances per GPU on every rank, same K / W
+    weak = None
+    if args.scaling == "strong" and world > 1:
+        Iw, first_w = args.instances, rank * args.instances
+        sim.prepare(Iw)
+        for _ in range(max(args.warmup, 1)):
+            sim.launch(first_w, stream)
+        torch.cuda.synchronize(dev)
+        vw = torch.tensor([sim.stats()["views"]], dtype=torch.int64, device=dev)
+        dist.all_reduce(vw)
+        dtw = timed_steps(first_w)
+        weak = {"value": int(vw.item()) * args.steps / dtw, "instances_per_gpu": Iw,
+                "instances_total": Iw * world, "ms_per_step": 1000.0 * dtw / args.steps,
+                "instance_rounds_per_step": int(vw.item()), "scaling": "weak"}
+        sim.kernel_ms_sum()
 
     if rank == 0:
         views_rank = st["views"]
@@ -348,10 +438,13 @@ def main():
             "config": {
                 "workload": (f"{cfg.name}: {I} instances per GPU, {cfg_desc(cfg)}, {args.heights} heights, "
                              f"window {args.window}") if c5 else
-                            (f"{wl}: {I} instances per GPU, {cfg_desc(cfg)}, {args.heights} heights" +
+                            ((f"{wl}: {args.instances} instances sharded over {world} GPU(s) ({I} on rank 0)"
+                              if args.scaling == "strong" else f"{wl}: {I} instances per GPU") +
+                             f", {cfg_desc(cfg)}, {args.heights} heights" +
                              (", little-endian U128 seeds" if cfg.seed_byte_order else "")),
                 "instances_per_gpu": I, "n_validators": cfg.n, "byzantine": cfg.byz_count,
                 "instances_total": args.instances if args.scaling == "strong" else args.instances * world,
+                "weak": weak,
                 "seed_byte_order": "le" if cfg.seed_byte_order else "be",
                 "heights": args.heights, "parallelism": f"instance-sharded x{world}",
                 "pipelined": pipelined, "pipeline_depth": args.pipeline_depth if pipelined else 0,
@@ -396,7 +489,7 @@ def main():
                              "hash 14976 lane-ops per header (SURVEY.md 8d)",
             },
         }
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:    # the CPU leg: rank 0 at N = 1 only
             try:
                 out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample, usable_cpus(), args.workload)
             except Exception as e:  # the baseline is reported, never the target

@@ -24,7 +24,7 @@ class CConfig(ctypes.Structure):
 class CResult(ctypes.Structure):
     _fields_ = [(k, ctypes.c_void_p) for k in (
         "committed_height", "flags", "ticks", "views", "round", "proposer", "variant",
-        "time_tick", "block_hash")]
+        "time_tick", "block_hash")] + [("capacity", ctypes.c_uint64)]
 
 
 class CStats(ctypes.Structure):
@@ -70,6 +70,7 @@ def alloc_result(n_inst: int, heights: int):
     r = CResult()
     for k, a in arrs.items():
         setattr(r, k, a.ctypes.data)
+    r.capacity = n_inst
     return r, arrs
 
 

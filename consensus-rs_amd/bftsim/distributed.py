@@ -45,39 +45,60 @@ def all_reduce_stats(st: Dict, device=None) -> Dict:
     return out
 
 
+def _agree(ok: bool, multi: bool) -> bool:
+    """MIN over the ranks of the default group (every rank calls it, whatever it holds)."""
+    if not multi:
+        return ok
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else None
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return bool(flag.item())
+
+
 def capi_comm_init(sim, rank: int, world: int) -> bool:
     """Join `sim` to the node's RCCL communicator of libbftsim (bftsim_comm_init): rank 0 makes the id,
     the default torch.distributed group carries it to the other ranks (any channel would do).
 
     Collective and all-or-nothing: every rank returns the same answer, True only if every rank joined.
-    Rank 0 broadcasts a failure marker instead of the id when it cannot make one, and the ranks agree on
-    their join results with one MIN all-reduce, so no rank is left waiting in a collective that the
-    others skipped (they then all take the torch.distributed fallback of all_reduce_stats)."""
-    import torch
+    ncclCommInitRank blocks until all ranks have joined, so no rank may enter it unless every rank will:
+      1. pre-flight: each rank checks that librccl opens (bftsim_comm_available); one MIN all-reduce;
+      2. rank 0 makes the id and broadcasts it, or a failure marker that every rank sees;
+      3. only then does every rank call comm_init; one more MIN all-reduce agrees on the result.
+    A rank that cannot open the library therefore fails in step 1, before anyone blocks in step 3. What
+    the pre-flight cannot see (ncclCommInitRank itself failing on one rank after the others entered it)
+    is RCCL's own bootstrap error path. On any failure all ranks take the torch.distributed fallback of
+    all_reduce_stats."""
     import torch.distributed as dist
     multi = world > 1 and dist.is_available() and dist.is_initialized()
-    uid, why = None, ""
+    why = ""
+    try:
+        sim.comm_available()
+        ok = True
+    except Exception as e:                         # noqa: BLE001 — reported by the caller
+        ok, why = False, str(e)
+    if not _agree(ok, multi):
+        sim.comm_error = why or "another rank cannot open librccl (bftsim_comm_available)"
+        return False
+    uid = None
     if rank == 0:
         try:
             uid = sim.comm_unique_id()
-        except Exception as e:                     # noqa: BLE001 — reported by the caller
+        except Exception as e:                     # noqa: BLE001
             why = str(e)
     box = [uid]
     if multi:
         dist.broadcast_object_list(box, src=0)
-    ok = box[0] is not None
-    if ok:
-        try:
-            sim.comm_init(world, rank, box[0])
-        except Exception as e:                     # noqa: BLE001
-            ok, why = False, str(e)
-    if multi:
-        dev = None
-        if dist.get_backend() == "nccl":
-            dev = torch.device("cuda", torch.cuda.current_device())
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        ok = bool(flag.item())
+    if box[0] is None:                             # every rank sees the marker: nobody joins
+        sim.comm_error = why or "rank 0 could not make the RCCL id"
+        return False
+    ok = True
+    try:
+        sim.comm_init(world, rank, box[0])
+    except Exception as e:                         # noqa: BLE001
+        ok, why = False, str(e)
+    ok = _agree(ok, multi)
     sim.comm_error = why
     return ok
 

@@ -58,9 +58,12 @@ def lib():
         L.bftsim_set_crypto.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32]
         L.bftsim_ledger_slot_bytes.argtypes = [ctypes.c_uint32]
         L.bftsim_ledger_slot_bytes.restype = ctypes.c_uint64
-        L.bftsim_export_ledger.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
-        L.bftsim_crypto_verify.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.CCryptoReport), ctypes.c_void_p,
+        L.bftsim_export_ledger.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
                                            ctypes.c_void_p]
+        L.bftsim_crypto_verify.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.CCryptoReport), ctypes.c_uint64,
+                                           ctypes.c_void_p, ctypes.c_void_p]
+        L.bftsim_launched_count.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                            ctypes.POINTER(ctypes.c_uint64)]
         L.bftsim_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
         L.bftsim_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
                                             ctypes.POINTER(ctypes.c_float)]
@@ -72,7 +75,7 @@ def lib():
         L.bftsim_set_window.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         if hasattr(L, "bftsim_set_rcs_capacity"):     # (absent from A/B builds of earlier rounds)
             L.bftsim_set_rcs_capacity.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
-        L.bftsim_fetch_summary.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 5
+        L.bftsim_fetch_summary.argtypes = [ctypes.c_void_p, ctypes.c_uint64] + [ctypes.c_void_p] * 5
         L.bftsim_two_thirds_majority.restype = ctypes.c_uint32
         L.bftsim_seed_from_hash.restype = ctypes.c_uint32
         L.bftsim_seed_from_hash.argtypes = [ctypes.c_char_p, ctypes.c_uint32]
@@ -84,7 +87,7 @@ def lib():
         L.bftsim_keccak256.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p]
         L.bftsim_genesis_hash.argtypes = [ctypes.POINTER(_abi.CConfig), ctypes.c_void_p]
         L.bftsim_view_cmp.argtypes = [ctypes.c_uint64] * 4
-        L.bftsim_export_headers.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.bftsim_export_headers.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -155,13 +158,23 @@ class Simulator:
         overflowing batch at twice the capacity."""
         _check(self.h, lib().bftsim_set_rcs_capacity(self.h, rounds), "bftsim_set_rcs_capacity")
 
-    def fetch_summary(self, n: int, tips: bool = True):
+    def launched(self):
+        """(first, n) of the last launch: the rows the fetch family writes (bftsim_launched_count)."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self.h, lib().bftsim_launched_count(self.h, ctypes.byref(a), ctypes.byref(b)), "bftsim_launched_count")
+        return a.value, b.value
+
+    def fetch_summary(self, n: int = None, tips: bool = True):
+        """Per-instance outputs of the last launch into buffers of `n` instances (default: the launched
+        count; a smaller n is refused by the library, bftsim.h)."""
+        if n is None:
+            n = self.launched()[1]
         out = dict(committed_height=np.zeros(n, np.uint64), flags=np.zeros(n, np.uint32),
                    ticks=np.zeros(n, np.uint32), views=np.zeros(n, np.uint64))
         if tips:
             out["tip_hash"] = np.zeros((n, 32), np.uint8)
         _check(self.h, lib().bftsim_fetch_summary(
-            self.h, out["committed_height"].ctypes.data, out["flags"].ctypes.data, out["ticks"].ctypes.data,
+            self.h, n, out["committed_height"].ctypes.data, out["flags"].ctypes.data, out["ticks"].ctypes.data,
             out["views"].ctypes.data, out["tip_hash"].ctypes.data if tips else None), "bftsim_fetch_summary")
         return out
 
@@ -193,14 +206,17 @@ class Simulator:
         _check(self.h, lib().bftsim_fetch(self.h, ctypes.byref(r)), "bftsim_fetch")
         return _abi.shape_result(arrs, n, self.cfg.heights)
 
-    def export_headers(self, n: int):
+    def export_headers(self, n: int = None):
         """Ledger export of the last run / launch (core/ledger.rs:193-245): ([n, H] list of the Header
         bytes of every committed height, empty beyond it). Keccak-256 of each is its block hash."""
+        if n is None:
+            n = self.launched()[1]
         H = self.cfg.heights
         slot = HEADER_SLOT
         buf = np.zeros(n * H * slot, np.uint8)
         lens = np.zeros(n * H, np.uint32)
-        _check(self.h, lib().bftsim_export_headers(self.h, buf.ctypes.data, lens.ctypes.data), "bftsim_export_headers")
+        _check(self.h, lib().bftsim_export_headers(self.h, n, buf.ctypes.data, lens.ctypes.data),
+               "bftsim_export_headers")
         buf = buf.reshape(n, H, slot)
         lens = lens.reshape(n, H)
         return [[bytes(buf[i, x, :lens[i, x]]) for x in range(H)] for i in range(n)]
@@ -258,7 +274,7 @@ class Simulator:
         rep = _abi.CCryptoReport()
         ck = np.zeros((n, 32), np.uint8)
         cnt = np.zeros(n, np.uint32)
-        _check(self.h, lib().bftsim_crypto_verify(self.h, ctypes.byref(rep), ck.ctypes.data, cnt.ctypes.data),
+        _check(self.h, lib().bftsim_crypto_verify(self.h, ctypes.byref(rep), n, ck.ctypes.data, cnt.ctypes.data),
                "bftsim_crypto_verify")
         out = {k: getattr(rep, k) for k, _ in _abi.CCryptoReport._fields_}
         out["checksum"], out["inst_messages"] = ck, cnt
@@ -271,7 +287,7 @@ class Simulator:
         slot = lib().bftsim_ledger_slot_bytes(self.cfg.n)
         buf = np.zeros(n * H * slot, np.uint8)
         lens = np.zeros(n * H, np.uint32)
-        _check(self.h, lib().bftsim_export_ledger(self.h, buf.ctypes.data, slot, lens.ctypes.data),
+        _check(self.h, lib().bftsim_export_ledger(self.h, n, buf.ctypes.data, slot, lens.ctypes.data),
                "bftsim_export_ledger")
         out = []
         for i in range(n):
@@ -284,6 +300,14 @@ class Simulator:
                 row.append(bytes(buf[o:o + k]))
             out.append(row)
         return out
+
+    @staticmethod
+    def comm_available():
+        """raises unless librccl opens with every entry point libbftsim uses (bftsim_comm_available): the
+        pre-flight each rank runs, and the ranks agree on, before any of them enters ncclCommInitRank"""
+        rc = lib().bftsim_comm_available()
+        if rc != 0:
+            raise BftsimError(f"bftsim_comm_available failed ({rc}): librccl.so.1 cannot be opened")
 
     @staticmethod
     def comm_unique_id() -> bytes:

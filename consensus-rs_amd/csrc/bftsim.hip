@@ -969,10 +969,27 @@ int bftsim_last_kernel_ms(bftsim_t* h, float* cms, float* hms) {
     return BFTSIM_OK;
 }
 
+// the fetch family writes one row per launched instance into caller buffers: refuse a short buffer
+// before anything is written (include/bftsim.h bftsim_launched_count)
+static int check_launched(bftsim* h, uint64_t capacity, const char* what) {
+    if (h->last_n == 0 || !h->d_ch) return fail(h, BFTSIM_EINVAL, std::string(what) + ": nothing launched");
+    if (capacity < h->last_n)
+        return fail(h, BFTSIM_EINVAL, std::string(what) + ": buffers hold " + std::to_string(capacity) +
+                                          " instances, the last launch has " + std::to_string(h->last_n));
+    return BFTSIM_OK;
+}
+
+int bftsim_launched_count(bftsim_t* h, uint64_t* first, uint64_t* n) {
+    if (!h) return BFTSIM_EINVAL;
+    if (first) *first = h->last_n ? h->last_first : 0;
+    if (n) *n = h->d_ch ? h->last_n : 0;
+    return BFTSIM_OK;
+}
+
 int bftsim_fetch(bftsim_t* h, bftsim_result* out) {
     if (!h || !out) return BFTSIM_EINVAL;
     if (h->window) return fail(h, BFTSIM_EINVAL, "windowed run: per-height rows are not kept (bftsim_fetch_summary)");
-    if (h->last_n == 0 || !h->d_ch) return fail(h, BFTSIM_EINVAL, "nothing launched");
+    if (int rc = check_launched(h, out->capacity, "bftsim_fetch")) return rc;
     if (int rc = sync_all(h)) return rc;
     uint64_t n = h->last_n;
     uint32_t H = h->cfg.heights, hc = h->hcap;
@@ -1007,10 +1024,10 @@ int bftsim_fetch(bftsim_t* h, bftsim_result* out) {
     return BFTSIM_OK;
 }
 
-int bftsim_export_headers(bftsim_t* h, uint8_t* hdr, uint32_t* hdr_len) {
+int bftsim_export_headers(bftsim_t* h, uint64_t capacity, uint8_t* hdr, uint32_t* hdr_len) {
     if (!h || !hdr || !hdr_len) return BFTSIM_EINVAL;
     if (h->window) return fail(h, BFTSIM_EINVAL, "windowed run: per-height rows are not kept");
-    if (h->last_n == 0 || !h->d_ch) return fail(h, BFTSIM_EINVAL, "nothing launched");
+    if (int rc = check_launched(h, capacity, "bftsim_export_headers")) return rc;
     if (int rc = sync_all(h)) return rc;
     const uint64_t n = h->last_n, H = h->cfg.heights, cnt = n * H;
     bft::Params p = make_params(h, h->last_first, n);
@@ -1032,6 +1049,9 @@ int bftsim_export_headers(bftsim_t* h, uint8_t* hdr, uint32_t* hdr_len) {
 
 int bftsim_run(bftsim_t* h, uint64_t first, uint64_t n, bftsim_result* out) {
     if (!h || !out) return BFTSIM_EINVAL;
+    if (out->capacity < n)
+        return fail(h, BFTSIM_EINVAL, "bftsim_run: result buffers hold " + std::to_string(out->capacity) +
+                                          " instances, " + std::to_string(n) + " requested");
     for (;;) {
         int rc = bftsim_prepare(h, n);
         if (rc) return rc;
@@ -1042,15 +1062,21 @@ int bftsim_run(bftsim_t* h, uint64_t first, uint64_t n, bftsim_result* out) {
         bool over = false;
         for (uint64_t i = 0; i < n && !over; ++i) over = (out->flags[i] & BFTSIM_FLAG_RCS_OVERFLOW) != 0;
         if (!over || h->rcs_k >= bft::RCS_MAX_K) return BFTSIM_OK;
-        const uint32_t k = 2u * h->rcs_k;
-        if ((rc = bftsim_set_rcs_capacity(h, k < bft::RCS_MAX_K ? k : bft::RCS_MAX_K))) return rc;
+        const uint32_t k = 2u * h->rcs_k < bft::RCS_MAX_K ? 2u * h->rcs_k : bft::RCS_MAX_K;
+        // the larger tables must fit beside everything else, or the flagged results stand (bftsim.h)
+        const uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg, blocks = (n + per_block - 1) / per_block;
+        const uint64_t grow = blocks * (bft::rcs_words(h->seg, k) - bft::rcs_words(h->seg, h->rcs_k)) * 4;
+        size_t free_b = 0, total_b = 0;
+        HIPCHECK(h, hipMemGetInfo(&free_b, &total_b));
+        if (grow > free_b / 10 * 9) return BFTSIM_OK;
+        if ((rc = bftsim_set_rcs_capacity(h, k))) return rc;
     }
 }
 
-int bftsim_fetch_summary(bftsim_t* h, uint64_t* committed_height, uint32_t* flags, uint32_t* ticks,
+int bftsim_fetch_summary(bftsim_t* h, uint64_t capacity, uint64_t* committed_height, uint32_t* flags, uint32_t* ticks,
                          uint64_t* views, uint8_t* tip_hash) {
     if (!h) return BFTSIM_EINVAL;
-    if (h->last_n == 0 || !h->d_ch) return fail(h, BFTSIM_EINVAL, "nothing launched");
+    if (int rc = check_launched(h, capacity, "bftsim_fetch_summary")) return rc;
     if (int rc = sync_all(h)) return rc;                // the hash pass may run on its own stream
     uint64_t n = h->last_n;
     if (tip_hash) {
@@ -1070,6 +1096,11 @@ int bftsim_fetch_summary(bftsim_t* h, uint64_t* committed_height, uint32_t* flag
     if (views) HIPCHECK(h, hipMemcpy(views, h->d_views, n * 8, hipMemcpyDeviceToHost));
     if (tip_hash) HIPCHECK(h, hipMemcpy(tip_hash, h->d_tips, n * 32, hipMemcpyDeviceToHost));
     return BFTSIM_OK;
+}
+
+int bftsim_comm_available(void) {
+    Rccl& r = rccl();
+    return r.ok ? BFTSIM_OK : BFTSIM_EUNSUPPORTED;
 }
 
 int bftsim_comm_unique_id(uint8_t out[128]) {
@@ -1176,10 +1207,13 @@ int bftsim_set_crypto(bftsim_t* h, const uint8_t* secrets32, const uint8_t* forg
     return BFTSIM_OK;
 }
 
-int bftsim_crypto_verify(bftsim_t* h, bftsim_crypto_report* out, uint8_t* inst_checksum, uint32_t* inst_messages) {
+int bftsim_crypto_verify(bftsim_t* h, bftsim_crypto_report* out, uint64_t capacity, uint8_t* inst_checksum,
+                         uint32_t* inst_messages) {
     if (!h || !out) return BFTSIM_EINVAL;
     if (!h->crypto) return fail(h, BFTSIM_EINVAL, "bftsim_set_crypto not called");
     if (h->last_n == 0 || !h->d_mlog) return fail(h, BFTSIM_EINVAL, "nothing launched");
+    if (inst_checksum || inst_messages)
+        if (int rc = check_launched(h, capacity, "bftsim_crypto_verify")) return rc;
     if (int rc = sync_all(h)) return rc;
     SigApi& sa = sig_api();
     const uint64_t n = h->last_n;
@@ -1279,10 +1313,11 @@ int bftsim_crypto_verify(bftsim_t* h, bftsim_crypto_report* out, uint8_t* inst_c
     return BFTSIM_OK;
 }
 
-int bftsim_export_ledger(bftsim_t* h, uint8_t* hdr, uint64_t slot_bytes, uint32_t* hdr_len) {
+int bftsim_export_ledger(bftsim_t* h, uint64_t capacity, uint8_t* hdr, uint64_t slot_bytes, uint32_t* hdr_len) {
     if (!h || !hdr || !hdr_len) return BFTSIM_EINVAL;
     if (!h->crypto || h->vsig_n == 0 || h->vsig_n != h->last_n)
         return fail(h, BFTSIM_EINVAL, "no votes: bftsim_crypto_verify after the launch first");
+    if (int rc = check_launched(h, capacity, "bftsim_export_ledger")) return rc;
     if (slot_bytes < bftsim_ledger_slot_bytes(h->cfg.n)) return fail(h, BFTSIM_EINVAL, "slot_bytes too small");
     if (int rc = sync_all(h)) return rc;
     const uint64_t n = h->last_n, H = h->cfg.heights, cnt = n * H;

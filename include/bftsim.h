@@ -91,6 +91,9 @@ typedef struct bftsim_result {   /* host buffers, caller-owned; H = config.heigh
     uint8_t *variant;            /* [n_inst*H] 1 = the equivocated second block */
     uint32_t *time_tick;         /* [n_inst*H] header.time = genesis + period*(tick+1) */
     uint8_t *block_hash;         /* [n_inst*H*32] Keccak-256 of the header (block.rs:76-80) */
+    uint64_t capacity;           /* instances the buffers above hold: at least the instances the call
+                                    writes (bftsim_run's n, bftsim_launched_count's n), else the call
+                                    fails with BFTSIM_EINVAL and writes nothing */
 } bftsim_result;
 
 typedef struct bftsim_stats {    /* summed over the instances of the last launch */
@@ -119,6 +122,12 @@ int bftsim_prepare(bftsim_t *h, uint64_t n_instances);
 int bftsim_launch(bftsim_t *h, uint64_t first_instance, void *hip_stream);   /* async */
 int bftsim_sync(bftsim_t *h);
 int bftsim_fetch(bftsim_t *h, bftsim_result *out);
+/* the instance range of the last launch [first, first + n): the count bftsim_fetch, _fetch_summary,
+ * _export_headers, _export_ledger and _crypto_verify write per-instance rows for (n = 0: nothing launched).
+ * Every one of those takes the capacity of the caller's buffers (in instances) and refuses a short one
+ * with BFTSIM_EINVAL before writing anything (the reference's Result-returning boundary,
+ * src/consensus/backend.rs:45-68) */
+int bftsim_launched_count(bftsim_t *h, uint64_t *first_instance, uint64_t *n_instances);
 int bftsim_stats_get(bftsim_t *h, bftsim_stats *out);   /* device reduction + copy */
 /* multi-GPU (one process per GPU): the instances shard over the ranks with no data-path
  * collective; the statistics of every rank are summed by one RCCL all-reduce over xGMI. Rank 0 makes
@@ -126,6 +135,11 @@ int bftsim_stats_get(bftsim_t *h, bftsim_stats *out);   /* device reduction + co
  * then joins with its handle. Replaces the per-node Engine of create_bft_engine
  * (src/consensus/consensus.rs:42-60) with one engine per device and a node-wide statistic.
  * BFTSIM_EUNSUPPORTED when librccl.so.1 cannot be opened. */
+/* 0 when librccl.so.1 opens with every entry point this library uses, else BFTSIM_EUNSUPPORTED. Every rank
+ * calls it and the ranks agree on the answer (any channel) BEFORE any of them calls bftsim_comm_init:
+ * ncclCommInitRank blocks until every rank has joined, so a rank that could not even open the library
+ * would leave the others waiting there (bftsim/distributed.py capi_comm_init). */
+int bftsim_comm_available(void);
 int bftsim_comm_unique_id(uint8_t unique_id[128]);
 int bftsim_comm_init(bftsim_t *h, int world_size, int rank, const uint8_t unique_id[128]);
 /* bftsim_stats of the last launch summed over every rank (collective: every rank calls it) */
@@ -158,11 +172,15 @@ int bftsim_set_window(bftsim_t *h, uint32_t window);
  * set (the reference's HashMap<u64, MessageManage>, round_change_set.rs:11-35, is unbounded).
  * 1..4096, default 16. A validator needing more sets BFTSIM_FLAG_RCS_OVERFLOW on its instance;
  * bftsim_run then re-runs the batch at twice the capacity until no instance overflows (instances are
- * independent and deterministic, so the others are unchanged). Takes effect at the next bftsim_prepare. */
+ * independent and deterministic, so the others are unchanged), as long as the doubled tables fit in 90 %
+ * of the free device memory; otherwise it returns BFTSIM_OK with the flagged results. The grown capacity
+ * stays in effect for later prepare / launch / run calls, with tables proportional to it (set it back
+ * with this call). Takes effect at the next bftsim_prepare. */
 int bftsim_set_rcs_capacity(bftsim_t *h, uint32_t rounds);
-/* per-instance outputs of the last launch (any pointer may be NULL); tip_hash[i*32..] = hash of
+/* per-instance outputs of the last launch (any pointer may be NULL; capacity = instances each
+ * buffer holds); tip_hash[i*32..] = hash of
  * the block at committed_height[i] (the genesis hash at 0), which commits to the whole chain */
-int bftsim_fetch_summary(bftsim_t *h, uint64_t *committed_height, uint32_t *flags, uint32_t *ticks,
+int bftsim_fetch_summary(bftsim_t *h, uint64_t capacity, uint64_t *committed_height, uint32_t *flags, uint32_t *ticks,
                          uint64_t *views, uint8_t *tip_hash);
 
 /* real-crypto mode (SPEC.md §11). Every consensus message the simulation
@@ -191,10 +209,12 @@ typedef struct bftsim_crypto_report {
     uint64_t log_overflows;        /* instances whose log exceeded log_cap (then the call fails) */
 } bftsim_crypto_report;
 int bftsim_set_crypto(bftsim_t *h, const uint8_t *secrets32, const uint8_t *forged, uint32_t log_cap);
-/* after a launch: the sign / recover pass of its messages; inst_checksum (host, n x 32, nullable) =
+/* after a launch: the sign / recover pass of its messages; capacity = instances inst_checksum and
+ * inst_messages hold (checked when either is non-NULL); inst_checksum (host, n x 32, nullable) =
  * per instance the XOR over its messages of keccak256(signature || seal or 65 zero bytes);
  * inst_messages (host, n, nullable) = messages per instance */
-int bftsim_crypto_verify(bftsim_t *h, bftsim_crypto_report *out, uint8_t *inst_checksum, uint32_t *inst_messages);
+int bftsim_crypto_verify(bftsim_t *h, bftsim_crypto_report *out, uint64_t capacity, uint8_t *inst_checksum,
+                         uint32_t *inst_messages);
 
 /* the ledger with votes (real-crypto mode, after bftsim_crypto_verify): for every instance and height
  * x <= committed_height, in slot [i*H + x-1] of `slot_bytes` bytes, the Header that Backend::commit
@@ -204,7 +224,7 @@ int bftsim_crypto_verify(bftsim_t *h, bftsim_crypto_report *out, uint8_t *inst_c
  * block_hash of that height (block_hash() ignores votes, types/block.rs:76-80). Together with
  * block_hash per height this is the ledger's headers + block_hashes_by_height (store/schema.rs). */
 uint64_t bftsim_ledger_slot_bytes(uint32_t n_validators);
-int bftsim_export_ledger(bftsim_t *h, uint8_t *hdr, uint64_t slot_bytes, uint32_t *hdr_len);
+int bftsim_export_ledger(bftsim_t *h, uint64_t capacity, uint8_t *hdr, uint64_t slot_bytes, uint32_t *hdr_len);
 
 /* ValidatorSet / block helpers on the host (validator.rs, types/block.rs) */
 uint32_t bftsim_two_thirds_majority(uint32_t n);                    /* validator.rs:149-154 */
@@ -230,9 +250,10 @@ int bftsim_check_message(uint32_t code, uint64_t msg_height, uint64_t core_heigh
  * launch or run, the MessagePack Header bytes (SPEC.md §7, votes None: commit seals are not
  * modelled) of every committed height of the last launch, host buffers:
  * hdr[(i*H + x-1) * BFTSIM_HEADER_SLOT ...] with hdr_len[i*H + x-1] bytes (0 beyond the committed
- * height); Keccak-256 of those bytes is that height's block hash. */
+ * height); Keccak-256 of those bytes is that height's block hash. capacity = instances the buffers
+ * hold (hdr: capacity*H slots, hdr_len: capacity*H words). */
 #define BFTSIM_HEADER_SLOT 288
-int bftsim_export_headers(bftsim_t *h, uint8_t *hdr, uint32_t *hdr_len);
+int bftsim_export_headers(bftsim_t *h, uint64_t capacity, uint8_t *hdr, uint32_t *hdr_len);
 
 #ifdef __cplusplus
 }

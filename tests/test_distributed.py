@@ -67,9 +67,16 @@ def test_gloo_world2_stats_equal_single_process():
 
 
 class _FakeSim:
-    """stands in for Simulator in the comm-init decision: fails where told to"""
-    def __init__(self, fail_id, fail_init):
-        self.fail_id, self.fail_init, self.joined = fail_id, fail_init, False
+    """stands in for Simulator in the comm-init decision: fails where told to. comm_init behaves like
+    ncclCommInitRank: it returns only once every rank has entered it (a shared barrier), so a rank that
+    fails before entering leaves the others blocked there -- the hang the pre-flight must prevent."""
+    def __init__(self, fail_avail, fail_id, fail_init, barrier=None):
+        self.fail_avail, self.fail_id, self.fail_init, self.barrier = fail_avail, fail_id, fail_init, barrier
+        self.entered_init = False
+
+    def comm_available(self):
+        if self.fail_avail:
+            raise RuntimeError("no librccl")
 
     def comm_unique_id(self):
         if self.fail_id:
@@ -78,12 +85,16 @@ class _FakeSim:
 
     def comm_init(self, world, rank, uid):
         assert uid == bytes(128)
+        if self.fail_avail:                          # the old path: dlopen fails inside comm_init
+            raise RuntimeError("dlopen librccl.so.1 failed")
+        self.entered_init = True
+        if self.barrier is not None:
+            self.barrier.wait(timeout=20)            # threading.BrokenBarrierError = the old hang
         if self.fail_init:
             raise RuntimeError("init failed")
-        self.joined = True
 
 
-def _comm_worker(rank, world, port, q, fail_id, fail_init_rank):
+def _comm_worker(rank, world, port, q, fail_avail_rank, fail_id, fail_init_rank, barrier):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "consensus-rs_amd"))
@@ -92,23 +103,33 @@ def _comm_worker(rank, world, port, q, fail_id, fail_init_rank):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    ok = capi_comm_init(_FakeSim(fail_id and rank == 0, rank == fail_init_rank), rank, world)
-    q.put((rank, ok))
+    sim = _FakeSim(rank == fail_avail_rank, fail_id and rank == 0, rank == fail_init_rank, barrier)
+    try:
+        ok = capi_comm_init(sim, rank, world)
+    except Exception as e:                           # noqa: BLE001
+        ok = f"raised {type(e).__name__}"
+    q.put((rank, ok, sim.entered_init))
     dist.barrier()                                   # every rank reaches the same next collective
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fail_id,fail_init_rank,want", [(False, -1, True), (True, -1, False), (False, 1, False)])
-def test_comm_init_decision_is_collective(fail_id, fail_init_rank, want):
-    """bench.py's RCCL-or-fallback choice: a failure on any rank sends every rank to the same branch"""
+@pytest.mark.parametrize("fail_avail_rank,fail_id,fail_init_rank,want", [
+    (-1, False, -1, True), (-1, True, -1, False), (-1, False, 1, False), (1, False, -1, False), (0, False, -1, False)])
+def test_comm_init_decision_is_collective(fail_avail_rank, fail_id, fail_init_rank, want):
+    """bench.py's RCCL-or-fallback choice: a failure on any rank sends every rank to the same branch, and a
+    rank that cannot open librccl stops everyone before anyone blocks in the (blocking) join"""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
+    barrier = ctx.Barrier(2)
     port = _free_port()
-    procs = [ctx.Process(target=_comm_worker, args=(r, 2, port, q, fail_id, fail_init_rank)) for r in range(2)]
+    procs = [ctx.Process(target=_comm_worker, args=(r, 2, port, q, fail_avail_rank, fail_id, fail_init_rank, barrier))
+             for r in range(2)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=120) for _ in range(2))
+    got = {r: (ok, entered) for r, ok, entered in (q.get(timeout=120) for _ in range(2))}
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    assert got == {0: want, 1: want}
+    assert {r: ok for r, (ok, _) in got.items()} == {0: want, 1: want}
+    if fail_avail_rank >= 0 or fail_id:              # nobody entered the blocking join
+        assert not any(e for _, e in got.values())
