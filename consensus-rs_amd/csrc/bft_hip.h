@@ -206,7 +206,8 @@ hipError_t launch_fast(dim3 grid, hipStream_t s, const Params& p);              
 // (loop: a thread per instance over its heights instead of a thread per (instance, height))
 hipError_t launch_hash_suffix(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, bool loop, hipStream_t s,
                               Params p);
-hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, hipStream_t s, Params p);
+// `wave`: one wave per instance (bft_hash_chain_wave_kernel, small shards) instead of a lane pair
+hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, bool wave, hipStream_t s, Params p);
 hipError_t launch_resume(dim3 grid, size_t lds, hipStream_t s, const Params& p);  // kern_resume.hip
 
 }  // namespace bft

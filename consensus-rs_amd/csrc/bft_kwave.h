@@ -168,4 +168,68 @@ BFT_FN __attribute__((always_inline)) uint32_t kw50_header_hash(W& wv, uint32_t 
     return a;
 }
 
+// ---- the prev_hash chain of one instance by ONE wave (small shards: bft_hash_chain_wave_kernel) ----
+// The block-hash pass of a launch is a chain per instance, sequential in height (prev_hash). With few
+// instances per GPU the chains run one lone wave per SIMD, and a chain's latency is the launch's: the
+// lane-pair chain issues ~130 dependent VALU per Keccak round (~600 cycles for a lone wave). Here the 50
+// lanes of kw50_permute take one round in ~4 dependent ds_bpermute levels instead. Per height:
+//   * the suffix row (bft_hash_suffix_kernel, header bytes after prev_hash, loaded one height ahead) goes
+//     into the splice buffer `sb` at dword SFX_PAD, as the lane-pair chain's splice (bft_common.h);
+//   * the prefix (array header + prev_hash as MessagePack array16 of 32 uints, 36..68 bytes) is written
+//     byte-wise into `pf` by lanes 0..35: lane e < 32 owns prev_hash byte e (`0xcc b` for b >= 128, at
+//     4 + e + the count of such bytes below it: a ballot prefix count);
+//   * lane l < 34 absorbs message dword 34 blk + l = align_bytes of the splice buffer | the prefix dword.
+// `srow`: dword k of the first height's suffix row at srow[k * stride], height j at + j * rstride;
+// `a_prev`: lane l < 8 holds the parent's hash dword l; `hdst`: the first height's hash row (8 dwords),
+// height j at + 8 j. Same bytes as spliced_block_hash (tests/test_emu_parity.py: emu_wave_chain_check).
+constexpr uint32_t KW_PFX_DW = 18;
+template <class W>
+BFT_FN __attribute__((always_inline)) void kw50_chain(W& wv, uint32_t lane, uint32_t* sb, uint32_t* pf,
+                                                     const uint32_t* srow, uint64_t rstride, uint32_t stride,
+                                                     uint32_t a_prev, uint32_t nx, uint32_t* hdst) {
+    for (uint32_t i = lane; i < SFX_BUF; i += 64u) sb[i] = 0u;
+    wv.sync();
+    uint32_t s = lane < SFX_DEV_DW ? srow[(uint64_t)lane * stride] : 0u;
+    uint8_t* pb = (uint8_t*)pf;
+    const uint32_t hdr = 0x2000dc9du;                     // array(13); prev_hash: array16(32)
+    for (uint32_t j = 0; j < nx; ++j) {
+        if (lane < KW_PFX_DW) pf[lane] = 0u;
+        if (lane < SFX_BODY_DW) sb[SFX_PAD + lane] = s;
+        const uint32_t len_s = wv.readlane(s, SFX_DEV_LEN_DW);
+        if ((j + 1u < nx) & (lane < SFX_DEV_DW)) s = srow[(uint64_t)(j + 1u) * rstride + (uint64_t)lane * stride];
+        const uint32_t pw = wv.bperm(4u * ((lane >> 2) & 7u), a_prev);
+        const uint32_t eb = (pw >> (8u * (lane & 3u))) & 0xffu;
+        const bool big = (lane < 32u) & (eb >= 128u);
+        const uint64_t bal = wv.ballot(big);
+        const uint32_t rank = wv.rank_below(bal);
+        const uint32_t nbig = (uint32_t)__builtin_popcountll(bal);
+        wv.sync();                                        // pf zeroed before the byte writes
+        if (lane < 32u) {
+            const uint32_t off = 4u + lane + rank;
+            pb[off] = (uint8_t)(big ? 0xccu : eb);
+            if (big) pb[off + 1u] = (uint8_t)eb;
+        } else if (lane < 36u) {
+            pb[lane - 32u] = (uint8_t)(hdr >> (8u * (lane - 32u)));
+        }
+        wv.sync();
+        const uint32_t len_p = 36u + nbig, c = 72u - len_p, r = c & 3u;
+        const uint32_t nb = splice_blocks(len_p, len_s);
+        const uint32_t* sx = sb + (c >> 2);
+        uint32_t a = 0;
+        for (uint32_t blk = 0; blk < nb; ++blk) {
+            if (lane < 34u) {
+                const uint32_t q = 34u * blk + lane;
+                uint32_t v = align_bytes(sx[q + 1u], sx[q], r);
+                if (q < KW_PFX_DW) v |= pf[q];
+                if (q == 34u * nb - 1u) v ^= 0x80000000u;
+                a ^= v;
+            }
+            kw50_permute(wv, lane, a);
+        }
+        if (lane < 8u) hdst[8ull * j + lane] = a;
+        a_prev = a;
+        wv.sync();                                        // this height's LDS reads before the next's writes
+    }
+}
+
 }  // namespace bft

@@ -399,10 +399,25 @@ struct bftsim {
         uint32_t* ch = nullptr; uint32_t* flags = nullptr; uint32_t* ticks = nullptr; uint64_t* views = nullptr;
         uint32_t* rec = nullptr; uint8_t* hash = nullptr;
         uint32_t* sfx = nullptr;      // header suffix rows of the hash pass (sfx_rows per instance)
-        hipStream_t hs = nullptr;     // the set's hash stream
+        // a launch's own scratch (set 0: the handle's buffers), so that launches on different sets may run
+        // their consensus kernels at the same time (concurrent mode)
+        uint64_t* hist = nullptr; uint32_t* rcs = nullptr; uint32_t* backlog = nullptr;
+        uint32_t* resume = nullptr; uint32_t* save = nullptr;
+        hipStream_t hs = nullptr;     // the set's stream: its hash passes (and, concurrent, whole launches)
         hipEvent_t done = nullptr;    // hash pass of the last launch that used the set
+        hipEvent_t entry = nullptr;   // concurrent mode: the caller's stream at the launch call
         bool busy = false;
     } sets[MAX_SETS];
+    // concurrent mode (pipelined, the default there): every launch runs entirely on its set's stream, so
+    // the consensus kernels of consecutive launches overlap too (BFTSIM_TESTING + BFTSIM_SERIAL_CONSENSUS=1:
+    // the consensus kernels stay on the caller's stream, round-3 behaviour)
+    bool concurrent = true;
+    bool last_conc = false;           // the last launch ran on its set's stream
+    // block-hash chains: one wave per instance (bft_hash_chain_wave_kernel) up to this many instances per
+    // launch, lane pairs above. 0: lane pairs at every size -- the wave chain measured slower at every
+    // shard size (ds_bpermute latency and LDS issue at low occupancy), kept as an A/B arm
+    // (BFTSIM_TESTING + BFTSIM_CHAIN_WAVE_MAX)
+    uint64_t chain_wave_max = 0;
     int pipeline = 0;                 // number of row-table sets (0: no pipelining)
     uint32_t sfx_rows = 0;            // heights per hash-pass chunk (0: no hash pass)
     uint32_t n_sets = 0, cur_set = 0;
@@ -425,7 +440,15 @@ static int fail(bftsim* h, int code, const std::string& msg) {
         if (e_ != hipSuccess) return fail(h, BFTSIM_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+static void use_set0_scratch(bftsim* h) {
+    // after a concurrent launch d_hist .. d_save point at that launch's set; set 0's are the handle's own
+    if (h->n_sets == 0 || !h->sets[0].hist) return;
+    bftsim::RowSet& r = h->sets[0];
+    h->d_hist = r.hist; h->d_rcs = r.rcs; h->d_backlog = r.backlog; h->d_resume = r.resume; h->d_save = r.save;
+}
+
 static void free_bufs(bftsim* h) {
+    use_set0_scratch(h);
     // the per-height row tables are owned by the sets (set 0 = the unpipelined tables); d_ch .. d_hash
     // only point at the set of the last launch
     if (h->n_sets == 0) {
@@ -436,8 +459,14 @@ static void free_bufs(bftsim* h) {
         bftsim::RowSet& r = h->sets[k];
         (void)hipFree(r.ch); (void)hipFree(r.flags); (void)hipFree(r.ticks); (void)hipFree(r.views);
         (void)hipFree(r.rec); (void)hipFree(r.hash); (void)hipFree(r.sfx);
+        if (k > 0) {                                   // set 0's scratch is the handle's own
+            (void)hipFree(r.hist); (void)hipFree(r.rcs); (void)hipFree(r.backlog); (void)hipFree(r.resume);
+            (void)hipFree(r.save);
+        }
         r.ch = r.flags = r.ticks = nullptr; r.views = nullptr; r.rec = nullptr; r.hash = nullptr; r.sfx = nullptr;
+        r.hist = nullptr; r.rcs = r.backlog = r.resume = r.save = nullptr;
     }
+
     (void)hipFree(h->d_trace); (void)hipFree(h->d_tips); (void)hipFree(h->d_rcs);
     h->d_rcs = nullptr;
     (void)hipFree(h->d_backlog);
@@ -658,6 +687,7 @@ void bftsim_destroy(bftsim_t* h) {
     }
     for (uint32_t i = 0; i < bftsim::MAX_SETS; ++i) {
         if (h->sets[i].done) (void)hipEventDestroy(h->sets[i].done);
+        if (h->sets[i].entry) (void)hipEventDestroy(h->sets[i].entry);
         if (h->sets[i].hs) (void)hipStreamDestroy(h->sets[i].hs);
     }
     delete h;
@@ -699,7 +729,18 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
     }
     h->sets[0].ch = h->d_ch; h->sets[0].flags = h->d_flags; h->sets[0].ticks = h->d_ticks;
     h->sets[0].views = h->d_views; h->sets[0].rec = h->d_rec; h->sets[0].hash = h->d_hash;
+    h->sets[0].hist = h->d_hist; h->sets[0].rcs = h->d_rcs; h->sets[0].backlog = h->d_backlog;
+    h->sets[0].resume = h->d_resume; h->sets[0].save = h->d_save;
     h->n_sets = 1;
+    {
+        const char* tst = getenv("BFTSIM_TESTING");
+        const bool testing = tst && strcmp(tst, "1") == 0;
+        const char* ser = getenv("BFTSIM_SERIAL_CONSENSUS");
+        h->concurrent = !(testing && ser && strcmp(ser, "1") == 0);
+        const char* cw = getenv("BFTSIM_CHAIN_WAVE_MAX");
+        if (testing && cw) h->chain_wave_max = strtoull(cw, nullptr, 10);
+    }
+    const uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg, blocks = (n + per_block - 1) / per_block;
     for (uint32_t k = 1; k < (uint32_t)h->pipeline; ++k) {
         bftsim::RowSet& r = h->sets[k];
         HIPCHECK(h, hipMalloc(&r.ch, n * 4));
@@ -709,6 +750,15 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         HIPCHECK(h, hipMalloc(&r.rec, n * h->hcap * 16));
         HIPCHECK(h, hipMalloc(&r.hash, n * h->hcap * 32));
         h->n_sets = k + 1;
+        if (h->concurrent) {
+            HIPCHECK(h, hipMalloc(&r.hist, bft::HIST_BINS * sizeof(uint64_t)));
+            HIPCHECK(h, hipMalloc(&r.rcs, blocks * bft::rcs_words(h->seg, h->rcs_k) * 4));
+            if (h->d_backlog) HIPCHECK(h, hipMalloc(&r.backlog, h->backlog_bytes));
+            if (h->d_resume) {
+                HIPCHECK(h, hipMalloc(&r.resume, n * 4));
+                HIPCHECK(h, hipMalloc(&r.save, (uint64_t)bft::SAVE_WORDS * n * 64 * 4));
+            }
+        }
     }
     // the hash pass's suffix rows (runs without in-kernel hashes): every height in one chunk up to 2 GiB
     // per set, fewer heights per chunk beyond
@@ -815,6 +865,17 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         HIPCHECK(h, hipMemsetAsync(h->d_trace, 0, tb, s));
     }
     bft::Params p = make_params(h, first, n);
+    const bool pipe = h->pipeline >= 2 && !p.need_seed && h->n_sets >= 2;
+    // concurrent: the whole launch on its set's stream (its own scratch); not with per-launch host state
+    // (traces, the crypto log, which the next calls read from the last launch alone)
+    const bool conc = pipe && h->concurrent && !h->h_trace && !p.mlog && h->sets[1].hist;
+    if (h->last_conc && !conc) {
+        // a launch on the caller's stream after concurrent ones: they may still use set 0's scratch
+        if (int rc = sync_all(h)) return rc;
+        h->last_conc = false;
+    }
+    use_set0_scratch(h);
+    p = make_params(h, first, n);
 #ifdef BFT_STAMPS
     {
         static uint64_t* d_st = nullptr;
@@ -828,18 +889,28 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         g_stamp_waves = waves;
     }
 #endif
-    const bool pipe = h->pipeline >= 2 && !p.need_seed && h->n_sets >= 2;
     if (pipe) {
         // the next row-table set in the ring: the hash pass of the launch that used it last may still be
         // reading it
         h->cur_set = (h->cur_set + 1) % h->n_sets;
         bftsim::RowSet& r = h->sets[h->cur_set];
-        if (r.busy) HIPCHECK(h, hipStreamWaitEvent(s, r.done, 0));
+        if (!r.hs) HIPCHECK(h, hipStreamCreateWithFlags(&r.hs, hipStreamNonBlocking));
+        if (conc) {
+            // after the caller's earlier work on its stream; the set's previous launch precedes on the set stream
+            if (!r.entry) HIPCHECK(h, hipEventCreateWithFlags(&r.entry, hipEventDisableTiming));
+            HIPCHECK(h, hipEventRecord(r.entry, s));
+            HIPCHECK(h, hipStreamWaitEvent(r.hs, r.entry, 0));
+            s = r.hs;
+            h->d_hist = r.hist; h->d_rcs = r.rcs; h->d_backlog = r.backlog; h->d_resume = r.resume; h->d_save = r.save;
+            p.hist = r.hist; p.rcs = r.rcs; p.backlog = r.backlog;
+            h->last_conc = true;
+        } else if (r.busy) {
+            HIPCHECK(h, hipStreamWaitEvent(s, r.done, 0));
+        }
         h->d_ch = r.ch; h->d_flags = r.flags; h->d_ticks = r.ticks; h->d_views = r.views;
         h->d_rec = r.rec; h->d_hash = r.hash;
         p.committed_height = h->d_ch; p.flags = h->d_flags; p.ticks = h->d_ticks; p.views = h->d_views;
         p.rec = h->d_rec; p.hash = h->d_hash;
-        if (!r.hs) HIPCHECK(h, hipStreamCreateWithFlags(&r.hs, hipStreamNonBlocking));
         h->hs = r.hs;
     }
     bftsim::LaunchEv& ev = h->ring[h->ring_head % bftsim::RING];
@@ -890,23 +961,24 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         // (many instances per wave, or a workgroup per instance) run far longer than the chains: a
         // thread per instance on the hash stream hides the rows entirely (cfg2 6.8e8 -> 7.9e8).
         const bool on_launch = fast;
+        const bool wave = n <= h->chain_wave_max;
         if (K >= H && on_launch) {
             HIPCHECK(h, hipEventRecord(ev.h0, s));
             HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, 1, K, sfx, false, s, p));
             HIPCHECK(h, hipEventRecord(ev.sx, s));
-            if (pipe) HIPCHECK(h, hipStreamWaitEvent(t, ev.sx, 0));
-            HIPCHECK(h, bft::launch_hash_chain((uint32_t)n, 1, K, sfx, t, p));
+            if (pipe && t != s) HIPCHECK(h, hipStreamWaitEvent(t, ev.sx, 0));
+            HIPCHECK(h, bft::launch_hash_chain((uint32_t)n, 1, K, sfx, wave, t, p));
         } else {
             // chunks of K heights share the suffix rows: suffix and chain kernels in order on one stream
-            if (pipe) HIPCHECK(h, hipStreamWaitEvent(t, ev.c1, 0));
+            if (pipe && t != s) HIPCHECK(h, hipStreamWaitEvent(t, ev.c1, 0));
             HIPCHECK(h, hipEventRecord(ev.h0, t));
             for (uint32_t x0 = 1; x0 <= H; x0 += K) {
                 HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, x0, K, sfx, !on_launch, t, p));
-                HIPCHECK(h, bft::launch_hash_chain((uint32_t)n, x0, K, sfx, t, p));
+                HIPCHECK(h, bft::launch_hash_chain((uint32_t)n, x0, K, sfx, wave, t, p));
             }
         }
         HIPCHECK(h, hipEventRecord(ev.h1, t));
-        if (pipe) {
+        if (pipe && !conc) {
             HIPCHECK(h, hipEventRecord(h->sets[h->cur_set].done, t));
             h->sets[h->cur_set].busy = true;
         }

@@ -137,7 +137,12 @@ __constant__ PfxSel PFX_TBL[16] = {pfx_sel(0), pfx_sel(1), pfx_sel(2), pfx_sel(3
                                    pfx_sel(6), pfx_sel(7), pfx_sel(8), pfx_sel(9), pfx_sel(10), pfx_sel(11),
                                    pfx_sel(12), pfx_sel(13), pfx_sel(14), pfx_sel(15)};
 
-__global__ __launch_bounds__(64) void bft_hash_chain_kernel(Params p) {
+// One block is exactly one wave (launch_hash_chain): each lane pair reads only its own sbuf / pbuf
+// slices, and the __syncthreads below sit inside loops whose trip counts differ between the pairs of a
+// block (and after early exits) -- safe only because a one-wave barrier orders the wave's own LDS accesses.
+constexpr uint32_t CHAIN_PAIR_BLOCK = 64;
+__global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params p) {
+    static_assert(CHAIN_PAIR_BLOCK == 64, "bft_hash_chain_kernel's barriers assume one-wave blocks");
 #if defined(__HIP_DEVICE_COMPILE__)
     __shared__ __attribute__((aligned(16))) uint32_t sbuf[32 * SFX_BUF];      // splice buffer per pair
     __shared__ __attribute__((aligned(16))) uint64_t pbuf[64 * (PFX_WORDS + 4)];   // prefix per lane
@@ -217,6 +222,31 @@ __global__ __launch_bounds__(64) void bft_hash_chain_kernel(Params p) {
 #endif
 }
 
+// Small shards: the chain of one instance by one wave (bft_kwave.h kw50_chain). Workgroup b runs on XCD
+// b % 8 (round-robin dispatch): consecutive instances, whose suffix dwords share cache lines (rows are
+// dword-major across instances), are given to the same XCD.
+#ifndef BFT_CHAIN_WAVE_PRIO
+#define BFT_CHAIN_WAVE_PRIO 0
+#endif
+__global__ __launch_bounds__(64) void bft_hash_chain_wave_kernel(Params p) {
+    __shared__ __attribute__((aligned(16))) uint32_t sb[SFX_BUF];
+    __shared__ __attribute__((aligned(16))) uint32_t pf[KW_PFX_DW];
+    __builtin_amdgcn_s_setprio(BFT_CHAIN_WAVE_PRIO);
+    const uint32_t lane = threadIdx.x;
+    const uint32_t per = gridDim.x >> 3;                  // gridDim.x = 8 * ceil(n / 8)
+    const uint32_t il = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    if (il >= p.n_instances) return;                      // the whole wave
+    const uint32_t K = p.sfx_rows, x0 = p.sfx_x0;
+    const uint32_t ch = p.committed_height[il];
+    const uint32_t x1 = ch < x0 + K - 1u ? ch : x0 + K - 1u;
+    if (x1 < x0) return;
+    const uint32_t* ph = (const uint32_t*)(x0 == 1u ? p.genesis_hash : p.hash + ((uint64_t)il * p.rows + x0 - 1u) * 32);
+    const uint32_t a_prev = lane < 8u ? ph[lane] : 0u;
+    WaveHip wv;
+    kw50_chain(wv, lane, sb, pf, p.sfx + il, (uint64_t)SFX_DEV_DW * p.n_instances, p.n_instances, a_prev,
+               x1 - x0 + 1u, (uint32_t*)(p.hash + ((uint64_t)il * p.rows + x0) * 32));
+}
+
 // heights [x0, x0 + rows) of the block-hash pass: the suffix rows, then the chains
 hipError_t launch_hash_suffix(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, bool loop, hipStream_t s,
                               Params p) {
@@ -227,11 +257,12 @@ hipError_t launch_hash_suffix(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* 
     else hipLaunchKernelGGL(bft_hash_suffix_kernel, dim3((uint32_t)(((uint64_t)n * rows + 255u) / 256u)), dim3(256), 0, s, p);
     return hipGetLastError();
 }
-hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, hipStream_t s, Params p) {
+hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, bool wave, hipStream_t s, Params p) {
     p.sfx = sfx;
     p.sfx_rows = rows;
     p.sfx_x0 = x0;
-    hipLaunchKernelGGL(bft_hash_chain_kernel, dim3((n + 31u) / 32u), dim3(64), 0, s, p);
+    if (wave) hipLaunchKernelGGL(bft_hash_chain_wave_kernel, dim3(8u * ((n + 7u) / 8u)), dim3(64), 0, s, p);
+    else hipLaunchKernelGGL(bft_hash_chain_kernel, dim3((n + 31u) / 32u), dim3(CHAIN_PAIR_BLOCK), 0, s, p);
     return hipGetLastError();
 }
 

@@ -59,6 +59,7 @@ struct Sched {
     uint8_t* lds;
     uint32_t wave;
     bool fast;  // FAST kernel (S == 64, power-of-two N)
+    void (*body)(int lane);   // another wave body than the consensus kernels (emu_wave_chain_check)
 };
 thread_local Sched* g = nullptr;
 
@@ -217,15 +218,18 @@ void run_sim_seg(bool ns, uint32_t seg) {
 }
 
 void lane_entry(int lane) {
-    run_sim_seg(g->P->need_seed != 0, g->P->seg);
+    if (g->body) g->body(lane);
+    else run_sim_seg(g->P->need_seed != 0, g->P->seg);
     g->done[lane] = true;
     g->op[lane] = 0;
 }
 
-int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds, int nl = 64, bool fast = false) {
+int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds, int nl = 64, bool fast = false,
+             void (*body)(int) = nullptr) {
     static thread_local Sched s;
     g = &s;
     s.fast = fast;
+    s.body = body;
     s.nl = nl;
     s.P = &P;
     s.lds = lds.data();
@@ -499,6 +503,68 @@ extern "C" int emu_splice_check(uint32_t trials, uint64_t seed) {
         bool same = ls == sfx[bft::SFX_LEN_DW] && strided[1 + 3 * bft::SFX_DEV_LEN_DW] == ls;
         for (uint32_t k = 0; k < bft::SFX_BODY_DW; ++k) same = same && strided[1 + 3 * k] == sfx[k];
         if (!same) ++bad;
+    }
+    return bad;
+}
+
+// The small-shard chain kernel's body (bft_kwave.h kw50_chain: one wave per instance, the 50-lane Keccak,
+// the prefix written byte-wise by the lanes) over random chains: each chain's hashes against the lane
+// splice of spliced_block_hash from the same suffix rows. Returns mismatching heights.
+namespace {
+struct ChainJob {
+    const uint32_t* srow; uint64_t rstride; uint32_t stride; uint32_t parent[8]; uint32_t nx; uint32_t* hdst;
+    uint32_t* sb; uint32_t* pf;
+};
+thread_local ChainJob* g_chain = nullptr;
+void chain_body(int lane) {
+    EmuWave wv;
+    ChainJob& j = *g_chain;
+    bft::kw50_chain(wv, (uint32_t)lane, j.sb, j.pf, j.srow, j.rstride, j.stride, lane < 8 ? j.parent[lane] : 0u, j.nx,
+                    j.hdst);
+}
+}  // namespace
+extern "C" int emu_wave_chain_check(uint32_t chains, uint32_t heights, uint64_t seed) {
+    uint64_t s = seed | 1ull;
+    auto rnd = [&]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
+    std::vector<uint8_t> addr(64 * 20);
+    for (auto& b : addr) b = (uint8_t)rnd();
+    const uint32_t stride = 3;                        // 3 instances per row table: dword k of the row at k * 3
+    const uint64_t rstride = (uint64_t)bft::SFX_DEV_DW * stride;
+    std::vector<uint32_t> rows(rstride * heights + stride, 0xdeadbeefu), host(bft::SFX_DWORDS);
+    std::vector<uint32_t> hd(8ull * heights), sb(bft::SFX_BUF + 8), pf(bft::KW_PFX_DW + 2);
+    const uint64_t times[] = {0ull, 127ull, 128ull, 255ull, 256ull, 65535ull, 65536ull, 4294967295ull, 4294967296ull};
+    int bad = 0;
+    std::vector<uint8_t> lds;
+    bft::Params P{};
+    for (uint32_t c = 0; c < chains; ++c) {
+        ChainJob job{};
+        uint32_t want[8], prev[8];
+        for (int i = 0; i < 8; ++i) {                 // the parent: all-high, all-low or random bytes
+            uint32_t v = (uint32_t)rnd();
+            if (c % 4 == 1) v |= 0x80808080u;
+            if (c % 4 == 2) v &= 0x7f7f7f7fu;
+            job.parent[i] = prev[i] = v;
+        }
+        const uint32_t inst = (uint32_t)rnd(), h0 = (c % 3 == 0) ? 120u + (uint32_t)(rnd() % 20) : (uint32_t)rnd() % 70000u;
+        for (uint32_t j = 0; j < heights; ++j) {
+            const uint32_t prop = (uint32_t)(rnd() % 64), var = (uint32_t)(rnd() & 1);
+            const uint64_t time = (c % 3 == 1) ? times[rnd() % 9] : rnd() >> (rnd() % 64);
+            bft::header_suffix_strided(rows.data() + rstride * j + 1, stride, addr.data() + 20u * prop, s, inst, h0 + j,
+                                       prop, var, time);
+        }
+        job.srow = rows.data() + 1; job.rstride = rstride; job.stride = stride; job.nx = heights;
+        for (auto& v : hd) v = 0;
+        job.hdst = hd.data(); job.sb = sb.data(); job.pf = pf.data();
+        g_chain = &job;
+        if (run_wave(P, 0, lds, 64, false, chain_body)) return -1;
+        g_chain = nullptr;
+        for (uint32_t j = 0; j < heights; ++j) {
+            for (uint32_t k = 0; k < bft::SFX_BODY_DW; ++k) host[k] = rows[1 + rstride * j + (uint64_t)k * stride];
+            host[bft::SFX_LEN_DW] = rows[1 + rstride * j + (uint64_t)bft::SFX_DEV_LEN_DW * stride];
+            bft::spliced_block_hash(host.data(), prev, want);
+            if (memcmp(want, &hd[8ull * j], 32) != 0) ++bad;
+            memcpy(prev, want, 32);
+        }
     }
     return bad;
 }

@@ -134,6 +134,19 @@ def test_block_hash_splice_matches_one_piece_encoder():
     assert lib.emu_splice_check(20000, 987654321) == 0
 
 
+def test_wave_chain_matches_lane_splice():
+    """The small-shard block-hash chain (bft_kwave.h kw50_chain, one wave per instance: the 50-lane Keccak,
+    the prefix written byte-wise by 36 lanes with ballot prefix counts, lanes < 34 absorbing the spliced
+    message dwords) gives the same chain of hashes as the lane splice (spliced_block_hash) over the same
+    device-layout suffix rows, run by the emulator's 64 lane fibers: 2- and 3-block headers (parents of
+    all-high / all-low bytes), heights and times across MessagePack width boundaries."""
+    import ctypes
+    lib = E.lib()
+    lib.emu_wave_chain_check.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
+    assert lib.emu_wave_chain_check(24, 9, 4242) == 0
+    assert lib.emu_wave_chain_check(12, 17, 77) == 0
+
+
 def test_roundchangeset_capacity_overflow_is_flagged_and_local(monkeypatch):
     """The GPU RoundChangeSet holds a runtime number of rounds per validator (Params::rcs_k,
     bftsim_set_rcs_capacity); the reference's is an unbounded HashMap (round_change_set.rs:11-35). A

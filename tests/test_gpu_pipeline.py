@@ -17,7 +17,13 @@ def _sim(cfg):
 
 
 @pytest.mark.parametrize("depth", [2, 3, 4])
-def test_pipelined_launches_match_oracle(depth):
+@pytest.mark.parametrize("chain,serial", [("wave", False), ("pair", False), ("wave", True)])
+def test_pipelined_launches_match_oracle(depth, chain, serial, monkeypatch):
+    """both chain kernels (one wave per instance below BFTSIM_CHAIN_WAVE_MAX, lane pairs above), with the
+    consensus kernels of consecutive launches concurrent on their sets' streams (product) or serial"""
+    monkeypatch.setenv("BFTSIM_TESTING", "1")
+    monkeypatch.setenv("BFTSIM_CHAIN_WAVE_MAX", "1000000" if chain == "wave" else "0")
+    monkeypatch.setenv("BFTSIM_SERIAL_CONSENSUS", "1" if serial else "0")
     cfg = cfg3(heights=30)
     n = 64
     sim = _sim(cfg)
@@ -105,3 +111,27 @@ def test_chunked_hash_pass(monkeypatch):
             finally:
                 sim.close()
             assert_same(O.run(cfg, 0, 96), got, f"chunk rows {rows} depth {depth}")
+
+
+@pytest.mark.parametrize("chain", ["wave", "pair"])
+def test_small_shard_timed_mode(chain, monkeypatch):
+    """The strong-scaling shard of 8 GPUs (2,048 cfg3 instances per GPU), as bench.py times it (pipeline depth
+    3, concurrent launches, repeated launches of the same instances), with both chain kernels."""
+    monkeypatch.setenv("BFTSIM_TESTING", "1")
+    monkeypatch.setenv("BFTSIM_CHAIN_WAVE_MAX", "1000000" if chain == "wave" else "0")
+    cfg = cfg3()
+    n = 2048
+    sim = _sim(cfg)
+    try:
+        sim.set_pipeline(True, 3)
+        sim.prepare(n)
+        for _ in range(4):
+            sim.launch(2048)
+        sim.sync()
+        got = sim.fetch()
+        st = sim.stats()
+    finally:
+        sim.close()
+    ref = O.run(cfg, 2048, n, threads=16)
+    assert_same(ref, got, f"cfg3 2048 pipelined x4 ({chain})")
+    assert st["views"] == int(ref["views"].sum()) == n * 100
