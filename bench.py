@@ -250,10 +250,13 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each step's block-hash pass on the launch stream (no overlap across steps)")
-    ap.add_argument("--pipeline-depth", type=int, default=3,
-                    help="row-table sets in the launch ring (bftsim_set_pipeline); 3 measured best at every shard "
-                         "size (profiles/r02/curve): one hash stream per set, and more streams than the 4 hardware "
-                         "queues serialize the hash passes")
+    ap.add_argument("--pipeline-depth", type=int, default=None,
+                    help="launches in flight (bftsim_set_pipeline: a ring of row-table sets, each launch on its set's "
+                         "stream). Default: 4 at >= 12,288 instances per GPU, 6 below (profiles/r04/ab_depth_queues)")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process (HIP's default is 4): every set's stream needs its own "
+                         "hardware queue, or launches serialize behind each other (profiles/r04/ab_depth_queues); "
+                         "0 leaves the environment as it is")
     ap.add_argument("--byz", type=int, default=None,
                     help="cfg2 / cfg5: run the tolerated f as this many equivocating validators (SPEC.md §6: "
                          "cfg2-byz = 1, cfg5-byz = 2)")
@@ -269,6 +272,8 @@ def main():
         sys.exit(spawn_ranks(args.gpus))           # before anything touches the GPU
     if os.environ.get("BFTSIM_TESTING") == "1" and os.environ.get("BFTSIM_BENCH_STUB_DIR"):
         return stub_rank(args)
+    if args.hw_queues > 0:                         # read by the HIP runtime at its initialisation (below)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']} from the launcher; "
               "using WORLD_SIZE", file=sys.stderr)
@@ -327,6 +332,9 @@ def main():
     else:
         I = args.instances
         first = rank * I
+    auto_depth = args.pipeline_depth is None
+    if auto_depth:
+        args.pipeline_depth = 4 if I >= 12_288 else 6
     sim.set_pipeline(pipelined, args.pipeline_depth)
     if c5:
         sim.set_window(args.window)
@@ -385,6 +393,8 @@ def main():
     weak = None
     if args.scaling == "strong" and world > 1:
         Iw, first_w = args.instances, rank * args.instances
+        if auto_depth:
+            sim.set_pipeline(pipelined, 4 if Iw >= 12_288 else 6)
         sim.prepare(Iw)
         for _ in range(max(args.warmup, 1)):
             sim.launch(first_w, stream)

@@ -79,6 +79,7 @@ struct Params {
     // block-hash pass (kern_fast.hip): header suffix rows of heights [sfx_x0, sfx_x0 + sfx_rows)
     uint32_t* sfx;                    // [n_inst][sfx_rows][SFX_DWORDS]
     uint32_t sfx_x0, sfx_rows;
+    uint32_t chain_prio;              // s_setprio of the block-hash chain waves (0..3)
     uint32_t rcs_k;                   // RoundChangeSet rounds per validator (bftsim_set_rcs_capacity)
     uint32_t pad5;
 };

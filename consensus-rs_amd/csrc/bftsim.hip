@@ -418,6 +418,7 @@ struct bftsim {
     // shard size (ds_bpermute latency and LDS issue at low occupancy), kept as an A/B arm
     // (BFTSIM_TESTING + BFTSIM_CHAIN_WAVE_MAX)
     uint64_t chain_wave_max = 0;
+    uint32_t chain_prio = 0;          // s_setprio of the chain waves (BFTSIM_TESTING + BFTSIM_CHAIN_PRIO)
     int pipeline = 0;                 // number of row-table sets (0: no pipelining)
     uint32_t sfx_rows = 0;            // heights per hash-pass chunk (0: no hash pass)
     uint32_t n_sets = 0, cur_set = 0;
@@ -739,6 +740,8 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         h->concurrent = !(testing && ser && strcmp(ser, "1") == 0);
         const char* cw = getenv("BFTSIM_CHAIN_WAVE_MAX");
         if (testing && cw) h->chain_wave_max = strtoull(cw, nullptr, 10);
+        const char* cp = getenv("BFTSIM_CHAIN_PRIO");
+        if (testing && cp) h->chain_prio = (uint32_t)atoi(cp);
     }
     const uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg, blocks = (n + per_block - 1) / per_block;
     for (uint32_t k = 1; k < (uint32_t)h->pipeline; ++k) {
@@ -832,6 +835,7 @@ static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
     p.hist = h->d_hist;
     p.rcs = h->d_rcs;
     p.rcs_k = h->rcs_k;
+    p.chain_prio = h->chain_prio;
     p.backlog = h->d_backlog;
     if (h->crypto && h->d_mlog) {
         p.mlog = h->d_mlog;

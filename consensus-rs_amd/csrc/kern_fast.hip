@@ -141,9 +141,15 @@ __constant__ PfxSel PFX_TBL[16] = {pfx_sel(0), pfx_sel(1), pfx_sel(2), pfx_sel(3
 // slices, and the __syncthreads below sit inside loops whose trip counts differ between the pairs of a
 // block (and after early exits) -- safe only because a one-wave barrier orders the wave's own LDS accesses.
 constexpr uint32_t CHAIN_PAIR_BLOCK = 64;
+__device__ inline void set_prio(uint32_t k) {      // s_setprio takes an immediate
+    if (k == 1u) __builtin_amdgcn_s_setprio(1);
+    else if (k == 2u) __builtin_amdgcn_s_setprio(2);
+    else if (k >= 3u) __builtin_amdgcn_s_setprio(3);
+}
 __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params p) {
     static_assert(CHAIN_PAIR_BLOCK == 64, "bft_hash_chain_kernel's barriers assume one-wave blocks");
 #if defined(__HIP_DEVICE_COMPILE__)
+    set_prio(p.chain_prio);
     __shared__ __attribute__((aligned(16))) uint32_t sbuf[32 * SFX_BUF];      // splice buffer per pair
     __shared__ __attribute__((aligned(16))) uint64_t pbuf[64 * (PFX_WORDS + 4)];   // prefix per lane
     __shared__ PfxSel ptbl[16];                                                 // header_prefix_perm
@@ -225,13 +231,10 @@ __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params
 // Small shards: the chain of one instance by one wave (bft_kwave.h kw50_chain). Workgroup b runs on XCD
 // b % 8 (round-robin dispatch): consecutive instances, whose suffix dwords share cache lines (rows are
 // dword-major across instances), are given to the same XCD.
-#ifndef BFT_CHAIN_WAVE_PRIO
-#define BFT_CHAIN_WAVE_PRIO 0
-#endif
 __global__ __launch_bounds__(64) void bft_hash_chain_wave_kernel(Params p) {
     __shared__ __attribute__((aligned(16))) uint32_t sb[SFX_BUF];
     __shared__ __attribute__((aligned(16))) uint32_t pf[KW_PFX_DW];
-    __builtin_amdgcn_s_setprio(BFT_CHAIN_WAVE_PRIO);
+    set_prio(p.chain_prio);
     const uint32_t lane = threadIdx.x;
     const uint32_t per = gridDim.x >> 3;                  // gridDim.x = 8 * ceil(n / 8)
     const uint32_t il = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
