@@ -671,6 +671,83 @@ struct Fast64 {
         return true;
     }
 
+    // ------------------------------------------------------------------ the canonical tick, composed
+    // Lossless schedule, big-endian seeds (proposer 0). When a tick starts with every validator where the
+    // previous canonical height left it -- its seal waking now for height H = canon_h + 1 (wake_tick ==
+    // tick, mint_height == H, chain tip H - 1), nothing in flight or queued -- the whole tick has one
+    // outcome, and this applies it to every lane's registers at once:
+    //   T-step  — the seal wakes (minner/mod.rs:95-143 → core.rs:154-163): start_new_zero_round
+    //             (core.rs:441-470) for everyone, the own candidate accepted as the pending request
+    //             (request.rs:19-42), validator 0 sends its Preprepare (preprepare.rs:30-43); no timer fires
+    //             (start_new_zero_round re-arms it first) and no miner event is queued;
+    //   PP, PC1, PC2 — canonical_step (above);
+    //   commit  — resolve_commits records height H (one digest among the committers);
+    //   BLK     — pattern A (every lane committed): the fused block phase; pattern B (an equivocating
+    //             proposer split the validators, only one variant committed): two block-gossip phases,
+    //             the committers' Blocks [H, H] inserted by the others (core.rs:75-82, chain.rs:45-71) and
+    //             then theirs, ChainError::Exists for everyone;
+    //   miner   — every lane mines H + 1 at max(tick, block time + 1) (minner/mod.rs:95-143) = the block
+    //             time + 1 > tick: the seal sleeps until then (wake_tick).
+    // Both patterns end in the same per-lane state except the variant each lane holds (pp, comm) and its
+    // state (Committed for the committing variant, Prepared for the other). Phases used: 4 (A) or 5 (B) of
+    // phase_cap. Preconditions: the ballot below, k0 != k1 (canonical_step), H < hcap, phase_cap >= 5,
+    // and the block time of H (the proposer's cand_T) >= tick. Anything else runs the T-step and phase loop.
+    // Bit-identical by construction; checked by the emulator suite and the lossless fuzzer
+    // (tests/fuzz_parity.py lossless64).
+    BFT_FN bool canonical_tick() {
+        const uint32_t H = canon_h + 1u;
+        if (frozen | (H >= P.hcap) | (P.phase_cap < 5u)) return false;
+        const int32_t t = tick;
+        const uint32_t ptout = uni(rl(cand_T, 0));                  // the proposer's block time tick
+        if ((int32_t)ptout < t) return false;
+        uint32_t* pc = cache_p(0);                                  // Preprepare {h, d32}
+        uint32_t* c1 = cache_p(2);                                  // Prepare
+        uint32_t* c2 = cache_p(4);                                  // Commit
+        const uint32_t hd = (H & 0x3fffffu) | 0x80000000u;          // blk_d32 of (H, proposer 0, variant 0)
+        const uint32_t pc_h = pc[0], pc_d = pc[64];
+        const bool pp_hit = (me == 0u) & (pc_d != 0u) & (pc_h == H) & (pc_d == hd);   // out_preprepare's cache
+        const bool ok = ((fl & (L_DEAD | L_SYNCP)) == 0u) & (wake_tick == t) & (miner_queue == 0u) & (nxf == 0u) &
+                        (last == canon_h) & (mint_height == H) & (c1[0] != H) & (c2[0] != H) & !pp_hit;
+        if (ballot(!ok) != 0) return false;
+        // canonical_step's split and quorum decision (the proposer's F_PP_EQ = it is Byzantine)
+        uint64_t v1m = 0;
+        if (byz_mask & 1ull) {
+            const uint64_t d = split_mask(H);
+            v1m = ((uint64_t)uni((uint32_t)d) | ((uint64_t)uni((uint32_t)(d >> 32)) << 32)) & ~1ull;
+        }
+        const uint64_t hon = ~byz_mask;
+        const bool k0 = popc(byz_mask | (hon & ~v1m)) > Q, k1 = popc(byz_mask | (hon & v1m)) > Q;
+        if (k0 == k1) return false;
+        // T-step: the pending request and validator 0's Preprepare through its outbound cache
+        *lane_p(F64Layout::W_PENDT) = cand_T;
+        if (me == 0u) { pc[0] = H; pc[64] = hd; }
+        pp_T_out = ptout;
+        // PP, PC1, PC2 (canonical_step) and the block phases: the per-lane result
+        const bool var = ((v1m >> me) & 1ull) != 0;
+        const bool fires = var == k1;
+        const uint32_t d32 = hd | (var ? (1u << 30) : 0u);
+        c1[0] = H; c1[64] = d32;
+        c2[0] = H; c2[64] = d32;
+        h = H;
+        pp = blk_make(H, 0u, var ? 1u : 0u, ptout);
+        prep = ~0ull;
+        comm = byz_mask | (hon & (var ? v1m : ~v1m));
+        fl = (fl & ~(L_ST | L_WAIT | L_LOCK | L_PENDV | L_CMT)) | L_PROP | L_PENDV | L_LOCK |
+             (fires ? ST_COMMITTED : ST_PREPARED);
+        timer_tick = t + 1;
+        last = H;
+        last_T = (int32_t)ptout;
+        cand_T = ptout + 1u;
+        mint_height = H + 1u;
+        wake_tick = (int32_t)ptout + 1;
+        miner_queue = 0;
+        nxf = 0;
+        nx_blo = H;
+        nx_bhi = H;
+        record_canon(H, blk_make(H, 0u, k1 ? 1u : 0u, ptout));
+        return true;
+    }
+
     // ------------------------------------------------------------------ hand-over to the full kernel
     // the full kernel's save layout (bft_wave.h BFT_STATE_32 / BFT_STATE_64, then prep, comm, the 12
     // cache words, the bool bits, tick, phase); every implied field is expanded here
@@ -741,6 +818,12 @@ struct Fast64 {
         bool bailed = false;
         for (tick = 0; tick < (int32_t)P.max_ticks; ++tick) {
             if (seg_done) break;
+            // the canonical tick (lossless, big-endian seeds): T-step and phases in one closed form
+            if (!LOSSY && !SEEDED && macro_ok && tick != 0 && canonical_tick()) {
+                F64_STAMP(1);
+                if (canon_h >= P.heights) { seg_done = true; done_tick = (uint32_t)tick + 1; }
+                continue;
+            }
             // act: this instance still runs this tick (uniform); per lane, only running validators
             // (not silent) handle events and messages
             bool act = !frozen;

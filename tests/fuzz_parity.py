@@ -1,6 +1,7 @@
 """Randomized parity fuzz: CPU wave emulator (the kernel body) vs the oracle on random configs.
 Usage: python tests/fuzz_parity.py [seconds] [rng seed] [big]. `big` draws N in 65..256 (the
-workgroup-segment kernels), `n64` N = 64 (the FAST kernel and its hand-overs); a fourth argument
+workgroup-segment kernels), `n64` N = 64 (the FAST kernel and its hand-overs), `lossless64` N = 64 without drops
+or crashes (the canonical step and tick, with phase caps, short max_ticks and silent validators); a fourth argument
 `replay` runs every config in backlog replay mode (SPEC.md §10), `le` with little-endian U128 seeds. Test-only tool (not collected by pytest)."""
 import random
 import sys
@@ -12,7 +13,16 @@ from bftsim.configs import BftConfig
 from parity_util import mismatches
 
 
-def random_config(rng, big=False, n64=False, replay=False, le=False):
+def random_config(rng, big=False, n64=False, replay=False, le=False, lossless=False):
+    if lossless:                         # N = 64 without drops or crashes: the canonical step and tick
+        n = 64
+        byz = rng.choice([0, 1, 5, 21, 21, 21, 30, 42, 43])
+        cap = rng.choice([16, 16, 3, 4, 5, 6, 8])
+        silent = rng.sample(range(n), k=rng.choice([0, 0, 0, 1]))
+        heights = rng.choice([5, 20, 70, 130])
+        return BftConfig(n=n, heights=heights, seed=rng.randrange(1 << 40), byz_count=byz, phase_cap=cap,
+                         silent=silent, max_ticks=heights * rng.choice([1, 2, 4]) + rng.choice([0, 1, 16]),
+                         name=f"lossless-b{byz}-cap{cap}-s{len(silent)}-h{heights}")
     if n64:                              # the FAST kernel (bft_fast64.h) and its hand-overs
         n = 64
     elif big:
@@ -39,9 +49,10 @@ def main():
     n64 = len(sys.argv) > 3 and sys.argv[3] == "n64"
     replay = "replay" in sys.argv[3:]
     le = "le" in sys.argv[3:]                     # little-endian U128 seeds (hash-dependent proposers)
+    lossless = len(sys.argv) > 3 and sys.argv[3] == "lossless64"
     t0, runs, fails = time.time(), 0, 0
     while time.time() - t0 < budget:
-        cfg = random_config(rng, big, n64, replay, le)
+        cfg = random_config(rng, big, n64, replay, le, lossless)
         first = rng.randrange(1 << 20)
         n_inst = rng.choice([1, 2] if big else [1, 3, 8])
         a = O.run(cfg, first, n_inst)
