@@ -69,7 +69,8 @@ ALGO_BYTES_PER_VIEW = 48
 
 def _pmc_files(workload: str):
     """The committed PMC summaries of a workload, oldest first: profiles/<round>/pmc_summary.json for the
-    headline (cfg3), profiles/<round>/<workload>/pmc_summary.json for the others."""
+    headline (cfg3), profiles/<round>/<workload>/pmc_summary.json for the others (cfg4 per validator count:
+    profiles/<round>/cfg4_n<N>/, so that two sweep points never share one record)."""
     import glob
     sub = "" if workload == "cfg3" else workload
     return sorted(glob.glob(os.path.join(ROOT, "profiles", "*", sub, "pmc_summary.json")))
@@ -424,7 +425,8 @@ def main():
             dom, ops, ms = "bft_hash_kernel", h_ops, hms
         achieved = ops / (ms / 1e3) / 1e12
         peak = VALU_PEAK / 1e12
-        traffic, traffic_src = pmc_traffic(wl)
+        pmc_key = f"cfg4_n{cfg.n}" if wl == "cfg4" else wl
+        traffic, traffic_src = pmc_traffic(pmc_key)
         algo_bytes = ALGO_BYTES_PER_VIEW * views_rank
         def trim(h):
             h = list(h)
@@ -478,7 +480,7 @@ def main():
                     "salu_per_s": q["salu"] / (ms / 1e3), "salu_peak_per_s": SALU_ISSUE_PEAK,
                     "salu_frac": q["salu"] / (ms / 1e3) / SALU_ISSUE_PEAK,
                     "per_instance_round": {"valu": q["valu"] / max(views_rank, 1),
-                                           "salu": q["salu"] / max(views_rank, 1)}})(pmc_issue(wl)),
+                                           "salu": q["salu"] / max(views_rank, 1)}})(pmc_issue(pmc_key)),
                 "traffic_source": traffic_src,
                 "hbm": {"algorithmic_bytes": algo_bytes, "achieved_GBps": algo_bytes / (ms / 1e3) / 1e9,
                         "peak_GBps": HBM_PEAK / 1e9, "frac": algo_bytes / (ms / 1e3) / HBM_PEAK},

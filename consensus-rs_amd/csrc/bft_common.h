@@ -60,6 +60,7 @@ struct Params {
     uint32_t nmask;                   // N-1 when N is a power of two (x mod N = x & nmask), else 0
     // FAST launches (bft_wave.h): instances that need the general path are saved and resumed
     uint32_t* resume_flags;           // [n_inst] 1 = saved by the FAST kernel
+    uint32_t* resume_q;               // [2 + n_inst] (device): hand-over count, queue head, instance list
     uint32_t* save;                   // [n_inst * 64][SAVE_WORDS] per-lane state
     uint64_t save_stride;             // unused (kept for the layout)
     uint32_t resume_mode;             // CPU emulator only: run the MODE_RESUME body

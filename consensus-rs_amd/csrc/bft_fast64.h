@@ -891,7 +891,12 @@ struct Fast64 {
                     if (ballot(bad != 0) != 0) path = P_GENERAL;
                     if (path == P_GENERAL) {                          // hand the instance to the full kernel
                         save_state(p);
-                        if (me == 0) P.resume_flags[inst_local] = 1u;
+                        if (me == 0) {
+                            P.resume_flags[inst_local] = 1u;
+#if defined(__HIP_DEVICE_COMPILE__)
+                            if (P.resume_q) P.resume_q[2u + atomicAdd(P.resume_q, 1u)] = inst_local;   // the resume queue
+#endif
+                        }
                         bailed = true;
                         seg_done = true;
                         break;

@@ -381,6 +381,7 @@ struct bftsim {
     uint32_t* d_backlog = nullptr;    // replay mode: backlog slots, backlog_words(seg) per wave / workgroup
     uint64_t backlog_bytes = 0;
     uint32_t* d_resume = nullptr;     // FAST launches: [cap_inst] hand-over flags
+    uint32_t* d_resume_q = nullptr;   // FAST launches: [2 + cap_inst] the resume kernel's queue
     uint32_t* d_save = nullptr;       // FAST launches: [SAVE_WORDS][cap_inst * 64] saved lane state
     int fast = 1;                     // FAST kernel + resume for N = 64 (bftsim_set_fast(h, 0): full kernel)
     uint32_t window = 0;              // 0: full per-height rows; else ring of `window` rows
@@ -402,7 +403,7 @@ struct bftsim {
         // a launch's own scratch (set 0: the handle's buffers), so that launches on different sets may run
         // their consensus kernels at the same time (concurrent mode)
         uint64_t* hist = nullptr; uint32_t* rcs = nullptr; uint32_t* backlog = nullptr;
-        uint32_t* resume = nullptr; uint32_t* save = nullptr;
+        uint32_t* resume = nullptr; uint32_t* save = nullptr; uint32_t* resume_q = nullptr;
         hipStream_t hs = nullptr;     // the set's stream: its hash passes (and, concurrent, whole launches)
         hipEvent_t done = nullptr;    // hash pass of the last launch that used the set
         hipEvent_t entry = nullptr;   // concurrent mode: the caller's stream at the launch call
@@ -446,6 +447,7 @@ static void use_set0_scratch(bftsim* h) {
     if (h->n_sets == 0 || !h->sets[0].hist) return;
     bftsim::RowSet& r = h->sets[0];
     h->d_hist = r.hist; h->d_rcs = r.rcs; h->d_backlog = r.backlog; h->d_resume = r.resume; h->d_save = r.save;
+    h->d_resume_q = r.resume_q;
 }
 
 static void free_bufs(bftsim* h) {
@@ -462,10 +464,10 @@ static void free_bufs(bftsim* h) {
         (void)hipFree(r.rec); (void)hipFree(r.hash); (void)hipFree(r.sfx);
         if (k > 0) {                                   // set 0's scratch is the handle's own
             (void)hipFree(r.hist); (void)hipFree(r.rcs); (void)hipFree(r.backlog); (void)hipFree(r.resume);
-            (void)hipFree(r.save);
+            (void)hipFree(r.save); (void)hipFree(r.resume_q);
         }
         r.ch = r.flags = r.ticks = nullptr; r.views = nullptr; r.rec = nullptr; r.hash = nullptr; r.sfx = nullptr;
-        r.hist = nullptr; r.rcs = r.backlog = r.resume = r.save = nullptr;
+        r.hist = nullptr; r.rcs = r.backlog = r.resume = r.save = r.resume_q = nullptr;
     }
 
     (void)hipFree(h->d_trace); (void)hipFree(h->d_tips); (void)hipFree(h->d_rcs);
@@ -477,8 +479,8 @@ static void free_bufs(bftsim* h) {
     (void)hipFree(h->d_vsnap); (void)hipFree(h->d_votes); (void)hipFree(h->d_vsig); (void)hipFree(h->d_vhas);
     h->d_vsnap = nullptr; h->d_votes = nullptr; h->d_vsig = nullptr; h->d_vhas = nullptr; h->vsig_n = 0;
     h->backlog_bytes = 0;
-    (void)hipFree(h->d_resume); (void)hipFree(h->d_save);
-    h->d_resume = nullptr; h->d_save = nullptr;
+    (void)hipFree(h->d_resume); (void)hipFree(h->d_save); (void)hipFree(h->d_resume_q);
+    h->d_resume = nullptr; h->d_save = nullptr; h->d_resume_q = nullptr;
     for (uint32_t k = 0; k < bftsim::MAX_SETS; ++k) h->sets[k].busy = false;
     h->n_sets = 0;
     h->cur_set = 0;
@@ -726,12 +728,13 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
     }
     if (h->seg == 64 && h->cfg.n == 64) {          // FAST kernel hand-over buffers
         HIPCHECK(h, hipMalloc(&h->d_resume, n * 4));
+        HIPCHECK(h, hipMalloc(&h->d_resume_q, (n + 2) * 4));
         HIPCHECK(h, hipMalloc(&h->d_save, (uint64_t)bft::SAVE_WORDS * n * 64 * 4));
     }
     h->sets[0].ch = h->d_ch; h->sets[0].flags = h->d_flags; h->sets[0].ticks = h->d_ticks;
     h->sets[0].views = h->d_views; h->sets[0].rec = h->d_rec; h->sets[0].hash = h->d_hash;
     h->sets[0].hist = h->d_hist; h->sets[0].rcs = h->d_rcs; h->sets[0].backlog = h->d_backlog;
-    h->sets[0].resume = h->d_resume; h->sets[0].save = h->d_save;
+    h->sets[0].resume = h->d_resume; h->sets[0].save = h->d_save; h->sets[0].resume_q = h->d_resume_q;
     h->n_sets = 1;
     {
         const char* tst = getenv("BFTSIM_TESTING");
@@ -759,6 +762,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
             if (h->d_backlog) HIPCHECK(h, hipMalloc(&r.backlog, h->backlog_bytes));
             if (h->d_resume) {
                 HIPCHECK(h, hipMalloc(&r.resume, n * 4));
+                HIPCHECK(h, hipMalloc(&r.resume_q, (n + 2) * 4));
                 HIPCHECK(h, hipMalloc(&r.save, (uint64_t)bft::SAVE_WORDS * n * 64 * 4));
             }
         }
@@ -906,6 +910,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
             HIPCHECK(h, hipStreamWaitEvent(r.hs, r.entry, 0));
             s = r.hs;
             h->d_hist = r.hist; h->d_rcs = r.rcs; h->d_backlog = r.backlog; h->d_resume = r.resume; h->d_save = r.save;
+            h->d_resume_q = r.resume_q;
             p.hist = r.hist; p.rcs = r.rcs; p.backlog = r.backlog;
             h->last_conc = true;
         } else if (r.busy) {
@@ -942,9 +947,11 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     if (fast) {
         // FAST kernel over every instance, then the full kernel over the ones it handed over
         p.resume_flags = h->d_resume;
+        p.resume_q = h->d_resume_q;
         p.save = h->d_save;
         p.save_stride = n * 64;
         HIPCHECK(h, hipMemsetAsync(h->d_resume, 0, n * 4, s));
+        HIPCHECK(h, hipMemsetAsync(h->d_resume_q, 0, 8, s));
         HIPCHECK(h, bft::launch_fast(dim3(grid), s, p));
         HIPCHECK(h, bft::launch_resume(dim3(grid), lds, s, p));
     } else {

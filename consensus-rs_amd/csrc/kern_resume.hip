@@ -9,15 +9,28 @@ namespace bft {
 #endif
 // the full kernel over the instances the FAST kernel handed over, from their saved phase (NEED_SEED:
 // little-endian seeds, block hashes in-kernel)
+// Persistent waves over a queue (Params::resume_q, filled by the FAST kernel: count, head, instance ids):
+// each wave takes the next handed-over instance until the queue is empty. A wave per instance of the launch
+// would dispatch n waves carrying the general body's LDS even when nothing was handed over, and beside the
+// concurrent launches' kernels that dispatch alone took ~0.2 ms per launch (cfg3, profiles/r04).
 template <bool NEED_SEED>
 __global__ __launch_bounds__(64, BFT_WAVES_PER_SIMD) void bft_consensus_resume_kernel(Params p) {
     extern __shared__ uint8_t lds[];
-    Sim<WaveHip, NEED_SEED, 64, MODE_RESUME> sim(p, lds, blockIdx.x);
-    sim.run();
+    const uint32_t count = __hip_atomic_load(p.resume_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+        uint32_t i = 0;
+        if (threadIdx.x == 0) i = atomicAdd(p.resume_q + 1, 1u);
+        i = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)i, 0, 64));
+        if (i >= count) break;                            // every wave gets here once the queue is empty
+        Sim<WaveHip, NEED_SEED, 64, MODE_RESUME> sim(p, lds, p.resume_q[2u + i]);
+        sim.run();
+    }
 }
 hipError_t launch_resume(dim3 grid, size_t lds, hipStream_t s, const Params& p) {
-    if (p.need_seed) hipLaunchKernelGGL(bft_consensus_resume_kernel<true>, grid, dim3(64), lds, s, p);
-    else hipLaunchKernelGGL(bft_consensus_resume_kernel<false>, grid, dim3(64), lds, s, p);
+    // waves that can be resident at once (3 per SIMD): more would only queue for the same slots
+    const uint32_t g = grid.x < 256u * 4u * BFT_WAVES_PER_SIMD ? grid.x : 256u * 4u * BFT_WAVES_PER_SIMD;
+    if (p.need_seed) hipLaunchKernelGGL(bft_consensus_resume_kernel<true>, dim3(g), dim3(64), lds, s, p);
+    else hipLaunchKernelGGL(bft_consensus_resume_kernel<false>, dim3(g), dim3(64), lds, s, p);
     return hipGetLastError();
 }
 
