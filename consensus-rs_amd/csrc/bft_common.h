@@ -61,6 +61,7 @@ struct Params {
     // FAST launches (bft_wave.h): instances that need the general path are saved and resumed
     uint32_t* resume_flags;           // [n_inst] 1 = saved by the FAST kernel
     uint32_t* resume_q;               // [2 + n_inst] (device): hand-over count, queue head, instance list
+    uint32_t* resume_hint;            // host-mapped word: the last resume kernel's count (sizes the next grid)
     uint32_t* save;                   // [n_inst * 64][SAVE_WORDS] per-lane state
     uint64_t save_stride;             // unused (kept for the layout)
     uint32_t resume_mode;             // CPU emulator only: run the MODE_RESUME body

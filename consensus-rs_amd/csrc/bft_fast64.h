@@ -818,11 +818,17 @@ struct Fast64 {
         bool bailed = false;
         for (tick = 0; tick < (int32_t)P.max_ticks; ++tick) {
             if (seg_done) break;
-            // the canonical tick (lossless, big-endian seeds): T-step and phases in one closed form
-            if (!LOSSY && !SEEDED && macro_ok && tick != 0 && canonical_tick()) {
-                F64_STAMP(1);
-                if (canon_h >= P.heights) { seg_done = true; done_tick = (uint32_t)tick + 1; }
-                continue;
+            // a run of canonical ticks (lossless, big-endian seeds): T-step and phases in one closed form each,
+            // in a loop of its own (few live values: no copies of the whole state at every branch); the first
+            // tick that is not canonical falls through to the T-step and phase loop below, unchanged
+            if (!LOSSY && !SEEDED && macro_ok && tick != 0) {
+                bool stop = false;
+                while (canonical_tick()) {
+                    F64_STAMP(1);
+                    if (canon_h >= P.heights) { seg_done = true; done_tick = (uint32_t)tick + 1; stop = true; break; }
+                    if (++tick >= (int32_t)P.max_ticks) { stop = true; break; }
+                }
+                if (stop) break;
             }
             // act: this instance still runs this tick (uniform); per lane, only running validators
             // (not silent) handle events and messages

@@ -404,6 +404,7 @@ struct bftsim {
         // their consensus kernels at the same time (concurrent mode)
         uint64_t* hist = nullptr; uint32_t* rcs = nullptr; uint32_t* backlog = nullptr;
         uint32_t* resume = nullptr; uint32_t* save = nullptr; uint32_t* resume_q = nullptr;
+        uint32_t* hint = nullptr;     // host-mapped: the hand-over count of the set's last launch (resume grid)
         hipStream_t hs = nullptr;     // the set's stream: its hash passes (and, concurrent, whole launches)
         hipEvent_t done = nullptr;    // hash pass of the last launch that used the set
         hipEvent_t entry = nullptr;   // concurrent mode: the caller's stream at the launch call
@@ -691,6 +692,7 @@ void bftsim_destroy(bftsim_t* h) {
     for (uint32_t i = 0; i < bftsim::MAX_SETS; ++i) {
         if (h->sets[i].done) (void)hipEventDestroy(h->sets[i].done);
         if (h->sets[i].entry) (void)hipEventDestroy(h->sets[i].entry);
+        if (h->sets[i].hint) (void)hipHostFree(h->sets[i].hint);
         if (h->sets[i].hs) (void)hipStreamDestroy(h->sets[i].hs);
     }
     delete h;
@@ -952,6 +954,14 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         p.save_stride = n * 64;
         HIPCHECK(h, hipMemsetAsync(h->d_resume, 0, n * 4, s));
         HIPCHECK(h, hipMemsetAsync(h->d_resume_q, 0, 8, s));
+        {
+            bftsim::RowSet& r = h->sets[pipe ? h->cur_set : 0];
+            if (!r.hint) {
+                HIPCHECK(h, hipHostMalloc((void**)&r.hint, 4, hipHostMallocMapped | hipHostMallocCoherent));
+                *r.hint = 0xffffffffu;                    // unknown: the full grid
+            }
+            p.resume_hint = r.hint;
+        }
         HIPCHECK(h, bft::launch_fast(dim3(grid), s, p));
         HIPCHECK(h, bft::launch_resume(dim3(grid), lds, s, p));
     } else {
