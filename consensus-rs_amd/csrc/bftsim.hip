@@ -425,6 +425,14 @@ struct bftsim {
     uint32_t sfx_rows = 0;            // heights per hash-pass chunk (0: no hash pass)
     uint32_t n_sets = 0, cur_set = 0;
     hipStream_t hs = nullptr;         // the hash stream of the last pipelined launch
+    // concurrent mode: the consensus kernels (+ resume + suffix rows) of successive launches go round-robin
+    // over `n_cs` launch streams, the chains of each set on the set's own stream. A set is reused once its
+    // last chain is done; the chains (long, sequential in height) thus overlap up to the ring's depth while
+    // the consensus kernels only need a couple of streams (BFTSIM_TESTING + BFTSIM_LAUNCH_STREAMS=0: every
+    // stage of a launch on its set's stream)
+    static constexpr uint32_t MAX_CS = 4;
+    hipStream_t cs[MAX_CS] = {};
+    uint32_t n_cs = 2, cur_cs = 0;
     // per-launch kernel timing: a ring of event quadruples, read by bftsim_kernel_ms_sum
     static constexpr uint32_t RING = 64;
     struct LaunchEv { hipEvent_t c0, c1, h0, h1, sx; bool has_hash, pending; } ring[RING] = {};
@@ -498,6 +506,8 @@ static int sync_all(bftsim* h) {
     HIPCHECK(h, hipStreamSynchronize(h->last_stream));
     for (uint32_t k = 0; k < bftsim::MAX_SETS; ++k)
         if (h->sets[k].hs) HIPCHECK(h, hipStreamSynchronize(h->sets[k].hs));
+    for (uint32_t k = 0; k < bftsim::MAX_CS; ++k)
+        if (h->cs[k]) HIPCHECK(h, hipStreamSynchronize(h->cs[k]));
     return BFTSIM_OK;
 }
 
@@ -695,6 +705,8 @@ void bftsim_destroy(bftsim_t* h) {
         if (h->sets[i].hint) (void)hipHostFree(h->sets[i].hint);
         if (h->sets[i].hs) (void)hipStreamDestroy(h->sets[i].hs);
     }
+    for (uint32_t i = 0; i < bftsim::MAX_CS; ++i)
+        if (h->cs[i]) (void)hipStreamDestroy(h->cs[i]);
     delete h;
 }
 
@@ -747,6 +759,8 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         if (testing && cw) h->chain_wave_max = strtoull(cw, nullptr, 10);
         const char* cp = getenv("BFTSIM_CHAIN_PRIO");
         if (testing && cp) h->chain_prio = (uint32_t)atoi(cp);
+        const char* ls = getenv("BFTSIM_LAUNCH_STREAMS");
+        if (testing && ls) h->n_cs = (uint32_t)atoi(ls) < bftsim::MAX_CS ? (uint32_t)atoi(ls) : bftsim::MAX_CS;
     }
     const uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg, blocks = (n + per_block - 1) / per_block;
     for (uint32_t k = 1; k < (uint32_t)h->pipeline; ++k) {
@@ -906,11 +920,18 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         bftsim::RowSet& r = h->sets[h->cur_set];
         if (!r.hs) HIPCHECK(h, hipStreamCreateWithFlags(&r.hs, hipStreamNonBlocking));
         if (conc) {
-            // after the caller's earlier work on its stream; the set's previous launch precedes on the set stream
+            // after the caller's earlier work on its stream, and after the set's last chain
             if (!r.entry) HIPCHECK(h, hipEventCreateWithFlags(&r.entry, hipEventDisableTiming));
             HIPCHECK(h, hipEventRecord(r.entry, s));
-            HIPCHECK(h, hipStreamWaitEvent(r.hs, r.entry, 0));
-            s = r.hs;
+            hipStream_t ls = r.hs;
+            if (h->n_cs) {
+                h->cur_cs = (h->cur_cs + 1) % h->n_cs;
+                if (!h->cs[h->cur_cs]) HIPCHECK(h, hipStreamCreateWithFlags(&h->cs[h->cur_cs], hipStreamNonBlocking));
+                ls = h->cs[h->cur_cs];
+                if (r.busy) HIPCHECK(h, hipStreamWaitEvent(ls, r.done, 0));
+            }
+            HIPCHECK(h, hipStreamWaitEvent(ls, r.entry, 0));
+            s = ls;
             h->d_hist = r.hist; h->d_rcs = r.rcs; h->d_backlog = r.backlog; h->d_resume = r.resume; h->d_save = r.save;
             h->d_resume_q = r.resume_q;
             p.hist = r.hist; p.rcs = r.rcs; p.backlog = r.backlog;
@@ -999,7 +1020,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
             }
         }
         HIPCHECK(h, hipEventRecord(ev.h1, t));
-        if (pipe && !conc) {
+        if (pipe) {
             HIPCHECK(h, hipEventRecord(h->sets[h->cur_set].done, t));
             h->sets[h->cur_set].busy = true;
         }

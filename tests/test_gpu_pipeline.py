@@ -17,13 +17,16 @@ def _sim(cfg):
 
 
 @pytest.mark.parametrize("depth", [2, 3, 4])
-@pytest.mark.parametrize("chain,serial", [("wave", False), ("pair", False), ("wave", True)])
-def test_pipelined_launches_match_oracle(depth, chain, serial, monkeypatch):
+@pytest.mark.parametrize("chain,serial,lstreams", [("wave", False, 2), ("pair", False, 2), ("pair", False, 1),
+                                                    ("pair", False, 0), ("wave", True, 2)])
+def test_pipelined_launches_match_oracle(depth, chain, serial, lstreams, monkeypatch):
     """both chain kernels (one wave per instance below BFTSIM_CHAIN_WAVE_MAX, lane pairs above), with the
-    consensus kernels of consecutive launches concurrent on their sets' streams (product) or serial"""
+    consensus kernels of consecutive launches concurrent (product: round-robin over launch streams, the chains
+    on the sets' streams; or every stage on the set's stream) or serial on the caller's stream"""
     monkeypatch.setenv("BFTSIM_TESTING", "1")
     monkeypatch.setenv("BFTSIM_CHAIN_WAVE_MAX", "1000000" if chain == "wave" else "0")
     monkeypatch.setenv("BFTSIM_SERIAL_CONSENSUS", "1" if serial else "0")
+    monkeypatch.setenv("BFTSIM_LAUNCH_STREAMS", str(lstreams))
     cfg = cfg3(heights=30)
     n = 64
     sim = _sim(cfg)
