@@ -350,6 +350,7 @@ def main():
         t0 = time.perf_counter()
         for _ in range(args.steps):
             sim.launch(first_id, stream)
+        sim.sync()                        # enqueues the last partial hash batch and waits for every stream
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -360,11 +361,13 @@ def main():
 
     for _ in range(args.warmup):
         sim.launch(first, stream)
+    sim.sync()
     torch.cuda.synchronize(dev)
 
     # work per step: instance-rounds of this shard (identical every step), summed over ranks
     if args.warmup == 0:                  # the work of a step is read from one run's statistics
         sim.launch(first, stream)
+        sim.sync()
         torch.cuda.synchronize(dev)
     st = sim.stats()
     # node-wide statistics: one RCCL all-reduce inside libbftsim (bftsim_stats_allreduce, over xGMI);
@@ -399,6 +402,7 @@ def main():
         sim.prepare(Iw)
         for _ in range(max(args.warmup, 1)):
             sim.launch(first_w, stream)
+        sim.sync()
         torch.cuda.synchronize(dev)
         vw = torch.tensor([sim.stats()["views"]], dtype=torch.int64, device=dev)
         dist.all_reduce(vw)

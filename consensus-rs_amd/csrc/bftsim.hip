@@ -392,29 +392,28 @@ struct bftsim {
     uint64_t n_req = 0;               // instances of the next launch (bftsim_prepare); <= cap_inst
     uint64_t last_n = 0, last_first = 0;
     hipStream_t last_stream = nullptr;
-    // pipelined launches (bftsim_set_pipeline): two row-table sets used alternately, the hash pass of
-    // launch k on the set's own stream, overlapping the consensus kernels of the following launches
-    // (and, with more than two sets, the hash passes of other launches: bftsim_set_pipeline)
-    static constexpr uint32_t MAX_SETS = 8;
+    // Pipelined launches (bftsim_set_pipeline(h, D), the batch-throughput mode): a ring of D row-table sets,
+    // each with the scratch of one launch, so that up to D launches are in flight at once.
+    //   * the consensus kernel (+ resume + suffix rows) of each launch runs on one of `n_cs` launch streams
+    //     (round-robin), after the caller's earlier work on its stream and after its set's last chain;
+    //   * the prev_hash chains of `hash_batch` consecutive launches run as ONE chain kernel on one of `n_hs`
+    //     hash streams (round-robin). A chain is sequential in height and a launch's chains take ~1.5 ms
+    //     whatever their number, so batching B launches per kernel gives B times the chain throughput
+    //     (profiles/r04). Results are complete once bftsim_sync (or any fetch) returns; those flush a
+    //     partial batch first.
+    static constexpr uint32_t MAX_SETS = 8, MAX_CS = 4, MAX_HS = 4, MAX_BATCH = 4;
     struct RowSet {
         uint32_t* ch = nullptr; uint32_t* flags = nullptr; uint32_t* ticks = nullptr; uint64_t* views = nullptr;
         uint32_t* rec = nullptr; uint8_t* hash = nullptr;
         uint32_t* sfx = nullptr;      // header suffix rows of the hash pass (sfx_rows per instance)
-        // a launch's own scratch (set 0: the handle's buffers), so that launches on different sets may run
-        // their consensus kernels at the same time (concurrent mode)
+        // a launch's own scratch (set 0: the handle's buffers)
         uint64_t* hist = nullptr; uint32_t* rcs = nullptr; uint32_t* backlog = nullptr;
         uint32_t* resume = nullptr; uint32_t* save = nullptr; uint32_t* resume_q = nullptr;
         uint32_t* hint = nullptr;     // host-mapped: the hand-over count of the set's last launch (resume grid)
-        hipStream_t hs = nullptr;     // the set's stream: its hash passes (and, concurrent, whole launches)
         hipEvent_t done = nullptr;    // hash pass of the last launch that used the set
-        hipEvent_t entry = nullptr;   // concurrent mode: the caller's stream at the launch call
+        hipEvent_t entry = nullptr;   // the caller's stream at the launch call
         bool busy = false;
     } sets[MAX_SETS];
-    // concurrent mode (pipelined, the default there): every launch runs entirely on its set's stream, so
-    // the consensus kernels of consecutive launches overlap too (BFTSIM_TESTING + BFTSIM_SERIAL_CONSENSUS=1:
-    // the consensus kernels stay on the caller's stream, round-3 behaviour)
-    bool concurrent = true;
-    bool last_conc = false;           // the last launch ran on its set's stream
     // block-hash chains: one wave per instance (bft_hash_chain_wave_kernel) up to this many instances per
     // launch, lane pairs above. 0: lane pairs at every size -- the wave chain measured slower at every
     // shard size (ds_bpermute latency and LDS issue at low occupancy), kept as an A/B arm
@@ -424,15 +423,13 @@ struct bftsim {
     int pipeline = 0;                 // number of row-table sets (0: no pipelining)
     uint32_t sfx_rows = 0;            // heights per hash-pass chunk (0: no hash pass)
     uint32_t n_sets = 0, cur_set = 0;
-    hipStream_t hs = nullptr;         // the hash stream of the last pipelined launch
-    // concurrent mode: the consensus kernels (+ resume + suffix rows) of successive launches go round-robin
-    // over `n_cs` launch streams, the chains of each set on the set's own stream. A set is reused once its
-    // last chain is done; the chains (long, sequential in height) thus overlap up to the ring's depth while
-    // the consensus kernels only need a couple of streams (BFTSIM_TESTING + BFTSIM_LAUNCH_STREAMS=0: every
-    // stage of a launch on its set's stream)
-    static constexpr uint32_t MAX_CS = 4;
-    hipStream_t cs[MAX_CS] = {};
-    uint32_t n_cs = 2, cur_cs = 0;
+    bool last_pipe = false;           // the last launch ran on the launch streams
+    hipStream_t cs[MAX_CS] = {}, hstr[MAX_HS] = {};
+    uint32_t n_cs = 2, n_hs = 2, cur_cs = 0, cur_hs = 0;
+    uint32_t hash_batch = 4;          // launches per chain kernel (BFTSIM_TESTING + BFTSIM_HASH_BATCH overrides)
+    struct Pending { uint32_t set, ev; } pend[MAX_BATCH];
+    uint32_t n_pend = 0;
+    bft::Params batch_p{};            // the launch parameters of the pending batch (sizes, genesis, prio)
     // per-launch kernel timing: a ring of event quadruples, read by bftsim_kernel_ms_sum
     static constexpr uint32_t RING = 64;
     struct LaunchEv { hipEvent_t c0, c1, h0, h1, sx; bool has_hash, pending; } ring[RING] = {};
@@ -452,7 +449,7 @@ static int fail(bftsim* h, int code, const std::string& msg) {
     } while (0)
 
 static void use_set0_scratch(bftsim* h) {
-    // after a concurrent launch d_hist .. d_save point at that launch's set; set 0's are the handle's own
+    // after a pipelined launch d_hist .. d_save point at that launch's set; set 0's are the handle's own
     if (h->n_sets == 0 || !h->sets[0].hist) return;
     bftsim::RowSet& r = h->sets[0];
     h->d_hist = r.hist; h->d_rcs = r.rcs; h->d_backlog = r.backlog; h->d_resume = r.resume; h->d_save = r.save;
@@ -501,13 +498,15 @@ static void free_bufs(bftsim* h) {
     h->last_first = 0;
 }
 
+static int flush_batch(bftsim* h);
 static int sync_all(bftsim* h) {
     HIPCHECK(h, hipSetDevice(h->device));
+    if (int rc = flush_batch(h)) return rc;
     HIPCHECK(h, hipStreamSynchronize(h->last_stream));
-    for (uint32_t k = 0; k < bftsim::MAX_SETS; ++k)
-        if (h->sets[k].hs) HIPCHECK(h, hipStreamSynchronize(h->sets[k].hs));
     for (uint32_t k = 0; k < bftsim::MAX_CS; ++k)
         if (h->cs[k]) HIPCHECK(h, hipStreamSynchronize(h->cs[k]));
+    for (uint32_t k = 0; k < bftsim::MAX_HS; ++k)
+        if (h->hstr[k]) HIPCHECK(h, hipStreamSynchronize(h->hstr[k]));
     return BFTSIM_OK;
 }
 
@@ -703,10 +702,11 @@ void bftsim_destroy(bftsim_t* h) {
         if (h->sets[i].done) (void)hipEventDestroy(h->sets[i].done);
         if (h->sets[i].entry) (void)hipEventDestroy(h->sets[i].entry);
         if (h->sets[i].hint) (void)hipHostFree(h->sets[i].hint);
-        if (h->sets[i].hs) (void)hipStreamDestroy(h->sets[i].hs);
     }
     for (uint32_t i = 0; i < bftsim::MAX_CS; ++i)
         if (h->cs[i]) (void)hipStreamDestroy(h->cs[i]);
+    for (uint32_t i = 0; i < bftsim::MAX_HS; ++i)
+        if (h->hstr[i]) (void)hipStreamDestroy(h->hstr[i]);
     delete h;
 }
 
@@ -753,14 +753,17 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
     {
         const char* tst = getenv("BFTSIM_TESTING");
         const bool testing = tst && strcmp(tst, "1") == 0;
-        const char* ser = getenv("BFTSIM_SERIAL_CONSENSUS");
-        h->concurrent = !(testing && ser && strcmp(ser, "1") == 0);
         const char* cw = getenv("BFTSIM_CHAIN_WAVE_MAX");
         if (testing && cw) h->chain_wave_max = strtoull(cw, nullptr, 10);
         const char* cp = getenv("BFTSIM_CHAIN_PRIO");
         if (testing && cp) h->chain_prio = (uint32_t)atoi(cp);
-        const char* ls = getenv("BFTSIM_LAUNCH_STREAMS");
-        if (testing && ls) h->n_cs = (uint32_t)atoi(ls) < bftsim::MAX_CS ? (uint32_t)atoi(ls) : bftsim::MAX_CS;
+        auto knob = [&](const char* name, uint32_t& v, uint32_t lo, uint32_t hi) {
+            const char* e = getenv(name);
+            if (testing && e) { const uint32_t x = (uint32_t)atoi(e); v = x < lo ? lo : x > hi ? hi : x; }
+        };
+        knob("BFTSIM_LAUNCH_STREAMS", h->n_cs, 1, bftsim::MAX_CS);
+        knob("BFTSIM_HASH_STREAMS", h->n_hs, 1, bftsim::MAX_HS);
+        knob("BFTSIM_HASH_BATCH", h->hash_batch, 1, bftsim::MAX_BATCH);
     }
     const uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg, blocks = (n + per_block - 1) / per_block;
     for (uint32_t k = 1; k < (uint32_t)h->pipeline; ++k) {
@@ -772,7 +775,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         HIPCHECK(h, hipMalloc(&r.rec, n * h->hcap * 16));
         HIPCHECK(h, hipMalloc(&r.hash, n * h->hcap * 32));
         h->n_sets = k + 1;
-        if (h->concurrent) {
+        {
             HIPCHECK(h, hipMalloc(&r.hist, bft::HIST_BINS * sizeof(uint64_t)));
             HIPCHECK(h, hipMalloc(&r.rcs, blocks * bft::rcs_words(h->seg, h->rcs_k) * 4));
             if (h->d_backlog) HIPCHECK(h, hipMalloc(&r.backlog, h->backlog_bytes));
@@ -820,7 +823,7 @@ int bftsim_set_rcs_capacity(bftsim_t* h, uint32_t rounds) {
     if (!h) return BFTSIM_EINVAL;
     if (rounds < 1 || rounds > bft::RCS_MAX_K) return fail(h, BFTSIM_EINVAL, "RoundChangeSet capacity must be 1..4096");
     if (rounds == h->rcs_k) return BFTSIM_OK;
-    if (h->last_stream || h->hs) if (int rc = sync_all(h)) return rc;
+    if (h->last_stream) if (int rc = sync_all(h)) return rc;
     h->rcs_k = rounds;
     (void)hipSetDevice(h->device);
     free_bufs(h);                                   // the tables are re-sized by the next prepare
@@ -889,14 +892,13 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         HIPCHECK(h, hipMemsetAsync(h->d_trace, 0, tb, s));
     }
     bft::Params p = make_params(h, first, n);
-    const bool pipe = h->pipeline >= 2 && !p.need_seed && h->n_sets >= 2;
-    // concurrent: the whole launch on its set's stream (its own scratch); not with per-launch host state
-    // (traces, the crypto log, which the next calls read from the last launch alone)
-    const bool conc = pipe && h->concurrent && !h->h_trace && !p.mlog && h->sets[1].hist;
-    if (h->last_conc && !conc) {
-        // a launch on the caller's stream after concurrent ones: they may still use set 0's scratch
+    // pipelined: on the launch streams with the set's own scratch; not with per-launch host state (traces,
+    // the crypto log, which the next calls read from the last launch alone)
+    const bool pipe = h->pipeline >= 2 && !p.need_seed && h->n_sets >= 2 && !h->h_trace && !p.mlog;
+    if (h->last_pipe && !pipe) {
+        // a launch on the caller's stream after pipelined ones: they may still use set 0's scratch
         if (int rc = sync_all(h)) return rc;
-        h->last_conc = false;
+        h->last_pipe = false;
     }
     use_set0_scratch(h);
     p = make_params(h, first, n);
@@ -914,36 +916,28 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     }
 #endif
     if (pipe) {
-        // the next row-table set in the ring: the hash pass of the launch that used it last may still be
-        // reading it
+        // the next row-table set in the ring, once its last launch's chains are done (a launch of it still
+        // waiting in the hash batch is flushed first)
         h->cur_set = (h->cur_set + 1) % h->n_sets;
+        for (uint32_t i = 0; i < h->n_pend; ++i)
+            if (h->pend[i].set == h->cur_set) { if (int rc = flush_batch(h)) return rc; break; }
         bftsim::RowSet& r = h->sets[h->cur_set];
-        if (!r.hs) HIPCHECK(h, hipStreamCreateWithFlags(&r.hs, hipStreamNonBlocking));
-        if (conc) {
-            // after the caller's earlier work on its stream, and after the set's last chain
-            if (!r.entry) HIPCHECK(h, hipEventCreateWithFlags(&r.entry, hipEventDisableTiming));
-            HIPCHECK(h, hipEventRecord(r.entry, s));
-            hipStream_t ls = r.hs;
-            if (h->n_cs) {
-                h->cur_cs = (h->cur_cs + 1) % h->n_cs;
-                if (!h->cs[h->cur_cs]) HIPCHECK(h, hipStreamCreateWithFlags(&h->cs[h->cur_cs], hipStreamNonBlocking));
-                ls = h->cs[h->cur_cs];
-                if (r.busy) HIPCHECK(h, hipStreamWaitEvent(ls, r.done, 0));
-            }
-            HIPCHECK(h, hipStreamWaitEvent(ls, r.entry, 0));
-            s = ls;
-            h->d_hist = r.hist; h->d_rcs = r.rcs; h->d_backlog = r.backlog; h->d_resume = r.resume; h->d_save = r.save;
-            h->d_resume_q = r.resume_q;
-            p.hist = r.hist; p.rcs = r.rcs; p.backlog = r.backlog;
-            h->last_conc = true;
-        } else if (r.busy) {
-            HIPCHECK(h, hipStreamWaitEvent(s, r.done, 0));
-        }
+        if (!r.entry) HIPCHECK(h, hipEventCreateWithFlags(&r.entry, hipEventDisableTiming));
+        HIPCHECK(h, hipEventRecord(r.entry, s));
+        h->cur_cs = (h->cur_cs + 1) % h->n_cs;
+        if (!h->cs[h->cur_cs]) HIPCHECK(h, hipStreamCreateWithFlags(&h->cs[h->cur_cs], hipStreamNonBlocking));
+        hipStream_t ls = h->cs[h->cur_cs];
+        HIPCHECK(h, hipStreamWaitEvent(ls, r.entry, 0));
+        if (r.busy) HIPCHECK(h, hipStreamWaitEvent(ls, r.done, 0));
+        s = ls;
+        h->d_hist = r.hist; h->d_rcs = r.rcs; h->d_backlog = r.backlog; h->d_resume = r.resume; h->d_save = r.save;
+        h->d_resume_q = r.resume_q;
+        p.hist = r.hist; p.rcs = r.rcs; p.backlog = r.backlog;
         h->d_ch = r.ch; h->d_flags = r.flags; h->d_ticks = r.ticks; h->d_views = r.views;
         h->d_rec = r.rec; h->d_hash = r.hash;
         p.committed_height = h->d_ch; p.flags = h->d_flags; p.ticks = h->d_ticks; p.views = h->d_views;
         p.rec = h->d_rec; p.hash = h->d_hash;
-        h->hs = r.hs;
+        h->last_pipe = true;
     }
     bftsim::LaunchEv& ev = h->ring[h->ring_head % bftsim::RING];
     if (ev.pending) {                                    // 64 launches unread: fold the oldest in
@@ -992,37 +986,42 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     ev.has_hash = !p.need_seed;
     ev.pending = true;
     if (!p.need_seed) {
-        hipStream_t t = pipe ? h->sets[h->cur_set].hs : s;
         uint32_t* sfx = h->sets[pipe ? h->cur_set : 0].sfx;
         const uint32_t H = h->cfg.heights, K = h->sfx_rows;
-        // Where the suffix rows go depends on how long the consensus kernel runs against the chains
-        // (A/B, profiles/r03/ab_sfx): the N = 64 FAST kernel (~1.9 ms at 16,384 instances) is shorter than
-        // the chains, so a full-chip pass by a thread per (instance, height) runs on the launch stream
-        // right behind it (on a hash stream its waves take the next consensus kernel's slots: cfg3 6.3e8
-        // instead of 7.6e8; a thread per instance there lengthens the ring: 6.4e8). The general kernels
-        // (many instances per wave, or a workgroup per instance) run far longer than the chains: a
-        // thread per instance on the hash stream hides the rows entirely (cfg2 6.8e8 -> 7.9e8).
-        const bool on_launch = fast;
         const bool wave = n <= h->chain_wave_max;
-        if (K >= H && on_launch) {
-            HIPCHECK(h, hipEventRecord(ev.h0, s));
+        // Where the suffix rows go depends on how long the consensus kernel runs against the chains
+        // (A/B, profiles/r03/ab_sfx): the N = 64 FAST kernel is short, so a full-chip pass by a thread per
+        // (instance, height) runs on the launch stream right behind it; the general kernels run far longer
+        // than the chains, so a thread per instance over its heights runs on the hash stream beside them.
+        const bool on_launch = fast;
+        if (pipe && K >= H && on_launch) {
+            // suffix rows now; the chains in the next batch (flush_batch)
             HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, 1, K, sfx, false, s, p));
             HIPCHECK(h, hipEventRecord(ev.sx, s));
-            if (pipe && t != s) HIPCHECK(h, hipStreamWaitEvent(t, ev.sx, 0));
-            HIPCHECK(h, bft::launch_hash_chain((uint32_t)n, 1, K, sfx, wave, t, p));
+            ev.has_hash = false;                          // the batch's last launch carries the chain time
+            if (h->n_pend == 0) h->batch_p = p;
+            h->pend[h->n_pend++] = {h->cur_set, (h->ring_head - 1) % bftsim::RING};
+            if (h->n_pend >= h->hash_batch) if (int rc = flush_batch(h)) return rc;
         } else {
-            // chunks of K heights share the suffix rows: suffix and chain kernels in order on one stream
-            if (pipe && t != s) HIPCHECK(h, hipStreamWaitEvent(t, ev.c1, 0));
+            // one launch's hash pass: on a hash stream (pipelined) or the launch stream; chunks of K heights
+            // share the suffix rows (suffix and chain kernels in order on one stream)
+            hipStream_t t = s;
+            if (pipe) {
+                h->cur_hs = (h->cur_hs + 1) % h->n_hs;
+                if (!h->hstr[h->cur_hs]) HIPCHECK(h, hipStreamCreateWithFlags(&h->hstr[h->cur_hs], hipStreamNonBlocking));
+                t = h->hstr[h->cur_hs];
+                HIPCHECK(h, hipStreamWaitEvent(t, ev.c1, 0));
+            }
             HIPCHECK(h, hipEventRecord(ev.h0, t));
             for (uint32_t x0 = 1; x0 <= H; x0 += K) {
                 HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, x0, K, sfx, !on_launch, t, p));
                 HIPCHECK(h, bft::launch_hash_chain((uint32_t)n, x0, K, sfx, wave, t, p));
             }
-        }
-        HIPCHECK(h, hipEventRecord(ev.h1, t));
-        if (pipe) {
-            HIPCHECK(h, hipEventRecord(h->sets[h->cur_set].done, t));
-            h->sets[h->cur_set].busy = true;
+            HIPCHECK(h, hipEventRecord(ev.h1, t));
+            if (pipe) {
+                HIPCHECK(h, hipEventRecord(h->sets[h->cur_set].done, t));
+                h->sets[h->cur_set].busy = true;
+            }
         }
     }
     h->last_n = n;
@@ -1032,12 +1031,40 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     return BFTSIM_OK;
 }
 
+// the chains of the pending launches as one kernel on the next hash stream, after each launch's suffix rows
+static int flush_batch(bftsim* h) {
+    if (h->n_pend == 0) return BFTSIM_OK;
+    h->cur_hs = (h->cur_hs + 1) % h->n_hs;
+    if (!h->hstr[h->cur_hs]) HIPCHECK(h, hipStreamCreateWithFlags(&h->hstr[h->cur_hs], hipStreamNonBlocking));
+    hipStream_t t = h->hstr[h->cur_hs];
+    bft::ChainSets cs{};
+    cs.count = h->n_pend;
+    for (uint32_t i = 0; i < h->n_pend; ++i) {
+        HIPCHECK(h, hipStreamWaitEvent(t, h->ring[h->pend[i].ev].sx, 0));
+        const bftsim::RowSet& r = h->sets[h->pend[i].set];
+        cs.sfx[i] = r.sfx; cs.ch[i] = r.ch; cs.hash[i] = r.hash;
+    }
+    bftsim::LaunchEv& last = h->ring[h->pend[h->n_pend - 1].ev];
+    const bft::Params& p = h->batch_p;
+    HIPCHECK(h, hipEventRecord(last.h0, t));
+    HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, p.n_instances <= h->chain_wave_max, t, p));
+    HIPCHECK(h, hipEventRecord(last.h1, t));
+    last.has_hash = true;
+    for (uint32_t i = 0; i < h->n_pend; ++i) {
+        bftsim::RowSet& r = h->sets[h->pend[i].set];
+        HIPCHECK(h, hipEventRecord(r.done, t));
+        r.busy = true;
+    }
+    h->n_pend = 0;
+    return BFTSIM_OK;
+}
+
 int bftsim_set_pipeline(bftsim_t* h, int on) {
     if (!h) return BFTSIM_EINVAL;
     if (on < 0 || on > (int)bftsim::MAX_SETS) return fail(h, BFTSIM_EINVAL, "pipeline depth must be 0..8");
     const int depth = on == 0 ? 0 : on == 1 ? 2 : on;
     if (depth == h->pipeline) return BFTSIM_OK;
-    int rc = h->last_stream || h->hs ? sync_all(h) : BFTSIM_OK;
+    int rc = h->last_stream ? sync_all(h) : BFTSIM_OK;
     if (rc) return rc;
     h->pipeline = depth;
     (void)hipSetDevice(h->device);
@@ -1067,7 +1094,7 @@ int bftsim_kernel_ms_sum(bftsim_t* h, double* consensus_ms, double* hash_ms, uin
 
 int bftsim_sync(bftsim_t* h) {
     if (!h) return BFTSIM_EINVAL;
-    if (!h->last_stream && !h->hs) return BFTSIM_OK;
+    if (!h->last_stream) return BFTSIM_OK;
     return sync_all(h);
 }
 

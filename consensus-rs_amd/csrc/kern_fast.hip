@@ -146,17 +146,25 @@ __device__ inline void set_prio(uint32_t k) {      // s_setprio takes an immedia
     else if (k == 2u) __builtin_amdgcn_s_setprio(2);
     else if (k >= 3u) __builtin_amdgcn_s_setprio(3);
 }
-__global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params p) {
+// `cs`: the row-table sets of the launches whose chains this kernel runs (a launch's blocks are contiguous)
+__global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params p, ChainSets cs) {
     static_assert(CHAIN_PAIR_BLOCK == 64, "bft_hash_chain_kernel's barriers assume one-wave blocks");
 #if defined(__HIP_DEVICE_COMPILE__)
     set_prio(p.chain_prio);
+    {
+        const uint32_t bps = (p.n_instances + 31u) / 32u, k = blockIdx.x / bps;   // k < cs.count (grid)
+        p.sfx = const_cast<uint32_t*>(cs.sfx[k]);
+        p.committed_height = const_cast<uint32_t*>(cs.ch[k]);
+        p.hash = cs.hash[k];
+    }
+    const uint32_t blk = blockIdx.x % ((p.n_instances + 31u) / 32u);
     __shared__ __attribute__((aligned(16))) uint32_t sbuf[32 * SFX_BUF];      // splice buffer per pair
     __shared__ __attribute__((aligned(16))) uint64_t pbuf[64 * (PFX_WORDS + 4)];   // prefix per lane
     __shared__ PfxSel ptbl[16];                                                 // header_prefix_perm
     if (threadIdx.x < 16) ptbl[threadIdx.x] = PFX_TBL[threadIdx.x];
     __syncthreads();
     const uint32_t odd = threadIdx.x & 1u, pair = threadIdx.x >> 1;
-    const uint32_t il = blockIdx.x * 32u + pair;
+    const uint32_t il = blk * 32u + pair;
     if (il >= p.n_instances) return;                  // both lanes of a pair leave together
     const uint32_t K = p.sfx_rows, x0 = p.sfx_x0;
     const uint32_t ch = p.committed_height[il];
@@ -231,13 +239,17 @@ __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params
 // Small shards: the chain of one instance by one wave (bft_kwave.h kw50_chain). Workgroup b runs on XCD
 // b % 8 (round-robin dispatch): consecutive instances, whose suffix dwords share cache lines (rows are
 // dword-major across instances), are given to the same XCD.
-__global__ __launch_bounds__(64) void bft_hash_chain_wave_kernel(Params p) {
+__global__ __launch_bounds__(64) void bft_hash_chain_wave_kernel(Params p, ChainSets cs) {
     __shared__ __attribute__((aligned(16))) uint32_t sb[SFX_BUF];
     __shared__ __attribute__((aligned(16))) uint32_t pf[KW_PFX_DW];
     set_prio(p.chain_prio);
     const uint32_t lane = threadIdx.x;
-    const uint32_t per = gridDim.x >> 3;                  // gridDim.x = 8 * ceil(n / 8)
-    const uint32_t il = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+    const uint32_t bps = 8u * ((p.n_instances + 7u) / 8u), k = blockIdx.x / bps, b = blockIdx.x % bps;
+    p.sfx = const_cast<uint32_t*>(cs.sfx[k]);
+    p.committed_height = const_cast<uint32_t*>(cs.ch[k]);
+    p.hash = cs.hash[k];
+    const uint32_t per = bps >> 3;                        // bps = 8 * ceil(n / 8)
+    const uint32_t il = (b & 7u) * per + (b >> 3);
     if (il >= p.n_instances) return;                      // the whole wave
     const uint32_t K = p.sfx_rows, x0 = p.sfx_x0;
     const uint32_t ch = p.committed_height[il];
@@ -264,8 +276,18 @@ hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* s
     p.sfx = sfx;
     p.sfx_rows = rows;
     p.sfx_x0 = x0;
-    if (wave) hipLaunchKernelGGL(bft_hash_chain_wave_kernel, dim3(8u * ((n + 7u) / 8u)), dim3(64), 0, s, p);
-    else hipLaunchKernelGGL(bft_hash_chain_kernel, dim3((n + 31u) / 32u), dim3(CHAIN_PAIR_BLOCK), 0, s, p);
+    ChainSets cs{};
+    cs.count = 1; cs.sfx[0] = sfx; cs.ch[0] = p.committed_height; cs.hash[0] = p.hash;
+    if (wave) hipLaunchKernelGGL(bft_hash_chain_wave_kernel, dim3(8u * ((n + 7u) / 8u)), dim3(64), 0, s, p, cs);
+    else hipLaunchKernelGGL(bft_hash_chain_kernel, dim3((n + 31u) / 32u), dim3(CHAIN_PAIR_BLOCK), 0, s, p, cs);
+    return hipGetLastError();
+}
+hipError_t launch_hash_chain_batch(uint32_t n, const ChainSets& cs, bool wave, hipStream_t s, Params p) {
+    p.sfx_rows = p.heights;                               // every height in one chunk (bftsim.hip)
+    p.sfx_x0 = 1;
+    if (cs.count < 1 || cs.count > 4) return hipErrorInvalidValue;
+    if (wave) hipLaunchKernelGGL(bft_hash_chain_wave_kernel, dim3(cs.count * 8u * ((n + 7u) / 8u)), dim3(64), 0, s, p, cs);
+    else hipLaunchKernelGGL(bft_hash_chain_kernel, dim3(cs.count * ((n + 31u) / 32u)), dim3(CHAIN_PAIR_BLOCK), 0, s, p, cs);
     return hipGetLastError();
 }
 

@@ -17,15 +17,15 @@ def _sim(cfg):
 
 
 @pytest.mark.parametrize("depth", [2, 3, 4])
-@pytest.mark.parametrize("chain,serial,lstreams", [("wave", False, 2), ("pair", False, 2), ("pair", False, 1),
-                                                    ("pair", False, 0), ("wave", True, 2)])
-def test_pipelined_launches_match_oracle(depth, chain, serial, lstreams, monkeypatch):
-    """both chain kernels (one wave per instance below BFTSIM_CHAIN_WAVE_MAX, lane pairs above), with the
-    consensus kernels of consecutive launches concurrent (product: round-robin over launch streams, the chains
-    on the sets' streams; or every stage on the set's stream) or serial on the caller's stream"""
+@pytest.mark.parametrize("chain,batch,lstreams", [("wave", 4, 2), ("pair", 4, 2), ("pair", 1, 2), ("pair", 2, 1),
+                                                  ("pair", 3, 1)])
+def test_pipelined_launches_match_oracle(depth, chain, batch, lstreams, monkeypatch):
+    """both chain kernels (one wave per instance below BFTSIM_CHAIN_WAVE_MAX, lane pairs above); the consensus
+    kernels round-robin over launch streams, the chains of `batch` launches as one kernel on the hash
+    streams (a set still waiting in the batch when the ring comes back to it is flushed first: depth < batch)"""
     monkeypatch.setenv("BFTSIM_TESTING", "1")
     monkeypatch.setenv("BFTSIM_CHAIN_WAVE_MAX", "1000000" if chain == "wave" else "0")
-    monkeypatch.setenv("BFTSIM_SERIAL_CONSENSUS", "1" if serial else "0")
+    monkeypatch.setenv("BFTSIM_HASH_BATCH", str(batch))
     monkeypatch.setenv("BFTSIM_LAUNCH_STREAMS", str(lstreams))
     cfg = cfg3(heights=30)
     n = 64
