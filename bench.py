@@ -253,7 +253,10 @@ def main():
                     help="run each step's block-hash pass on the launch stream (no overlap across steps)")
     ap.add_argument("--pipeline-depth", type=int, default=None,
                     help="launches in flight (bftsim_set_pipeline: a ring of row-table sets, each launch on its set's "
-                         "stream). Default: 4 at >= 12,288 instances per GPU, 6 below (profiles/r04/ab_depth_queues)")
+                         "stream). Default: 6 at >= 12,288 instances per GPU, 8 below (profiles/r04/ab_hash_batch)")
+    ap.add_argument("--hash-batch", type=int, default=None,
+                    help="launches whose block-hash chains run as one kernel (bftsim_set_hash_batch). Default: 2 at "
+                         ">= 12,288 instances per GPU, 4 below (profiles/r04/ab_hash_batch)")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (HIP's default is 4): every set's stream needs its own "
                          "hardware queue, or launches serialize behind each other (profiles/r04/ab_depth_queues); "
@@ -335,8 +338,11 @@ def main():
         first = rank * I
     auto_depth = args.pipeline_depth is None
     if auto_depth:
-        args.pipeline_depth = 4 if I >= 12_288 else 6
+        args.pipeline_depth = 6 if I >= 12_288 else 8
+    if args.hash_batch is None:
+        args.hash_batch = 2 if I >= 12_288 else 4
     sim.set_pipeline(pipelined, args.pipeline_depth)
+    sim.set_hash_batch(args.hash_batch)
     if c5:
         sim.set_window(args.window)
     sim.prepare(I)
@@ -398,7 +404,8 @@ def main():
     if args.scaling == "strong" and world > 1:
         Iw, first_w = args.instances, rank * args.instances
         if auto_depth:
-            sim.set_pipeline(pipelined, 4 if Iw >= 12_288 else 6)
+            sim.set_pipeline(pipelined, 6 if Iw >= 12_288 else 8)
+            sim.set_hash_batch(2 if Iw >= 12_288 else 4)
         sim.prepare(Iw)
         for _ in range(max(args.warmup, 1)):
             sim.launch(first_w, stream)
@@ -464,6 +471,7 @@ def main():
                 "seed_byte_order": "le" if cfg.seed_byte_order else "be",
                 "heights": args.heights, "parallelism": f"instance-sharded x{world}",
                 "pipelined": pipelined, "pipeline_depth": args.pipeline_depth if pipelined else 0,
+                "hash_batch": args.hash_batch if pipelined else 0,
                 "instance_rounds_per_step": views_all,
                 "stats_allreduce": reduce_via,
                 "committed_heights_per_step": heights_all,

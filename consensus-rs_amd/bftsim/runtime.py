@@ -70,6 +70,7 @@ def lib():
         L.bftsim_kernel_ms_sum.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]
         L.bftsim_set_pipeline.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.bftsim_set_hash_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         L.bftsim_set_fast.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.bftsim_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
         L.bftsim_set_window.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
@@ -244,6 +245,10 @@ class Simulator:
         """Batch throughput mode: a ring of `depth` row-table sets; the hash pass of each launch overlaps
         the following launches (include/bftsim.h bftsim_set_pipeline)."""
         _check(self.h, lib().bftsim_set_pipeline(self.h, depth if on else 0), "bftsim_set_pipeline")
+
+    def set_hash_batch(self, launches: int):
+        """Pipelined launches: the chains of this many consecutive launches as one kernel (include/bftsim.h)."""
+        _check(self.h, lib().bftsim_set_hash_batch(self.h, launches), "bftsim_set_hash_batch")
 
     @staticmethod
     def _stats_dict(s):

@@ -270,7 +270,10 @@ struct Fast64 {
         const uint32_t lat = (uint32_t)tick - canon_tick;
         views_acc += cnt;
         if (me == 0) {                                           // one lane: latency histogram and the ring row
-            wv.lds_add((uint32_t*)(lds + F64Layout::LAT_OFF) + (lat < 64u ? lat : 64u), cnt);
+            // the wave's own LDS histogram, one writer: a plain read-modify-write (an atomic becomes a
+            // scalar loop over the active lanes)
+            uint32_t* lb = (uint32_t*)(lds + F64Layout::LAT_OFF) + (lat < 64u ? lat : 64u);
+            *lb += cnt;
             uint32_t* r = ring_row(x);
             r[0] = 0; r[1] = blk_prop(b) | (blk_var(b) << 16) | (1u << 24); r[2] = blk_T(b); r[3] = 0;   // seed: hash_pending
         }
@@ -704,11 +707,15 @@ struct Fast64 {
         uint32_t* c1 = cache_p(2);                                  // Prepare
         uint32_t* c2 = cache_p(4);                                  // Commit
         const uint32_t hd = (H & 0x3fffffu) | 0x80000000u;          // blk_d32 of (H, proposer 0, variant 0)
+        // integer form (one compare per lane, no lane-mask arithmetic on the scalar unit): a nonzero word
+        // marks a validator that is not where the previous canonical tick left it; heights are < 2^22, so
+        // ((a ^ b) - 1) >> 31 is 1 exactly when a == b
         const uint32_t pc_h = pc[0], pc_d = pc[64];
-        const bool pp_hit = (me == 0u) & (pc_d != 0u) & (pc_h == H) & (pc_d == hd);   // out_preprepare's cache
-        const bool ok = ((fl & (L_DEAD | L_SYNCP)) == 0u) & (wake_tick == t) & (miner_queue == 0u) & (nxf == 0u) &
-                        (last == canon_h) & (mint_height == H) & (c1[0] != H) & (c2[0] != H) & !pp_hit;
-        if (ballot(!ok) != 0) return false;
+        const uint32_t pp_hit = (((pc_h ^ H) | (pc_d ^ hd) | me) == 0u) ? 1u : 0u;   // out_preprepare's cache
+        const uint32_t bad = (fl & (L_DEAD | L_SYNCP)) | ((uint32_t)wake_tick ^ (uint32_t)t) | miner_queue | nxf |
+                             (last ^ canon_h) | (mint_height ^ H) | (((c1[0] ^ H) - 1u) >> 31) |
+                             (((c2[0] ^ H) - 1u) >> 31) | pp_hit;
+        if (ballot(bad != 0u) != 0) return false;
         // canonical_step's split and quorum decision (the proposer's F_PP_EQ = it is Byzantine)
         uint64_t v1m = 0;
         if (byz_mask & 1ull) {

@@ -763,7 +763,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         };
         knob("BFTSIM_LAUNCH_STREAMS", h->n_cs, 1, bftsim::MAX_CS);
         knob("BFTSIM_HASH_STREAMS", h->n_hs, 1, bftsim::MAX_HS);
-        knob("BFTSIM_HASH_BATCH", h->hash_batch, 1, bftsim::MAX_BATCH);
+        knob("BFTSIM_HASH_BATCH", h->hash_batch, 1, bftsim::MAX_BATCH);   // A/B arms (bftsim_set_hash_batch)
     }
     const uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg, blocks = (n + per_block - 1) / per_block;
     for (uint32_t k = 1; k < (uint32_t)h->pipeline; ++k) {
@@ -1056,6 +1056,14 @@ static int flush_batch(bftsim* h) {
         r.busy = true;
     }
     h->n_pend = 0;
+    return BFTSIM_OK;
+}
+
+int bftsim_set_hash_batch(bftsim_t* h, uint32_t launches) {
+    if (!h) return BFTSIM_EINVAL;
+    if (launches < 1 || launches > bftsim::MAX_BATCH) return fail(h, BFTSIM_EINVAL, "hash batch must be 1..4 launches");
+    if (int rc = flush_batch(h)) return rc;
+    h->hash_batch = launches;
     return BFTSIM_OK;
 }
 
