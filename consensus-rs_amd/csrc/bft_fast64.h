@@ -675,13 +675,14 @@ struct Fast64 {
     }
 
     // ------------------------------------------------------------------ the canonical tick, composed
-    // Lossless schedule, big-endian seeds (proposer 0). When a tick starts with every validator where the
+    // Lossless schedule; proposer j = 0 (big-endian seeds) or seed(tip) mod 64 (little-endian, SEEDED: the
+    // new height is hashed by the wave as resolve_commits does). When a tick starts with every validator where the
     // previous canonical height left it -- its seal waking now for height H = canon_h + 1 (wake_tick ==
     // tick, mint_height == H, chain tip H - 1), nothing in flight or queued -- the whole tick has one
     // outcome, and this applies it to every lane's registers at once:
     //   T-step  — the seal wakes (minner/mod.rs:95-143 → core.rs:154-163): start_new_zero_round
     //             (core.rs:441-470) for everyone, the own candidate accepted as the pending request
-    //             (request.rs:19-42), validator 0 sends its Preprepare (preprepare.rs:30-43); no timer fires
+    //             (request.rs:19-42), validator j sends its Preprepare (preprepare.rs:30-43); no timer fires
     //             (start_new_zero_round re-arms it first) and no miner event is queued;
     //   PP, PC1, PC2 — canonical_step (above);
     //   commit  — resolve_commits records height H (one digest among the committers);
@@ -701,34 +702,38 @@ struct Fast64 {
         const uint32_t H = canon_h + 1u;
         if (frozen | (H >= P.hcap) | (P.phase_cap < 5u)) return false;
         const int32_t t = tick;
-        const uint32_t ptout = uni(rl(cand_T, 0));                  // the proposer's block time tick
+        // the round-0 proposer of H: validator 0 with big-endian seeds, seed(tip) mod 64 with little-endian
+        // ones (start_new_zero_round_p: the seed of block H - 1 = the canonical tip)
+        const uint32_t j = SEEDED ? (canon_seed & 63u) : 0u;
+        const uint32_t ptout = uni(rl(cand_T, j));                  // the proposer's block time tick
         if ((int32_t)ptout < t) return false;
         uint32_t* pc = cache_p(0);                                  // Preprepare {h, d32}
         uint32_t* c1 = cache_p(2);                                  // Prepare
         uint32_t* c2 = cache_p(4);                                  // Commit
-        const uint32_t hd = (H & 0x3fffffu) | 0x80000000u;          // blk_d32 of (H, proposer 0, variant 0)
+        const uint32_t hd = (H & 0x3fffffu) | (j << 22) | 0x80000000u;   // blk_d32 of (H, proposer j, variant 0)
         // integer form (one compare per lane, no lane-mask arithmetic on the scalar unit): a nonzero word
         // marks a validator that is not where the previous canonical tick left it; heights are < 2^22, so
         // ((a ^ b) - 1) >> 31 is 1 exactly when a == b
         const uint32_t pc_h = pc[0], pc_d = pc[64];
-        const uint32_t pp_hit = (((pc_h ^ H) | (pc_d ^ hd) | me) == 0u) ? 1u : 0u;   // out_preprepare's cache
+        const uint32_t pp_hit = (((pc_h ^ H) | (pc_d ^ hd) | (me ^ j)) == 0u) ? 1u : 0u;   // out_preprepare's cache
         const uint32_t bad = (fl & (L_DEAD | L_SYNCP)) | ((uint32_t)wake_tick ^ (uint32_t)t) | miner_queue | nxf |
                              (last ^ canon_h) | (mint_height ^ H) | (((c1[0] ^ H) - 1u) >> 31) |
                              (((c2[0] ^ H) - 1u) >> 31) | pp_hit;
         if (ballot(bad != 0u) != 0) return false;
         // canonical_step's split and quorum decision (the proposer's F_PP_EQ = it is Byzantine)
         uint64_t v1m = 0;
-        if (byz_mask & 1ull) {
+        if ((byz_mask >> j) & 1ull) {
             const uint64_t d = split_mask(H);
-            v1m = ((uint64_t)uni((uint32_t)d) | ((uint64_t)uni((uint32_t)(d >> 32)) << 32)) & ~1ull;
+            v1m = ((uint64_t)uni((uint32_t)d) | ((uint64_t)uni((uint32_t)(d >> 32)) << 32)) & ~(1ull << j);
         }
         const uint64_t hon = ~byz_mask;
         const bool k0 = popc(byz_mask | (hon & ~v1m)) > Q, k1 = popc(byz_mask | (hon & v1m)) > Q;
         if (k0 == k1) return false;
-        // T-step: the pending request and validator 0's Preprepare through its outbound cache
+        // T-step: the pending request and the proposer's Preprepare through its outbound cache
         *lane_p(F64Layout::W_PENDT) = cand_T;
-        if (me == 0u) { pc[0] = H; pc[64] = hd; }
+        if (me == j) { pc[0] = H; pc[64] = hd; }
         pp_T_out = ptout;
+        if (SEEDED) prop_l = j;
         // PP, PC1, PC2 (canonical_step) and the block phases: the per-lane result
         const bool var = ((v1m >> me) & 1ull) != 0;
         const bool fires = var == k1;
@@ -736,7 +741,7 @@ struct Fast64 {
         c1[0] = H; c1[64] = d32;
         c2[0] = H; c2[64] = d32;
         h = H;
-        pp = blk_make(H, 0u, var ? 1u : 0u, ptout);
+        pp = blk_make(H, j, var ? 1u : 0u, ptout);
         prep = ~0ull;
         comm = byz_mask | (hon & (var ? v1m : ~v1m));
         fl = (fl & ~(L_ST | L_WAIT | L_LOCK | L_PENDV | L_CMT)) | L_PROP | L_PENDV | L_LOCK |
@@ -751,7 +756,8 @@ struct Fast64 {
         nxf = 0;
         nx_blo = H;
         nx_bhi = H;
-        record_canon(H, blk_make(H, 0u, k1 ? 1u : 0u, ptout));
+        record_canon(H, blk_make(H, j, k1 ? 1u : 0u, ptout));
+        if (SEEDED) hash_pending();                                 // resolve_commits: hash (and seed) of H
         return true;
     }
 
@@ -825,10 +831,10 @@ struct Fast64 {
         bool bailed = false;
         for (tick = 0; tick < (int32_t)P.max_ticks; ++tick) {
             if (seg_done) break;
-            // a run of canonical ticks (lossless, big-endian seeds): T-step and phases in one closed form each,
+            // a run of canonical ticks (lossless schedules): T-step and phases in one closed form each,
             // in a loop of its own (few live values: no copies of the whole state at every branch); the first
             // tick that is not canonical falls through to the T-step and phase loop below, unchanged
-            if (!LOSSY && !SEEDED && macro_ok && tick != 0) {
+            if (!LOSSY && macro_ok && tick != 0) {
                 bool stop = false;
                 while (canonical_tick()) {
                     F64_STAMP(1);

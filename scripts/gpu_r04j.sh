@@ -16,6 +16,7 @@ for r in 1 2; do
   for B in 2 3 4; do for D in 6 8; do BARGS="--hash-batch $B --pipeline-depth $D" run c16k_b${B}_d${D}_r$r; done; done
 done
 for I in 2048 4096 8192; do BARGS="--instances $I" run c$I; done
+BARGS="--seed-order le --steps 10" run cfg3_le
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -s KILL 180 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU -d $O/sq -o run --output-format csv -- python3 bench.py --no-pipeline --steps 5 --warmup 2 --no-cpu > $O/sq.json 2> $O/sq.err || exit 1
 python3 - <<'PY'

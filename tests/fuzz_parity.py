@@ -22,7 +22,8 @@ def random_config(rng, big=False, n64=False, replay=False, le=False, lossless=Fa
         heights = rng.choice([5, 20, 70, 130])
         return BftConfig(n=n, heights=heights, seed=rng.randrange(1 << 40), byz_count=byz, phase_cap=cap,
                          silent=silent, max_ticks=heights * rng.choice([1, 2, 4]) + rng.choice([0, 1, 16]),
-                         name=f"lossless-b{byz}-cap{cap}-s{len(silent)}-h{heights}")
+                         seed_byte_order=1 if le else 0,
+                         name=f"lossless-b{byz}-cap{cap}-s{len(silent)}-h{heights}{'-le' if le else ''}")
     if n64:                              # the FAST kernel (bft_fast64.h) and its hand-overs
         n = 64
     elif big:
