@@ -735,7 +735,10 @@ struct Fast64 {
         pp_T_out = ptout;
         if (SEEDED) prop_l = j;
         // PP, PC1, PC2 (canonical_step) and the block phases: the per-lane result
-        const bool var = ((v1m >> me) & 1ull) != 0;
+        // this lane's bit of the uniform mask from its 32-bit half (a 64-bit per-lane 1 << me would be one
+        // more register pair, spilled at 6 waves per SIMD and reloaded on every tick)
+        const uint32_t vw = me < 32u ? (uint32_t)v1m : (uint32_t)(v1m >> 32);
+        const bool var = ((vw >> (me & 31u)) & 1u) != 0u;
         const bool fires = var == k1;
         const uint32_t d32 = hd | (var ? (1u << 30) : 0u);
         c1[0] = H; c1[64] = d32;

@@ -8,7 +8,7 @@ namespace bft {
 // FAST kernel (N = 64, big-endian seeds): the closed-form phases only (bft_fast64.h); instances
 // needing the general path are saved for the resume kernel
 #ifndef BFT_FAST_WAVES_PER_SIMD
-#define BFT_FAST_WAVES_PER_SIMD 6   // measured best of 4..8 (profiles/r02: 4 → 3.86e8, 5 → 3.97e8, 6 → 4.17e8, 7 → 3.69e8)
+#define BFT_FAST_WAVES_PER_SIMD 4   // 110 VGPRs, no scratch; since the canonical tick 4, 5 and 6 (80 VGPRs, 76-88 B/lane of spills) measure the same (profiles/r04/ab_occupancy)
 #endif
 #ifndef BFT_FAST_SEEDED_WAVES_PER_SIMD
 #define BFT_FAST_SEEDED_WAVES_PER_SIMD 4   // the in-kernel wave hash needs registers: 5 spills to scratch (gpurun r03c: 4 waves +6 %)
