@@ -92,14 +92,16 @@ VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2   # wave64 VALU instructions/s: one per 2 
 SALU_ISSUE_PEAK = 256 * 2.4e9           # scalar instructions/s: one scalar unit per CU, one per cycle
 
 
-def pmc_issue(workload: str = "cfg3"):
-    """Per dispatch VALU / SALU wave-instructions of the consensus kernel from the newest PMC
-    summary of this workload (SQ_INSTS_VALU, SQ_INSTS_SALU of scripts/gpu_profile.sh's SQ pass), or None."""
+def pmc_issue(workload: str = "cfg3", kernel: str = "bft_consensus_kernel"):
+    """Per dispatch VALU / SALU wave-instructions of a kernel (the consensus kernel: its FAST body) from the
+    newest PMC summary of this workload (SQ_INSTS_VALU, SQ_INSTS_SALU of scripts/gpu_profile.sh's SQ pass),
+    or None."""
     files = _pmc_files(workload)
     if not files:
         return None
     k = json.load(open(files[-1])).get("kernels", {})
-    e = k.get("bft_consensus_fast_kernel") or k.get("bft_consensus_kernel") or {}
+    e = ((k.get("bft_consensus_fast_kernel") or k.get("bft_consensus_kernel") or {}) if kernel == "bft_consensus_kernel"
+         else k.get(kernel) or {})
     if "SQ_INSTS_VALU" not in e:
         return None
     return {"valu": e["SQ_INSTS_VALU"], "salu": e.get("SQ_INSTS_SALU")}
@@ -426,14 +428,15 @@ def main():
         h_ops = HEADER_HASH_OPS * st["committed_heights"]
         if c5 or cfg.seed_byte_order or (cfg.n & (cfg.n - 1)):   # block hashes inside the consensus kernel
             c_ops, h_ops = c_ops + h_ops, 0
-        # the dominant kernel is the one on the step's critical path: the consensus kernel, unless the
-        # block-hash pass runs serially after it (no pipeline) and takes longer. A pipelined hash pass runs
-        # on its own stream beside the next launches' consensus kernels at lower priority, so its
-        # (stretched) duration is not step time.
-        if cms >= hms or (pipelined and h_ops):
+        # the dominant kernel is the one with the larger device time per launch: the consensus kernel (FAST +
+        # resume, HIP events c0..c1 per launch) or the prev_hash chains (events around each chain dispatch;
+        # pipelined, one dispatch hashes `hash_batch` launches and its time is shared among them). Launches
+        # overlap when pipelined, so these are stretched durations, as rocprof reports them.
+        batch = args.hash_batch if (pipelined and h_ops) else 1
+        if cms >= hms:
             dom, ops, ms = "bft_consensus_kernel", c_ops, cms
         else:
-            dom, ops, ms = "bft_hash_kernel", h_ops, hms
+            dom, ops, ms = "bft_hash_chain_kernel", h_ops * batch, hms * batch   # per chain dispatch
         achieved = ops / (ms / 1e3) / 1e12
         peak = VALU_PEAK / 1e12
         pmc_key = f"cfg4_n{cfg.n}" if wl == "cfg4" else wl
@@ -485,18 +488,19 @@ def main():
                 "traffic": (traffic or {}).get(dom),
                 # what the hardware issues, beside the algorithmic model: VALU wave-instructions of
                 # the profiled launch (PMC) per second of this run's kernel time vs the issue peak
-                "issue": (lambda q: None if q is None or dom != "bft_consensus_kernel" else {
+                "issue": (lambda q: None if q is None else {
                     "valu_wave_instr_per_launch": q["valu"], "salu_wave_instr_per_launch": q["salu"],
                     "valu_per_s": q["valu"] / (ms / 1e3), "valu_peak_per_s": VALU_ISSUE_PEAK,
                     "valu_frac": q["valu"] / (ms / 1e3) / VALU_ISSUE_PEAK,
                     "salu_per_s": q["salu"] / (ms / 1e3), "salu_peak_per_s": SALU_ISSUE_PEAK,
                     "salu_frac": q["salu"] / (ms / 1e3) / SALU_ISSUE_PEAK,
-                    "per_instance_round": {"valu": q["valu"] / max(views_rank, 1),
-                                           "salu": q["salu"] / max(views_rank, 1)}})(pmc_issue(pmc_key)),
+                    "per_instance_round": {"valu": q["valu"] / max(views_rank * batch, 1),
+                                           "salu": q["salu"] / max(views_rank * batch, 1)}})(pmc_issue(pmc_key, dom)),
+                "dispatch": {"launches_per_dispatch": batch, "ops_per_dispatch": ops, "ms_per_dispatch": ms},
                 "traffic_source": traffic_src,
                 "hbm": {"algorithmic_bytes": algo_bytes, "achieved_GBps": algo_bytes / (ms / 1e3) / 1e9,
                         "peak_GBps": HBM_PEAK / 1e9, "frac": algo_bytes / (ms / 1e3) / HBM_PEAK},
-                "kernel_ms": {"bft_consensus_kernel": cms, "bft_hash_kernel": hms},
+                "kernel_ms": {"bft_consensus_kernel": cms, "bft_hash_kernel": hms},   # per launch
                 # both kernels' fractions, whichever is dominant, and the whole step against the full
                 # per-instance-round model (consensus + one header hash per committed height). The hash
                 # pass's own time is exclusive only with --no-pipeline (pipelined, it runs beside the
