@@ -208,12 +208,13 @@ hipError_t launch_hash_suffix(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* 
                               Params p);
 // `wave`: one wave per instance (bft_hash_chain_wave_kernel, small shards) instead of a lane pair
 hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, bool wave, hipStream_t s, Params p);
-// the chains of up to 4 launches (row-table sets) of n instances each, heights 1..H, as one kernel
+// the chains of up to CHAIN_MAX_SETS launches (row-table sets) of n instances each, heights 1..H, as one kernel
+constexpr uint32_t CHAIN_MAX_SETS = 8;
 struct ChainSets {
     uint32_t count;
-    const uint32_t* sfx[4];
-    const uint32_t* ch[4];
-    uint8_t* hash[4];
+    const uint32_t* sfx[CHAIN_MAX_SETS];
+    const uint32_t* ch[CHAIN_MAX_SETS];
+    uint8_t* hash[CHAIN_MAX_SETS];
 };
 hipError_t launch_hash_chain_batch(uint32_t n, const ChainSets& cs, bool wave, hipStream_t s, Params p);
 hipError_t launch_resume(dim3 grid, size_t lds, hipStream_t s, const Params& p);  // kern_resume.hip

@@ -401,7 +401,7 @@ struct bftsim {
     //     whatever their number, so batching B launches per kernel gives B times the chain throughput
     //     (profiles/r04). Results are complete once bftsim_sync (or any fetch) returns; those flush a
     //     partial batch first.
-    static constexpr uint32_t MAX_SETS = 8, MAX_CS = 4, MAX_HS = 4, MAX_BATCH = 4;
+    static constexpr uint32_t MAX_SETS = 16, MAX_CS = 4, MAX_HS = 4, MAX_BATCH = bft::CHAIN_MAX_SETS;
     struct RowSet {
         uint32_t* ch = nullptr; uint32_t* flags = nullptr; uint32_t* ticks = nullptr; uint64_t* views = nullptr;
         uint32_t* rec = nullptr; uint8_t* hash = nullptr;
@@ -762,7 +762,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
             if (testing && e) { const uint32_t x = (uint32_t)atoi(e); v = x < lo ? lo : x > hi ? hi : x; }
         };
         knob("BFTSIM_LAUNCH_STREAMS", h->n_cs, 1, bftsim::MAX_CS);
-        knob("BFTSIM_HASH_STREAMS", h->n_hs, 1, bftsim::MAX_HS);
+        knob("BFTSIM_HASH_STREAMS", h->n_hs, 1, bftsim::MAX_HS);   // A/B arms
         knob("BFTSIM_HASH_BATCH", h->hash_batch, 1, bftsim::MAX_BATCH);   // A/B arms (bftsim_set_hash_batch)
     }
     const uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg, blocks = (n + per_block - 1) / per_block;
@@ -1061,7 +1061,7 @@ static int flush_batch(bftsim* h) {
 
 int bftsim_set_hash_batch(bftsim_t* h, uint32_t launches) {
     if (!h) return BFTSIM_EINVAL;
-    if (launches < 1 || launches > bftsim::MAX_BATCH) return fail(h, BFTSIM_EINVAL, "hash batch must be 1..4 launches");
+    if (launches < 1 || launches > bftsim::MAX_BATCH) return fail(h, BFTSIM_EINVAL, "hash batch must be 1..8 launches");
     if (int rc = flush_batch(h)) return rc;
     h->hash_batch = launches;
     return BFTSIM_OK;
@@ -1069,7 +1069,7 @@ int bftsim_set_hash_batch(bftsim_t* h, uint32_t launches) {
 
 int bftsim_set_pipeline(bftsim_t* h, int on) {
     if (!h) return BFTSIM_EINVAL;
-    if (on < 0 || on > (int)bftsim::MAX_SETS) return fail(h, BFTSIM_EINVAL, "pipeline depth must be 0..8");
+    if (on < 0 || on > (int)bftsim::MAX_SETS) return fail(h, BFTSIM_EINVAL, "pipeline depth must be 0..16");
     const int depth = on == 0 ? 0 : on == 1 ? 2 : on;
     if (depth == h->pipeline) return BFTSIM_OK;
     int rc = h->last_stream ? sync_all(h) : BFTSIM_OK;

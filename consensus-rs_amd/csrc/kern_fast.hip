@@ -285,7 +285,7 @@ hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* s
 hipError_t launch_hash_chain_batch(uint32_t n, const ChainSets& cs, bool wave, hipStream_t s, Params p) {
     p.sfx_rows = p.heights;                               // every height in one chunk (bftsim.hip)
     p.sfx_x0 = 1;
-    if (cs.count < 1 || cs.count > 4) return hipErrorInvalidValue;
+    if (cs.count < 1 || cs.count > CHAIN_MAX_SETS) return hipErrorInvalidValue;
     if (wave) hipLaunchKernelGGL(bft_hash_chain_wave_kernel, dim3(cs.count * 8u * ((n + 7u) / 8u)), dim3(64), 0, s, p, cs);
     else hipLaunchKernelGGL(bft_hash_chain_kernel, dim3(cs.count * ((n + 31u) / 32u)), dim3(CHAIN_PAIR_BLOCK), 0, s, p, cs);
     return hipGetLastError();

@@ -51,6 +51,27 @@ def test_pipelined_launches_match_oracle(depth, chain, batch, lstreams, monkeypa
     assert st["views"] == int(ref["views"].sum())
 
 
+@pytest.mark.parametrize("depth,batch,hstreams", [(16, 8, 3), (5, 8, 2), (12, 6, 4)])
+def test_deep_ring_and_large_hash_batches(depth, batch, hstreams, monkeypatch):
+    """rings up to 16 sets and chain kernels over up to 8 launches (a set still waiting in the batch when the
+    ring comes back to it is flushed first: depth 5 < batch 8), 20 launches of the same instances"""
+    monkeypatch.setenv("BFTSIM_TESTING", "1")
+    monkeypatch.setenv("BFTSIM_HASH_STREAMS", str(hstreams))
+    cfg = cfg3(heights=30)
+    n = 96
+    sim = _sim(cfg)
+    try:
+        sim.set_pipeline(True, depth)
+        sim.set_hash_batch(batch)
+        sim.prepare(n)
+        for k in range(20):
+            sim.launch(k * n)
+        got = sim.fetch()
+    finally:
+        sim.close()
+    assert_same(O.run(cfg, 19 * n, n), got, f"depth {depth} batch {batch}")
+
+
 def test_pipeline_toggle_and_sizes():
     cfg = BftConfig(n=16, heights=20, seed=21, drop_ppm=100_000)
     sim = _sim(cfg)
