@@ -255,10 +255,10 @@ def main():
                     help="run each step's block-hash pass on the launch stream (no overlap across steps)")
     ap.add_argument("--pipeline-depth", type=int, default=None,
                     help="launches in flight (bftsim_set_pipeline: a ring of row-table sets, each launch on its set's "
-                         "stream). Default: 6 at >= 12,288 instances per GPU, 8 below (profiles/r04/ab_hash_batch)")
+                         "stream). Default: 6 at >= 12,288 instances per GPU, 16 below (profiles/r04/ab_deep_ring)")
     ap.add_argument("--hash-batch", type=int, default=None,
                     help="launches whose block-hash chains run as one kernel (bftsim_set_hash_batch, 1..8). Default: 2 "
-                         "at >= 12,288 instances per GPU, 4 below (profiles/r04/ab_hash_batch)")
+                         "at >= 12,288 instances per GPU, 8 below (profiles/r04/ab_deep_ring)")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (HIP's default is 4): every set's stream needs its own "
                          "hardware queue, or launches serialize behind each other (profiles/r04/ab_depth_queues); "
@@ -340,9 +340,9 @@ def main():
         first = rank * I
     auto_depth = args.pipeline_depth is None
     if auto_depth:
-        args.pipeline_depth = 6 if I >= 12_288 else 8
+        args.pipeline_depth = 6 if I >= 12_288 else 16
     if args.hash_batch is None:
-        args.hash_batch = 2 if I >= 12_288 else 4
+        args.hash_batch = 2 if I >= 12_288 else 8
     sim.set_pipeline(pipelined, args.pipeline_depth)
     sim.set_hash_batch(args.hash_batch)
     if c5:
@@ -406,8 +406,8 @@ def main():
     if args.scaling == "strong" and world > 1:
         Iw, first_w = args.instances, rank * args.instances
         if auto_depth:
-            sim.set_pipeline(pipelined, 6 if Iw >= 12_288 else 8)
-            sim.set_hash_batch(2 if Iw >= 12_288 else 4)
+            sim.set_pipeline(pipelined, 6 if Iw >= 12_288 else 16)
+            sim.set_hash_batch(2 if Iw >= 12_288 else 8)
         sim.prepare(Iw)
         for _ in range(max(args.warmup, 1)):
             sim.launch(first_w, stream)
