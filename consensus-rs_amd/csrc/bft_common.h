@@ -84,6 +84,8 @@ struct Params {
     uint32_t chain_prio;              // s_setprio of the block-hash chain waves (0..3)
     uint32_t rcs_k;                   // RoundChangeSet rounds per validator (bftsim_set_rcs_capacity)
     uint32_t pad5;
+    // little-endian seeds, N = 64: the predicted canonical blocks (bft_seed_chain_kernel; nullptr: none)
+    uint32_t* spec;                   // [heights + 1][n_inst] spec_word or 0
 };
 constexpr uint32_t RCS_DEFAULT_K = 16, RCS_MAX_K = 4096;
 // one logged broadcast: {tick, phase | code << 8 | sender << 16, height, round, block id lo, hi,
@@ -287,6 +289,43 @@ BFT_FN void philox(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
+// a ^ b ^ c as one v_bitop3_b32 on gfx950 (the compiler leaves 3-input XORs as two v_xor_b32)
+BFT_FN uint32_t pxor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+    return a ^ b ^ c;
+#endif
+}
+
+// The drop draw of deliver_mask: philox(seed, inst, tick, c2, DOM_DROP) with c2 = (phase << 24) |
+// (recv << 8) | j, computed with the products of wave-uniform words taken out of the vector work:
+// * round 1: c0 = inst is uniform, so its product is; the fields of c2 are disjoint, so
+//   c2 · M1 = base1 + j · M1 with base1 = ((phase << 24) | (recv << 8)) · M1 (once per phase): one 64-bit add;
+// * round 2: c2 = hi(inst · M0) ^ DOM_DROP ^ k1 is uniform again, so that product is too.
+// Rounds 3-10 are Philox's, each round's two 3-input XORs one v_bitop3_b32 apiece. Same words as philox().
+BFT_FN void philox_drop(uint64_t seed, uint32_t inst, uint32_t tick, uint64_t base1, uint32_t j, uint32_t out[4]) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const uint64_t q0 = (uint64_t)inst * 0xD2511F53u;                  // uniform
+    const uint64_t q1 = base1 + (uint64_t)j * 0xCD9E8D57u;             // = c2 * M1
+    uint32_t c0 = pxor3((uint32_t)(q1 >> 32), tick, k0), c1 = (uint32_t)q1;
+    uint32_t c2 = (uint32_t)(q0 >> 32) ^ DOM_DROP ^ k1, c3 = (uint32_t)q0;   // uniform
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)c0 * 0xD2511F53u, p1 = (uint64_t)c2 * 0xCD9E8D57u;
+        const uint32_t n0 = pxor3((uint32_t)(p1 >> 32), c1, k0), n2 = pxor3((uint32_t)(p0 >> 32), c3, k1);
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+BFT_FN uint64_t philox_drop_base(uint32_t phase, uint32_t recv) {
+    return (uint64_t)((phase << 24) | (recv << 8)) * 0xCD9E8D57u;
+}
+
 BFT_FN uint32_t lowbias32(uint32_t x) {
     x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
     return x;
@@ -316,10 +355,11 @@ BFT_FN Bits<NW> deliver_mask(uint64_t seed, uint32_t n, uint32_t thr16, uint32_t
     Bits<NW> all = Bits<NW>::low(n);
     if (thr16 == 0) return all;
     Bits<NW> m = Bits<NW>::zero();
+    const uint64_t base1 = philox_drop_base(phase, recv);
     for (uint32_t j = 0; 8 * j < n; ++j) {
         if (SKIP && ((present.word((int)(j >> 3)) >> (8u * (j & 7u))) & 0xffull) == 0) continue;
         uint32_t w[4];
-        philox(seed, inst, tick, (phase << 24) | (recv << 8) | j, DOM_DROP, w);
+        philox_drop(seed, inst, tick, base1, j, w);   // = philox(seed, inst, tick, (phase << 24) | (recv << 8) | j, DOM_DROP)
         uint64_t byte = 0;
 #pragma unroll
         for (uint32_t i = 0; i < 8; ++i) {
@@ -799,6 +839,47 @@ inline void spliced_block_hash(const uint32_t* sfx, const uint32_t prev[8], uint
     for (int i = 0; i < 4; ++i) { out[2 * i] = (uint32_t)a[i]; out[2 * i + 1] = (uint32_t)(a[i] >> 32); }
 }
 #endif
+
+// ---- little-endian seeds, N = 64: the canonical schedule's blocks, predicted ----
+// The Byzantine validators of an instance of 64 (SPEC.md §5: partial Fisher-Yates; `perm`: 64 bytes of
+// scratch), as Fast64::init_byzantine draws them.
+BFT_FN uint64_t byz_mask64(uint64_t seed, uint32_t inst, uint32_t f, uint8_t* perm) {
+    for (uint32_t i = 0; i < 64u; ++i) perm[i] = (uint8_t)i;
+    uint64_t mask = 0;
+    if (f > 64u) f = 64u;
+    for (uint32_t i = 0; i < f; ++i) {
+        uint32_t w[4];
+        philox(seed, inst, i, 0, DOM_BYZ, w);
+        const uint32_t j = i + w[0] % (64u - i);
+        const uint8_t t = perm[i]; perm[i] = perm[j]; perm[j] = t;
+        mask |= 1ull << perm[i];
+    }
+    return mask;
+}
+constexpr uint32_t SPEC_VALID = 0x80000000u;
+// Block x as the canonical tick would commit it (bft_fast64.h canonical_tick) if every tick since the
+// genesis was canonical: proposer j = seed(tip) mod 64 at round 0 (validator.rs:33-48, 74-77; the tip's
+// little-endian U128 seed mod 64 is the low 6 bits of its first hash word); an equivocating proposer
+// splits the validators by the SPLIT draw of view (x, 0) (SPEC.md §5) and the variant whose honest
+// validators with the Byzantine wildcards exceed Q = 42 commits; neither or both: no prediction (round
+// changes or a fork follow). The block's time tick is x - 1. The consumer (Fast64::hash_pending) takes a
+// prediction only where the recorded block equals it, height after height.
+BFT_FN bool spec_block64(uint64_t seed, uint32_t inst, uint32_t x, uint64_t byz, uint32_t tip_w0, uint32_t& j,
+                         uint32_t& var) {
+    j = tip_w0 & 63u;
+    uint64_t v1m = 0;
+    if ((byz >> j) & 1ull) {
+        uint32_t w[4];
+        philox(seed, inst, x, 0, DOM_SPLIT, w);
+        v1m = ((uint64_t)w[0] | ((uint64_t)w[1] << 32)) & ~(1ull << j);
+    }
+    const uint64_t hon = ~byz;
+    const bool k0 = __builtin_popcountll(byz | (hon & ~v1m)) > 42, k1 = __builtin_popcountll(byz | (hon & v1m)) > 42;
+    var = k1 ? 1u : 0u;
+    return k0 != k1;
+}
+// {valid, proposer, variant, seed of the block's hash mod 64}
+BFT_FN uint32_t spec_word(uint32_t j, uint32_t var, uint32_t seed_next) { return SPEC_VALID | j | (var << 8) | (seed_next << 16); }
 
 // randon_seed (validator.rs:39-48): U128::from(hash[0..8] ++ 0^8) mod n. `le` selects how the
 // 16-byte buffer is read (bftsim.h BFTSIM_SEED_*): big-endian (BE64(hash[0..8]) * 2^64) mod n, or

@@ -119,6 +119,7 @@ struct Fast64 {
         off_tick = 0;
         canon_seed = p.genesis_seed;
         hashed_h = 0;
+        spec_ok = SEEDED && p.spec != nullptr;
         prop_l = 0;
         tip_w = 0;
         if (SEEDED && me < 8u)
@@ -548,17 +549,37 @@ struct Fast64 {
     // SEEDED: the hash and seed of every height recorded since the last call, in height order (one call site,
     // so the wave hash is inlined once), before any validator can start the next height
     uint32_t hashed_h;
+    // SEEDED with predicted blocks (P.spec, bft_seed_chain_kernel): while every recorded height equals its
+    // prediction, the prediction's hash (already in P.hash) and seed are the block's; from the first height
+    // that differs, the wave hashes as before, from the last matching block's hash
+    bool spec_ok;
     BFT_FN void hash_pending() {
         while (hashed_h < canon_h) {                             // uniform
             const uint32_t x = hashed_h + 1u;
             const uint64_t b = canon_blk(x);
-            const uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
-            const uint32_t hw = kw50_header_hash(wv, me, lds + F64Layout::KW_OFF, tip_w,
-                                                 P.addresses + 20u * blk_prop(b), seed(), inst, x, blk_prop(b),
-                                                 blk_var(b), time);
-            if (me < 8u) ((uint32_t*)(P.hash + ((uint64_t)inst_local * P.rows + x) * 32))[me] = hw;
-            tip_w = hw;
-            const uint32_t sd = seed_from_words(uni(rl(hw, 0)), uni(rl(hw, 1)), N, P.seed_le != 0);
+            uint32_t sd = 0;
+            bool take = false;
+            if (spec_ok) {
+                const uint32_t sw = x <= P.heights ? uni(wv.gload(P.spec + (uint64_t)x * P.n_instances + inst_local)) : 0u;
+                const uint32_t sseed = (sw >> 16) & 0xffu;
+                take = (sw == spec_word(blk_prop(b), blk_var(b), sseed)) & (blk_T(b) + 1u == x);
+                sd = sseed;
+                if (!take) {                                     // the wave hashes from here: the parent's hash
+                    spec_ok = false;
+                    const uint32_t* ph = x == 1u ? (const uint32_t*)P.genesis_hash
+                                                 : (const uint32_t*)(P.hash + ((uint64_t)inst_local * P.rows + x - 1u) * 32);
+                    tip_w = me < 8u ? ph[me] : 0u;
+                }
+            }
+            if (!take) {
+                const uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
+                const uint32_t hw = kw50_header_hash(wv, me, lds + F64Layout::KW_OFF, tip_w,
+                                                     P.addresses + 20u * blk_prop(b), seed(), inst, x, blk_prop(b),
+                                                     blk_var(b), time);
+                if (me < 8u) ((uint32_t*)(P.hash + ((uint64_t)inst_local * P.rows + x) * 32))[me] = hw;
+                tip_w = hw;
+                sd = seed_from_words(uni(rl(hw, 0)), uni(rl(hw, 1)), N, P.seed_le != 0);
+            }
             if (me == 0) {                                       // the row's seed word, wherever the row is now
                 if (x > flushed) ring_row(x)[3] = sd;
                 else wv.gstore(rec_row(x) + 3, sd);

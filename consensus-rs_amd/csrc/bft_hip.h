@@ -217,6 +217,8 @@ struct ChainSets {
     uint8_t* hash[CHAIN_MAX_SETS];
 };
 hipError_t launch_hash_chain_batch(uint32_t n, const ChainSets& cs, bool wave, hipStream_t s, Params p);
+// little-endian seeds, N = 64: the predicted canonical blocks into p.spec / p.hash (kern_fast.hip)
+hipError_t launch_seed_chain(uint32_t n, hipStream_t s, const Params& p);
 hipError_t launch_resume(dim3 grid, size_t lds, hipStream_t s, const Params& p);  // kern_resume.hip
 
 }  // namespace bft

@@ -401,11 +401,12 @@ struct bftsim {
     //     whatever their number, so batching B launches per kernel gives B times the chain throughput
     //     (profiles/r04). Results are complete once bftsim_sync (or any fetch) returns; those flush a
     //     partial batch first.
-    static constexpr uint32_t MAX_SETS = 16, MAX_CS = 4, MAX_HS = 4, MAX_BATCH = bft::CHAIN_MAX_SETS;
+    static constexpr uint32_t MAX_SETS = 16, MAX_CS = 8, MAX_HS = 4, MAX_BATCH = bft::CHAIN_MAX_SETS;
     struct RowSet {
         uint32_t* ch = nullptr; uint32_t* flags = nullptr; uint32_t* ticks = nullptr; uint64_t* views = nullptr;
         uint32_t* rec = nullptr; uint8_t* hash = nullptr;
         uint32_t* sfx = nullptr;      // header suffix rows of the hash pass (sfx_rows per instance)
+        uint32_t* spec = nullptr;     // little-endian seeds, N = 64: predicted blocks [H + 1][n] (seed chain)
         // a launch's own scratch (set 0: the handle's buffers)
         uint64_t* hist = nullptr; uint32_t* rcs = nullptr; uint32_t* backlog = nullptr;
         uint32_t* resume = nullptr; uint32_t* save = nullptr; uint32_t* resume_q = nullptr;
@@ -420,12 +421,16 @@ struct bftsim {
     // (BFTSIM_TESTING + BFTSIM_CHAIN_WAVE_MAX)
     uint64_t chain_wave_max = 0;
     uint32_t chain_prio = 0;          // s_setprio of the chain waves (BFTSIM_TESTING + BFTSIM_CHAIN_PRIO)
+    bool seed_spec = true;            // little-endian seeds, N = 64: predicted blocks (BFTSIM_TESTING + BFTSIM_SEED_SPEC=0: off)
     int pipeline = 0;                 // number of row-table sets (0: no pipelining)
     uint32_t sfx_rows = 0;            // heights per hash-pass chunk (0: no hash pass)
     uint32_t n_sets = 0, cur_set = 0;
     bool last_pipe = false;           // the last launch ran on the launch streams
     hipStream_t cs[MAX_CS] = {}, hstr[MAX_HS] = {};
     uint32_t n_cs = 2, n_hs = 2, cur_cs = 0, cur_hs = 0;
+    // launch streams with little-endian seeds: a launch's seed chain and FAST kernel are serial on its stream
+    // and there is no hash pass, so more launches run side by side (profiles/r04/ab_le_streams)
+    uint32_t n_cs_seeded = 4;
     uint32_t hash_batch = 4;          // launches per chain kernel (BFTSIM_TESTING + BFTSIM_HASH_BATCH overrides)
     struct Pending { uint32_t set, ev; } pend[MAX_BATCH];
     uint32_t n_pend = 0;
@@ -467,12 +472,13 @@ static void free_bufs(bftsim* h) {
     for (uint32_t k = 0; k < h->n_sets; ++k) {
         bftsim::RowSet& r = h->sets[k];
         (void)hipFree(r.ch); (void)hipFree(r.flags); (void)hipFree(r.ticks); (void)hipFree(r.views);
-        (void)hipFree(r.rec); (void)hipFree(r.hash); (void)hipFree(r.sfx);
+        (void)hipFree(r.rec); (void)hipFree(r.hash); (void)hipFree(r.sfx); (void)hipFree(r.spec);
         if (k > 0) {                                   // set 0's scratch is the handle's own
             (void)hipFree(r.hist); (void)hipFree(r.rcs); (void)hipFree(r.backlog); (void)hipFree(r.resume);
             (void)hipFree(r.save); (void)hipFree(r.resume_q);
         }
         r.ch = r.flags = r.ticks = nullptr; r.views = nullptr; r.rec = nullptr; r.hash = nullptr; r.sfx = nullptr;
+        r.spec = nullptr;
         r.hist = nullptr; r.rcs = r.backlog = r.resume = r.save = r.resume_q = nullptr;
     }
 
@@ -762,8 +768,11 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
             if (testing && e) { const uint32_t x = (uint32_t)atoi(e); v = x < lo ? lo : x > hi ? hi : x; }
         };
         knob("BFTSIM_LAUNCH_STREAMS", h->n_cs, 1, bftsim::MAX_CS);
+        knob("BFTSIM_LAUNCH_STREAMS_SEEDED", h->n_cs_seeded, 1, bftsim::MAX_CS);
         knob("BFTSIM_HASH_STREAMS", h->n_hs, 1, bftsim::MAX_HS);   // A/B arms
         knob("BFTSIM_HASH_BATCH", h->hash_batch, 1, bftsim::MAX_BATCH);   // A/B arms (bftsim_set_hash_batch)
+        const char* ss = getenv("BFTSIM_SEED_SPEC");
+        if (testing && ss) h->seed_spec = atoi(ss) != 0;
     }
     const uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg, blocks = (n + per_block - 1) / per_block;
     for (uint32_t k = 1; k < (uint32_t)h->pipeline; ++k) {
@@ -801,6 +810,10 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         if (rows * n >= (1ull << 32)) rows = ((1ull << 32) - 1) / n;
         h->sfx_rows = (uint32_t)rows;
         for (uint32_t k = 0; k < h->n_sets; ++k) HIPCHECK(h, hipMalloc(&h->sets[k].sfx, rows * per_row));
+    } else if (h->seg == 64 && h->cfg.n == 64 && !h->window) {
+        // little-endian seeds at N = 64: the seed chain's predicted blocks
+        for (uint32_t k = 0; k < h->n_sets; ++k)
+            HIPCHECK(h, hipMalloc(&h->sets[k].spec, (uint64_t)(h->cfg.heights + 1u) * n * 4ull));
     }
     h->cap_inst = n;
     h->n_req = n;
@@ -894,7 +907,13 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     bft::Params p = make_params(h, first, n);
     // pipelined: on the launch streams with the set's own scratch; not with per-launch host state (traces,
     // the crypto log, which the next calls read from the last launch alone)
-    const bool pipe = h->pipeline >= 2 && !p.need_seed && h->n_sets >= 2 && !h->h_trace && !p.mlog;
+    // FAST + resume for N = 64: big-endian seeds (proposer 0, hashes in the post-pass) or little-endian
+    // seeds (SEEDED: the seed chain's predictions, else hashes in-kernel); not for windowed rows, traces or
+    // the opt-in modes
+    const bool fast = h->fast && p.fast && !p.mlog && h->d_save && !h->window && !h->h_trace && h->seg == 64 &&
+                      h->cfg.n == 64;
+    const bool spec = fast && p.need_seed && h->seed_spec && h->sets[0].spec;
+    const bool pipe = h->pipeline >= 2 && (!p.need_seed || spec) && h->n_sets >= 2 && !h->h_trace && !p.mlog;
     if (h->last_pipe && !pipe) {
         // a launch on the caller's stream after pipelined ones: they may still use set 0's scratch
         if (int rc = sync_all(h)) return rc;
@@ -924,7 +943,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         bftsim::RowSet& r = h->sets[h->cur_set];
         if (!r.entry) HIPCHECK(h, hipEventCreateWithFlags(&r.entry, hipEventDisableTiming));
         HIPCHECK(h, hipEventRecord(r.entry, s));
-        h->cur_cs = (h->cur_cs + 1) % h->n_cs;
+        h->cur_cs = (h->cur_cs + 1) % (spec ? h->n_cs_seeded : h->n_cs);
         if (!h->cs[h->cur_cs]) HIPCHECK(h, hipStreamCreateWithFlags(&h->cs[h->cur_cs], hipStreamNonBlocking));
         hipStream_t ls = h->cs[h->cur_cs];
         HIPCHECK(h, hipStreamWaitEvent(ls, r.entry, 0));
@@ -955,10 +974,6 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     uint32_t per_block = h->seg > 64 ? 1u : 64u / h->seg;      // instances per workgroup
     uint32_t grid = (uint32_t)((n + per_block - 1) / per_block);
     size_t lds = bft::lds_bytes(h->seg, p.need_seed != 0);
-    // FAST + resume for N = 64: big-endian seeds (proposer 0, hashes in the post-pass) or little-endian
-    // seeds (SEEDED: hashes in-kernel); not for windowed rows, traces or the opt-in modes
-    const bool fast = h->fast && p.fast && !p.mlog && h->d_save && !h->window && !h->h_trace && h->seg == 64 &&
-                      h->cfg.n == 64;
     const bool ext = p.backlog_replay || p.mlog;       // the opt-in modes' kernel build (MODE_EXT)
     HIPCHECK(h, hipEventRecord(ev.c0, s));
     if (fast) {
@@ -976,6 +991,10 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
                 *r.hint = 0xffffffffu;                    // unknown: the full grid
             }
             p.resume_hint = r.hint;
+        }
+        if (spec) {                                      // the predicted blocks first (little-endian seeds)
+            p.spec = h->sets[pipe ? h->cur_set : 0].spec;
+            HIPCHECK(h, bft::launch_seed_chain((uint32_t)n, s, p));
         }
         HIPCHECK(h, bft::launch_fast(dim3(grid), s, p));
         HIPCHECK(h, bft::launch_resume(dim3(grid), lds, s, p));
@@ -1023,6 +1042,10 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
                 h->sets[h->cur_set].busy = true;
             }
         }
+    }
+    if (pipe && p.need_seed) {                          // no hash pass: the set is free once this launch is done
+        HIPCHECK(h, hipEventRecord(h->sets[h->cur_set].done, s));
+        h->sets[h->cur_set].busy = true;
     }
     h->last_n = n;
     h->vsig_n = 0;

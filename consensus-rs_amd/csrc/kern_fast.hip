@@ -133,6 +133,43 @@ __global__ __launch_bounds__(256) void bft_hash_suffix_loop_kernel(Params p) {
     for (uint32_t j = 0; j < p.sfx_rows && p.sfx_x0 + j <= ch; ++j) suffix_row(p, il, j);
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// A lane pair's header hash: absorb the header spliced from the prefix (this lane's dwords `pw`, len_p
+// bytes) and the suffix in the pair's splice buffer `sb` (len_s bytes), permute; `prev` <- the hash (both
+// lanes: 8 words), `dst` <- this lane's four words of it.
+__device__ inline void pair_header_hash(const uint32_t* sb, const uint32_t* pw, uint32_t odd, uint32_t len_p,
+                                        uint32_t len_s, uint32_t prev[8], uint32_t* dst) {
+    const uint32_t c = 72u - len_p, r = c & 3u, nb = splice_blocks(len_p, len_s);
+    const uint32_t* sx = sb + (c >> 2) + odd;         // dword w = 2i + odd of each block
+    uint32_t X[25];
+#pragma unroll
+    for (int i = 0; i < 25; ++i) X[i] = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 17; ++i) {               // block 0: the prefix lies here
+        uint32_t v = align_bytes(sx[2u * i + 1u], sx[2u * i], r);
+        if (i < PFX_WORDS) v |= pw[2u * i];
+        X[i] ^= v;
+    }
+    if (odd & (nb == 1u)) X[16] ^= 0x80000000u;
+    keccak_f1600_pair(X, odd);
+#pragma unroll 1
+    for (uint32_t blk = 1; blk < nb; ++blk) {
+        const uint32_t* sxb = sx + 34u * blk;
+#pragma unroll
+        for (uint32_t i = 0; i < 17; ++i) X[i] ^= align_bytes(sxb[2u * i + 1u], sxb[2u * i], r);
+        if (odd & (blk + 1u == nb)) X[16] ^= 0x80000000u;
+        keccak_f1600_pair(X, odd);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t o = pair_swap(X[i]);
+        dst[2 * i + odd] = X[i];
+        prev[2 * i] = odd ? o : X[i];
+        prev[2 * i + 1] = odd ? X[i] : o;
+    }
+}
+#endif
+
 __constant__ PfxSel PFX_TBL[16] = {pfx_sel(0), pfx_sel(1), pfx_sel(2), pfx_sel(3), pfx_sel(4), pfx_sel(5),
                                    pfx_sel(6), pfx_sel(7), pfx_sel(8), pfx_sel(9), pfx_sel(10), pfx_sel(11),
                                    pfx_sel(12), pfx_sel(13), pfx_sel(14), pfx_sel(15)};
@@ -202,38 +239,70 @@ __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params
         }
         const uint32_t len_p = header_prefix_perm(pb, prev, ptbl);
         __syncthreads();                              // the pair's suffix halves and this lane's prefix
-        const uint32_t c = 72u - len_p, r = c & 3u, nb = splice_blocks(len_p, len_s);
-        const uint32_t* sx = sb + (c >> 2) + odd;    // dword w = 2i + odd of each block
-        uint32_t X[25];
-#pragma unroll
-        for (int i = 0; i < 25; ++i) X[i] = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < 17; ++i) {           // block 0: the prefix lies here
-            uint32_t v = align_bytes(sx[2u * i + 1u], sx[2u * i], r);
-            if (i < PFX_WORDS) v |= pw[2u * i];
-            X[i] ^= v;
-        }
-        if (odd & (nb == 1u)) X[16] ^= 0x80000000u;
-        keccak_f1600_pair(X, odd);
-#pragma unroll 1
-        for (uint32_t blk = 1; blk < nb; ++blk) {
-            const uint32_t* sxb = sx + 34u * blk;
-#pragma unroll
-            for (uint32_t i = 0; i < 17; ++i) X[i] ^= align_bytes(sxb[2u * i + 1u], sxb[2u * i], r);
-            if (odd & (blk + 1u == nb)) X[16] ^= 0x80000000u;
-            keccak_f1600_pair(X, odd);
-        }
-        uint32_t* dst = (uint32_t*)(p.hash + ((uint64_t)il * p.rows + x) * 32);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t o = pair_swap(X[i]);
-            dst[2 * i + odd] = X[i];
-            prev[2 * i] = odd ? o : X[i];
-            prev[2 * i + 1] = odd ? X[i] : o;
-        }
+        pair_header_hash(sb, pw, odd, len_p, len_s, prev, (uint32_t*)(p.hash + ((uint64_t)il * p.rows + x) * 32));
         __syncthreads();                              // splice buffer read before the next height's write
     }
 #endif
+}
+
+// Little-endian seeds, N = 64: the canonical blocks predicted ahead of the consensus kernel by a
+// lane pair per instance. The proposer of height x follows from the hash of x - 1, so with the wave hash the
+// consensus kernel hashed every height itself (~1,900 VALU per height for one instance); here the chain of
+// predictions runs as the block-hash chains do (32 instances per wave). Per height: proposer and committing
+// variant (spec_block64), the header suffix by the pair's even lane into the splice buffer, prev_hash,
+// Keccak; then the hash row and the prediction word. It ends at H or at the first height without a
+// prediction (word 0 there). Fast64::hash_pending takes a prediction only while each recorded block equals
+// it, and hashes in the wave from the first one that does not.
+__global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_seed_chain_kernel(Params p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __shared__ __attribute__((aligned(16))) uint32_t sbuf[32 * SFX_BUF];      // splice buffer per pair
+    __shared__ __attribute__((aligned(16))) uint64_t pbuf[64 * (PFX_WORDS + 4)];   // prefix per lane
+    __shared__ PfxSel ptbl[16];
+    __shared__ uint32_t slen[32];                                               // suffix length per pair
+    if (threadIdx.x < 16) ptbl[threadIdx.x] = PFX_TBL[threadIdx.x];
+    __syncthreads();
+    const uint32_t odd = threadIdx.x & 1u, pair = threadIdx.x >> 1;
+    const uint32_t il = blockIdx.x * 32u + pair;
+    if (il >= p.n_instances) return;                  // both lanes of a pair leave together
+    const uint32_t n = p.n_instances, inst = p.first_instance + il;
+    uint32_t* sb = sbuf + pair * SFX_BUF;
+    // the Byzantine validators: each lane draws them, its 64-byte permutation in the pair's splice buffer
+    const uint64_t byz = byz_mask64(p.seed, inst, p.byz_count, (uint8_t*)(sb + SFX_PAD) + 64u * odd);
+    __syncthreads();
+    for (uint32_t i = odd; i < SFX_PAD; i += 2u) sb[i] = 0;
+    for (uint32_t i = SFX_PAD + SFX_BODY_DW + odd; i < SFX_BUF; i += 2u) sb[i] = 0;
+    const uint8_t* ph = p.genesis_hash;
+    uint32_t prev[8];
+    for (int i = 0; i < 8; ++i)
+        prev[i] = (uint32_t)ph[4 * i] | ((uint32_t)ph[4 * i + 1] << 8) | ((uint32_t)ph[4 * i + 2] << 16) |
+                  ((uint32_t)ph[4 * i + 3] << 24);
+    uint64_t* pb = pbuf + threadIdx.x * (PFX_WORDS + 4);
+    const uint32_t* pw = (const uint32_t*)pb + odd;
+    for (uint32_t x = 1; x <= p.heights; ++x) {
+        uint32_t j, var;
+        if (!spec_block64(p.seed, inst, x, byz, prev[0], j, var)) {
+            if (!odd) p.spec[(uint64_t)x * n + il] = 0u;
+            break;
+        }
+        if (!odd) {                                   // header_suffix_fields of (x, j, var) at time tick x - 1
+            HdrWriter w(sb + SFX_PAD, 1u);
+            header_suffix_fields(w, p.addresses + 20u * j, p.seed, inst, x, j, var,
+                                 p.genesis_time + (uint64_t)p.block_period * (uint64_t)x);
+            slen[pair] = 8u * w.wi + w.fill;
+            w.store(w.wi++, w.acc | (0x01ull << (8u * w.fill)));
+            while (w.wi < SFX_BODY_DW / 2u) w.store(w.wi++, 0);
+        }
+        const uint32_t len_p = header_prefix_perm(pb, prev, ptbl);
+        __syncthreads();                              // the suffix and this lane's prefix
+        pair_header_hash(sb, pw, odd, len_p, slen[pair], prev, (uint32_t*)(p.hash + ((uint64_t)il * p.rows + x) * 32));
+        if (!odd) p.spec[(uint64_t)x * n + il] = spec_word(j, var, seed_from_words(prev[0], prev[1], 64u, true));
+        __syncthreads();                              // splice buffer read before the next height's write
+    }
+#endif
+}
+hipError_t launch_seed_chain(uint32_t n, hipStream_t s, const Params& p) {
+    hipLaunchKernelGGL(bft_seed_chain_kernel, dim3((n + 31u) / 32u), dim3(CHAIN_PAIR_BLOCK), 0, s, p);
+    return hipGetLastError();
 }
 
 // Small shards: the chain of one instance by one wave (bft_kwave.h kw50_chain). Workgroup b runs on XCD

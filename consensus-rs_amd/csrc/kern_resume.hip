@@ -4,8 +4,8 @@
 
 namespace bft {
 
-#ifndef BFT_WAVES_PER_SIMD
-#define BFT_WAVES_PER_SIMD 3
+#ifndef BFT_RESUME_WAVES_PER_SIMD
+#define BFT_RESUME_WAVES_PER_SIMD 3
 #endif
 // the full kernel over the instances the FAST kernel handed over, from their saved phase (NEED_SEED:
 // little-endian seeds, block hashes in-kernel)
@@ -14,7 +14,7 @@ namespace bft {
 // would dispatch n waves carrying the general body's LDS even when nothing was handed over, and beside the
 // concurrent launches' kernels that dispatch alone took ~0.2 ms per launch (cfg3, profiles/r04).
 template <bool NEED_SEED>
-__global__ __launch_bounds__(64, BFT_WAVES_PER_SIMD) void bft_consensus_resume_kernel(Params p) {
+__global__ __launch_bounds__(64, BFT_RESUME_WAVES_PER_SIMD) void bft_consensus_resume_kernel(Params p) {
     extern __shared__ uint8_t lds[];
     const uint32_t count = __hip_atomic_load(p.resume_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (blockIdx.x == 0 && threadIdx.x == 0 && p.resume_hint)
@@ -32,7 +32,7 @@ hipError_t launch_resume(dim3 grid, size_t lds, hipStream_t s, const Params& p) 
     // waves that can be resident at once (3 per SIMD): more would only queue for the same slots. Fewer when
     // the host's hint (the count of an earlier launch) says few instances hand over: beside concurrent
     // launches every wave waits for a free slot, and the queue is drained by however many waves there are
-    constexpr uint32_t MAXW = 256u * 4u * BFT_WAVES_PER_SIMD;
+    constexpr uint32_t MAXW = 256u * 4u * BFT_RESUME_WAVES_PER_SIMD;
     uint32_t g = grid.x < MAXW ? grid.x : MAXW;
     if (p.resume_hint) {
         const uint32_t hint = __atomic_load_n(p.resume_hint, __ATOMIC_RELAXED);

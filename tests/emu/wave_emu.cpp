@@ -407,11 +407,40 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
         save.assign((size_t)n * 64 * bft::SAVE_WORDS, 0xcdcdcdcdu);
         P.resume_flags = resume.data();
         P.save = save.data();
+        // little-endian seeds: the seed chain's predicted blocks first (kern_fast.hip bft_seed_chain_kernel, here
+        // with the one-piece header encoder; BFT_EMU_SPEC=0: none, the wave hashes every height)
+        std::vector<uint32_t> spec;
+        const char* es = getenv("BFT_EMU_SPEC");
+        if (P.need_seed && !(es && strcmp(es, "0") == 0)) {
+            spec.assign((size_t)(cfg->heights + 1) * n, 0xcdcdcdcdu);
+            P.spec = spec.data();
+            for (uint64_t il = 0; il < n; ++il) {
+                const uint32_t inst = (uint32_t)(first + il);
+                uint8_t perm[64];
+                const uint64_t byz = bft::byz_mask64(P.seed, inst, P.byz_count, perm);
+                uint32_t prev[8];
+                for (int i = 0; i < 8; ++i)
+                    prev[i] = (uint32_t)gh[4 * i] | ((uint32_t)gh[4 * i + 1] << 8) | ((uint32_t)gh[4 * i + 2] << 16) |
+                              ((uint32_t)gh[4 * i + 3] << 24);
+                for (uint32_t x = 1; x <= cfg->heights; ++x) {
+                    uint32_t j, var;
+                    if (!bft::spec_block64(P.seed, inst, x, byz, prev[0], j, var)) { spec[(size_t)x * n + il] = 0; break; }
+                    alignas(8) uint8_t buf[bft::LANE_HASH_BUF];
+                    uint32_t out[8];
+                    bft::lane_block_hash(buf, prev, cfg->addresses + 20u * j, P.seed, inst, x, j, var,
+                                         cfg->genesis_time + (uint64_t)cfg->block_period * x, out);
+                    memcpy(&hs[(il * hcap + x) * 32], out, 32);
+                    for (int i = 0; i < 8; ++i) prev[i] = out[i];
+                    spec[(size_t)x * n + il] = bft::spec_word(j, var, bft::seed_from_words(out[0], out[1], 64, true));
+                }
+            }
+        }
         std::vector<uint8_t> lds_fast(bft::lds_bytes_fast64(P.need_seed != 0));   // the FAST kernel's exact LDS size
         for (uint32_t w = 0; w < waves; ++w) {
             memset(lds_fast.data(), 0xcd, lds_fast.size());
             if (run_wave(P, w, lds_fast, 64, true)) return -1;
         }
+        P.spec = nullptr;                                  // read by the FAST kernel only
         P.resume_mode = 1;
     }
     for (uint32_t w = 0; w < waves; ++w) {
@@ -465,6 +494,25 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
         }
     }
     return 0;
+}
+
+// philox_drop (deliver_mask's draw, products of uniform words hoisted) against philox on random counters,
+// including the largest phase / receiver / block fields. Returns mismatches.
+extern "C" int emu_philox_drop_check(uint32_t trials, uint64_t seed) {
+    uint64_t s = seed | 1ull;
+    auto nxt = [&]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
+    int bad = 0;
+    for (uint32_t t = 0; t < trials; ++t) {
+        const uint64_t key = nxt();
+        const uint32_t inst = (uint32_t)nxt(), tick = (uint32_t)nxt();
+        const uint32_t phase = t < 8 ? 255u - t : (uint32_t)nxt() & 255u, recv = t < 8 ? 255u : (uint32_t)nxt() & 255u;
+        const uint32_t j = t < 8 ? 31u : (uint32_t)nxt() & 31u;
+        uint32_t a[4], b[4];
+        bft::philox(key, inst, tick, (phase << 24) | (recv << 8) | j, bft::DOM_DROP, a);
+        bft::philox_drop(key, inst, tick, bft::philox_drop_base(phase, recv), j, b);
+        if (memcmp(a, b, sizeof a) != 0) ++bad;
+    }
+    return bad;
 }
 
 // The splice of the block-hash pass against the one-piece encoder: `trials` random headers (random parent

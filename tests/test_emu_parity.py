@@ -58,6 +58,12 @@ CASES = [
     ("cfg3-le", lambda: _le(cfg3(heights=8)), 0, 2),
     ("cfg4-n64-le", lambda: _le(cfg4(64, heights=10)), 0, 2),
     ("cfg4-n128-le", lambda: _le(cfg4(128, heights=6)), 0, 1),
+    # N = 64 with little-endian seeds: the seed chain's predicted blocks, taken while they match (cfg3 shape),
+    # left at the first height that differs (drops, forks, phase caps)
+    ("cfg3-le-30", lambda: _le(cfg3(heights=30)), 5, 3),
+    ("n64-le-drop", lambda: _le(BftConfig(n=64, heights=12, seed=15, byz_count=21, drop_ppm=50_000)), 0, 3),
+    ("n64-le-byz32-fork", lambda: _le(BftConfig(n=64, heights=12, seed=31, byz_count=32)), 0, 3),
+    ("n64-le-byz21-cap4", lambda: _le(BftConfig(n=64, heights=20, seed=46, byz_count=21, phase_cap=4)), 0, 3),
     # backlog replay mode (bftsim.h BFTSIM_BACKLOG_REPLAY, SPEC.md §10): every phase one message at a time
     ("cfg2-replay", lambda: _replay(cfg2(heights=30)), 0, 16),
     ("n4-drop30-replay", lambda: _replay(BftConfig(n=4, heights=25, seed=7, drop_ppm=300_000)), 0, 8),
@@ -169,3 +175,29 @@ def test_roundchangeset_capacity_overflow_is_flagged_and_local(monkeypatch):
     assert ((E.run(cfg7, 0, 16)["flags"] & 32) != 0).all()
     monkeypatch.setenv("BFT_EMU_RCS_K", "8")
     assert_same(O.run(cfg7, 0, 16), E.run(cfg7, 0, 16), "n7-drop30 rcs_k=8")
+
+def test_drop_draw_hoisted_products_match_philox():
+    """deliver_mask's drop draw (bft_common.h philox_drop: round 1's products from the uniform instance
+    word and a 64-bit add per 8-sender block, round 2's product uniform) gives the words of
+    philox(seed, inst, tick, phase << 24 | recv << 8 | block, DOM_DROP), SPEC.md §3, on random counters
+    and at the largest phase / receiver / block fields."""
+    import ctypes
+    lib = E.lib()
+    lib.emu_philox_drop_check.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
+    assert lib.emu_philox_drop_check(200000, 31337) == 0
+
+
+@pytest.mark.parametrize("name,mk,first,n", [
+    ("cfg3-le", lambda: _le(cfg3(heights=30)), 0, 3),
+    ("n64-le-drop", lambda: _le(BftConfig(n=64, heights=12, seed=15, byz_count=21, drop_ppm=50_000)), 3, 3),
+    ("n64-le-honest", lambda: _le(BftConfig(n=64, heights=25, seed=47)), 0, 2)])
+def test_seed_predictions_change_nothing(name, mk, first, n, monkeypatch):
+    """Little-endian seeds at N = 64: the run with the seed chain's predicted blocks (Fast64::hash_pending
+    takes a prediction while the recorded block equals it) equals the run where the wave hashes every
+    height (BFT_EMU_SPEC=0), and both equal the oracle."""
+    cfg = mk()
+    with_spec = E.run(cfg, first, n)
+    monkeypatch.setenv("BFT_EMU_SPEC", "0")
+    without = E.run(cfg, first, n)
+    assert_same(with_spec, without, name + " predictions on / off")
+    assert_same(O.run(cfg, first, n), with_spec, name)
