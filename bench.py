@@ -259,11 +259,10 @@ def main():
     ap.add_argument("--hash-batch", type=int, default=None,
                     help="launches whose block-hash chains run as one kernel (bftsim_set_hash_batch, 1..8). Default: 2 "
                          "at >= 12,288 instances per GPU, 8 below (profiles/r04/ab_deep_ring)")
-    ap.add_argument("--hw-queues", type=int, default=None,
+    ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (HIP's default is 4): every set's stream needs its own "
                          "hardware queue, or launches serialize behind each other (profiles/r04/ab_depth_queues); "
-                         "0 leaves the environment as it is. Default 8; 12 with little-endian seeds (more launch "
-                         "streams, profiles/r04/ab_le_streams)")
+                         "0 leaves the environment as it is")
     ap.add_argument("--byz", type=int, default=None,
                     help="cfg2 / cfg5: run the tolerated f as this many equivocating validators (SPEC.md §6: "
                          "cfg2-byz = 1, cfg5-byz = 2)")
@@ -279,8 +278,6 @@ def main():
         sys.exit(spawn_ranks(args.gpus))           # before anything touches the GPU
     if os.environ.get("BFTSIM_TESTING") == "1" and os.environ.get("BFTSIM_BENCH_STUB_DIR"):
         return stub_rank(args)
-    if args.hw_queues is None:
-        args.hw_queues = 12 if args.seed_order == "le" else 8
     if args.hw_queues > 0:                         # read by the HIP runtime at its initialisation (below)
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:

@@ -306,6 +306,10 @@ BFT_FN uint32_t pxor3(uint32_t a, uint32_t b, uint32_t c) {
 // Rounds 3-10 are Philox's, each round's two 3-input XORs one v_bitop3_b32 apiece. Same words as philox().
 BFT_FN void philox_drop(uint64_t seed, uint32_t inst, uint32_t tick, uint64_t base1, uint32_t j, uint32_t out[4]) {
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    // the key schedule from opaque scalars: one s_add per key and round here, instead of 20 words LLVM would
+    // hoist out of the kernel's loops, spill into VGPR lanes and read back with v_readlane (general kernel)
+    BFT_OPAQUE_SGPR(k0);
+    BFT_OPAQUE_SGPR(k1);
     const uint64_t q0 = (uint64_t)inst * 0xD2511F53u;                  // uniform
     const uint64_t q1 = base1 + (uint64_t)j * 0xCD9E8D57u;             // = c2 * M1
     uint32_t c0 = pxor3((uint32_t)(q1 >> 32), tick, k0), c1 = (uint32_t)q1;

@@ -13,7 +13,8 @@ names = ["t_step", "summarize", "publish+classify", "post-sync", "resolve", "mas
          "#rc", "#none"]
 for name, cfg, fast in (("drop64-full", BftConfig(n=64, heights=100, seed=15, byz_count=21, drop_ppm=50_000, name="drop64"), 0),
                         ("cfg2", __import__("bftsim.configs", fromlist=["cfg2"]).cfg2(), 1),
-                        ("cfg4-256", __import__("bftsim.configs", fromlist=["cfg4"]).cfg4(256), 1)):
+                        ("cfg4-256", __import__("bftsim.configs", fromlist=["cfg4"]).cfg4(256), 1),
+                        ("cfg4-128", __import__("bftsim.configs", fromlist=["cfg4"]).cfg4(128), 1)):
     sim = runtime.Simulator(cfg)
     if not fast:
         sim.set_fast(False)
