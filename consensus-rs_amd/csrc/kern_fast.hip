@@ -133,6 +133,20 @@ __global__ __launch_bounds__(256) void bft_hash_suffix_loop_kernel(Params p) {
     for (uint32_t j = 0; j < p.sfx_rows && p.sfx_x0 + j <= ch; ++j) suffix_row(p, il, j);
 }
 
+// LDS of a chain block (one wave, 32 lane pairs): per pair a splice buffer and the prefix. Compact (an A/B arm,
+// -DBFT_CHAIN_COMPACT=1): the splice buffer stops after the suffix body plus one zero dword that every read past
+// the body is clamped to (only a 3-block header's last block reads there), and the two lanes of a pair share one
+// prefix buffer (they compute the same words): 13.7 KB per block instead of 21.1 KB, 3 chain waves per SIMD
+// instead of 2. Measured 2-4 % slower at every shard size (profiles/r04/ab_chain_lds): more resident chain waves
+// only take issue slots from the consensus kernels beside them.
+#ifndef BFT_CHAIN_COMPACT
+#define BFT_CHAIN_COMPACT 0
+#endif
+constexpr uint32_t CHAIN_SB = BFT_CHAIN_COMPACT ? 80u : SFX_BUF;        // splice buffer dwords per pair
+constexpr uint32_t CHAIN_SB_ZERO = SFX_PAD + SFX_BODY_DW;              // a zero dword (compact: reads past it clamp here)
+constexpr uint32_t CHAIN_PB_SLOTS = BFT_CHAIN_COMPACT ? 32u : 64u;      // prefix buffers per block
+static_assert(CHAIN_SB > CHAIN_SB_ZERO && CHAIN_SB % 4u == 0u, "splice buffer layout");
+
 #if defined(__HIP_DEVICE_COMPILE__)
 // A lane pair's header hash: absorb the header spliced from the prefix (this lane's dwords `pw`, len_p
 // bytes) and the suffix in the pair's splice buffer `sb` (len_s bytes), permute; `prev` <- the hash (both
@@ -154,9 +168,15 @@ __device__ inline void pair_header_hash(const uint32_t* sb, const uint32_t* pw, 
     keccak_f1600_pair(X, odd);
 #pragma unroll 1
     for (uint32_t blk = 1; blk < nb; ++blk) {
-        const uint32_t* sxb = sx + 34u * blk;
+        // block 1 reads at most dword 77 of the buffer (c >> 2 <= 9); a third block's reads past the suffix
+        // body clamp to the zero dword (compact buffer)
+        const uint32_t k0 = (c >> 2) + odd + 34u * blk;
 #pragma unroll
-        for (uint32_t i = 0; i < 17; ++i) X[i] ^= align_bytes(sxb[2u * i + 1u], sxb[2u * i], r);
+        for (uint32_t i = 0; i < 17; ++i) {
+            uint32_t ka = k0 + 2u * i, kb = ka + 1u;
+            if (BFT_CHAIN_COMPACT) { ka = ka < CHAIN_SB_ZERO ? ka : CHAIN_SB_ZERO; kb = kb < CHAIN_SB_ZERO ? kb : CHAIN_SB_ZERO; }
+            X[i] ^= align_bytes(sb[kb], sb[ka], r);
+        }
         if (odd & (blk + 1u == nb)) X[16] ^= 0x80000000u;
         keccak_f1600_pair(X, odd);
     }
@@ -195,8 +215,8 @@ __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params
         p.hash = cs.hash[k];
     }
     const uint32_t blk = blockIdx.x % ((p.n_instances + 31u) / 32u);
-    __shared__ __attribute__((aligned(16))) uint32_t sbuf[32 * SFX_BUF];      // splice buffer per pair
-    __shared__ __attribute__((aligned(16))) uint64_t pbuf[64 * (PFX_WORDS + 4)];   // prefix per lane
+    __shared__ __attribute__((aligned(16))) uint32_t sbuf[32 * CHAIN_SB];     // splice buffer per pair
+    __shared__ __attribute__((aligned(16))) uint64_t pbuf[CHAIN_PB_SLOTS * (PFX_WORDS + 4)];   // prefix (per pair: compact)
     __shared__ PfxSel ptbl[16];                                                 // header_prefix_perm
     if (threadIdx.x < 16) ptbl[threadIdx.x] = PFX_TBL[threadIdx.x];
     __syncthreads();
@@ -207,9 +227,9 @@ __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params
     const uint32_t ch = p.committed_height[il];
     const uint32_t x1 = ch < x0 + K - 1u ? ch : x0 + K - 1u;
     if (x1 < x0) return;
-    uint32_t* sb = sbuf + pair * SFX_BUF;
+    uint32_t* sb = sbuf + pair * CHAIN_SB;
     for (uint32_t i = odd; i < SFX_PAD; i += 2u) sb[i] = 0;
-    for (uint32_t i = SFX_PAD + SFX_BODY_DW + odd; i < SFX_BUF; i += 2u) sb[i] = 0;
+    for (uint32_t i = SFX_PAD + SFX_BODY_DW + odd; i < CHAIN_SB; i += 2u) sb[i] = 0;
     // the parent of x0: genesis, or the previous chunk's last hash (same stream, already written)
     const uint8_t* ph = x0 == 1u ? p.genesis_hash : p.hash + ((uint64_t)il * p.rows + x0 - 1u) * 32;
     uint32_t prev[8];
@@ -225,7 +245,7 @@ __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params
 #pragma unroll
     for (uint32_t i = 0; i < HALF; ++i) s[i] = srow[(uint64_t)i * n];
     slen = p.sfx[il + (uint64_t)SFX_DEV_LEN_DW * n];
-    uint64_t* pb = pbuf + threadIdx.x * (PFX_WORDS + 4);
+    uint64_t* pb = pbuf + (BFT_CHAIN_COMPACT ? pair : threadIdx.x) * (PFX_WORDS + 4);   // both lanes write the same words
     const uint32_t* pw = (const uint32_t*)pb + odd;
     for (uint32_t x = x0; x <= x1; ++x) {
 #pragma unroll
@@ -255,8 +275,8 @@ __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params
 // it, and hashes in the wave from the first one that does not.
 __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_seed_chain_kernel(Params p) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    __shared__ __attribute__((aligned(16))) uint32_t sbuf[32 * SFX_BUF];      // splice buffer per pair
-    __shared__ __attribute__((aligned(16))) uint64_t pbuf[64 * (PFX_WORDS + 4)];   // prefix per lane
+    __shared__ __attribute__((aligned(16))) uint32_t sbuf[32 * CHAIN_SB];     // splice buffer per pair
+    __shared__ __attribute__((aligned(16))) uint64_t pbuf[CHAIN_PB_SLOTS * (PFX_WORDS + 4)];   // prefix (per pair: compact)
     __shared__ PfxSel ptbl[16];
     __shared__ uint32_t slen[32];                                               // suffix length per pair
     if (threadIdx.x < 16) ptbl[threadIdx.x] = PFX_TBL[threadIdx.x];
@@ -265,18 +285,18 @@ __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_seed_chain_kernel(Params
     const uint32_t il = blockIdx.x * 32u + pair;
     if (il >= p.n_instances) return;                  // both lanes of a pair leave together
     const uint32_t n = p.n_instances, inst = p.first_instance + il;
-    uint32_t* sb = sbuf + pair * SFX_BUF;
+    uint32_t* sb = sbuf + pair * CHAIN_SB;
     // the Byzantine validators: each lane draws them, its 64-byte permutation in the pair's splice buffer
     const uint64_t byz = byz_mask64(p.seed, inst, p.byz_count, (uint8_t*)(sb + SFX_PAD) + 64u * odd);
     __syncthreads();
     for (uint32_t i = odd; i < SFX_PAD; i += 2u) sb[i] = 0;
-    for (uint32_t i = SFX_PAD + SFX_BODY_DW + odd; i < SFX_BUF; i += 2u) sb[i] = 0;
+    for (uint32_t i = SFX_PAD + SFX_BODY_DW + odd; i < CHAIN_SB; i += 2u) sb[i] = 0;
     const uint8_t* ph = p.genesis_hash;
     uint32_t prev[8];
     for (int i = 0; i < 8; ++i)
         prev[i] = (uint32_t)ph[4 * i] | ((uint32_t)ph[4 * i + 1] << 8) | ((uint32_t)ph[4 * i + 2] << 16) |
                   ((uint32_t)ph[4 * i + 3] << 24);
-    uint64_t* pb = pbuf + threadIdx.x * (PFX_WORDS + 4);
+    uint64_t* pb = pbuf + (BFT_CHAIN_COMPACT ? pair : threadIdx.x) * (PFX_WORDS + 4);   // both lanes write the same words
     const uint32_t* pw = (const uint32_t*)pb + odd;
     for (uint32_t x = 1; x <= p.heights; ++x) {
         uint32_t j, var;
