@@ -157,6 +157,7 @@ struct Sim {
     bool wait;
     uint64_t lock, pp, pend;
     M prep, comm;            // MessageManage sender sets (protocol/mod.rs:176-209)
+    M canon_voters;          // canonical_pp: the running validators (their Prepares and Commits)
     uint32_t n_rcs;          // RoundChangeSet entries (the table itself lives in LDS)
     uint32_t proposer;       // 0xffffffff = None
     // chain tip
@@ -946,11 +947,12 @@ struct Sim {
         return add;
     }
 
-    // first Core commits of the phase → canonical table, in lane order (oracle receiver order)
-    BFT_FN void resolve_commits() {
+    // first Core commits of the phase → canonical table, in lane order (oracle receiver order). Returns the
+    // committed height when every committer of the segment committed the same one (segment-uniform), else 0.
+    BFT_FN uint32_t resolve_commits() {
         bool c = commit_x != 0;
         M bal = ballot(c);
-        if (bal.none()) return;
+        if (bal.none()) return 0;
         if constexpr (S == 64) {
             // one instance per wave: the first committer's values by readlane, and when every committer
             // commits that same height (the common case) the canonical update is computed by all lanes
@@ -977,7 +979,7 @@ struct Sim {
                 if (x0 >= P.hcap) fr = true;
                 if (fr) { frozen = true; seg_flags |= FLAG_SAFETY; }
                 commit_x = 0;
-                return;
+                return x0;
             }
         }
         uint32_t* cm = (uint32_t*)(lds + LDS_CMT_OFF) + lane * LY::CMT_STRIDE;
@@ -1070,6 +1072,7 @@ struct Sim {
         }
         commit_x = 0;
         sync();
+        return (mine && uniform) ? x0 : 0u;
     }
 
     BFT_FN uint64_t state_digest() const {
@@ -1470,6 +1473,52 @@ struct Sim {
         if (p2 >= 0) rc_set_store((uint32_t)p2, later);
     }
 
+    // ---------------------------------------------------------------- the canonical view, composed
+    // A lone Preprepare in flight (PATH_PP) of view (vh, vr) from its proposer, no link drops and no Byzantine
+    // validators, and every running validator waiting for it: AcceptRequest at (vh, vr), unlocked, its chain
+    // tip vh - 1, no seal about to mine in this phase's event step, and no outbound-cache entry for this
+    // subject's Prepare or Commit. Then this phase and the next two have one outcome (the same steps the
+    // closed forms take one phase at a time): every running validator accepts (preprepare.rs:87-106) and
+    // sends its Prepare; all Prepares cross the quorum (prepare.rs:59-63): lock, Prepared, Commit out; all
+    // Commits cross it (commit.rs:63-82): Committed, Core::commit → insert_block (chain.rs:45-71). The Prepare
+    // and Commit phases' event steps have nothing queued. One instance per wave or workgroup (the segments of a
+    // wave share the phase index), not in the opt-in modes (they log or re-deliver every message).
+    // Segment-uniform; every lane reaches the ballots.
+    BFT_FN bool canonical_pp(const PhaseSummary& ps, uint32_t path, uint32_t p, bool act) {
+        if constexpr (S < 64 || MODE == MODE_EXT) return false;
+        else {
+            if ((path != PATH_PP) | (ps.pp_eq != 0u) | (P.thr16 != 0u) | (P.byz_count != 0u) | frozen |
+                (p + 2u >= P.phase_cap))
+                return false;
+            const uint32_t vh = ps.pp_h, vr = ps.pp_r, d32 = blk_d32(ps.pp_b);
+            const uint32_t* c1 = cache_p(3);                  // Prepare {h, r, d32}
+            const uint32_t* c2 = cache_p(6);                  // Commit
+            const bool hit1 = (c1[2u * LY::L] == d32) & (c1[0] == vh) & (c1[LY::L] == vr);
+            const bool hit2 = (c2[2u * LY::L] == d32) & (c2[0] == vh) & (c2[LY::L] == vr);
+            const bool mines = (wake_tick < 0) & (miner_queue != 0u) & (miner_queue >= mint_height);
+            const bool ok = !core_dead & (h == vh) & (r == vr) & (st == ST_ACCEPT_REQUEST) & !blk_valid(lock) &
+                            (proposer == ps.pp_src) & (last + 1u == vh) & (blk_h(ps.pp_b) == vh) & !mines & !hit1 & !hit2;
+            const M bad = ballot(act & !ok);
+            canon_voters = ballot(act);
+            return bad.none() && canon_voters.popc() > qval();
+        }
+    }
+    BFT_FN void apply_canonical_pp(const PhaseSummary& ps) {
+        const uint32_t vh = ps.pp_h, vr = ps.pp_r, d32 = blk_d32(ps.pp_b);
+        uint32_t* c1 = cache_p(3);
+        uint32_t* c2 = cache_p(6);
+        c1[0] = vh; c1[LY::L] = vr; c1[2u * LY::L] = d32;     // send_prepare (the PP phase)
+        c2[0] = vh; c2[LY::L] = vr; c2[2u * LY::L] = d32;     // send_commit (the Prepare phase)
+        pp = ps.pp_b;
+        prep = canon_voters;                                  // every running validator's Prepare
+        comm = canon_voters;                                  // and Commit
+        lock_hash();
+        st = ST_COMMITTED;                                    // the Commit phase: Core::commit
+        in_pc = true;
+        chain_insert_core(pp);
+        in_pc = false;
+    }
+
     BFT_FN void deliver_phase(const PhaseSummary& ps, uint32_t path, const M& mk, uint32_t off) {
         if (path == PATH_NONE) return;
         if (path == PATH_PP) {                        // one Preprepare: its handler at every receiver
@@ -1604,6 +1653,7 @@ struct Sim {
                 if (pub) { publish(); sync(); }
                 else outbox_clear(nx);
                 BFT_STAMP(2);
+                const bool canon = canonical_pp(ps, path, p, act);
                 if (act & seg_pending) {
                     miner_step();                             // event step
                     // the draws of the senders in flight only (a Preprepare phase: one block of 8)
@@ -1615,14 +1665,35 @@ struct Sim {
                     uint32_t off = (path == PATH_GENERAL || path == PATH_PC || path == PATH_RC)
                                        ? offset_from_parts(P.seed, nval(), off_tick, p, me) : 0u;
                     BFT_STAMP(5);
-                    deliver_phase(ps, path, mk, off);
+                    if (canon) apply_canonical_pp(ps);
+                    else deliver_phase(ps, path, mk, off);
                 }
+                if (canon) p += 2u;                           // the Prepare and Commit phases, applied
                 if (pub) sync();                              // records read before the next publish
                 BFT_STAMP(3);
                 if constexpr (WAVE_HASH) resolve_deferred_hash();
-                resolve_commits();
+                const uint32_t xc = resolve_commits();
                 BFT_STAMP(4);
                 if (frozen) act = false;
+                // The block-gossip phase after a commit, fused (as bft_fast64.h does): when a Prepare/Commit phase
+                // ends with every committer at height xc, the next phase carries their Blocks ranges [.., xc]. If
+                // nothing else is in flight and every running validator already holds xc, handle_blocks is
+                // ChainError::Exists for all of them (core.rs:75-82), whatever the delivery masks, and that phase
+                // reduces to its event step (same phase index, same miner step). One instance per wave or
+                // workgroup only (segments of a wave share the phase loop), and not in the opt-in modes (the
+                // crypto log records every broadcast, replay mode re-delivers at every phase).
+                if constexpr (S >= 64 && MODE != MODE_EXT) {
+                    if ((xc != 0u) & ((path == PATH_PC) | canon) & !frozen & (p + 1u < P.phase_cap)) {
+                        const M pb = ballot(act & pending_local());
+                        const bool nop = !running | seg_done |
+                                         ((((nx.f & ~F_BLK) == 0u) & (((nx.f & F_BLK) == 0u) | (nx.blk_hi == xc))) & (last >= xc));
+                        if (pb.any() && ballot(!nop).none()) {
+                            ++p;
+                            outbox_clear(nx);
+                            if (act) miner_step();
+                        }
+                    }
+                }
             }
             if (P.trace && is_val && !seg_done && (uint32_t)tick < P.trace_ticks)
                 P.trace[((uint64_t)inst_local * P.trace_ticks + (uint32_t)tick) * nval() + me] = state_digest();
