@@ -157,7 +157,6 @@ struct Sim {
     bool wait;
     uint64_t lock, pp, pend;
     M prep, comm;            // MessageManage sender sets (protocol/mod.rs:176-209)
-    M canon_voters;          // canonical_pp: the running validators (their Prepares and Commits)
     uint32_t n_rcs;          // RoundChangeSet entries (the table itself lives in LDS)
     uint32_t proposer;       // 0xffffffff = None
     // chain tip
@@ -1482,10 +1481,19 @@ struct Sim {
     // sends its Prepare; all Prepares cross the quorum (prepare.rs:59-63): lock, Prepared, Commit out; all
     // Commits cross it (commit.rs:63-82): Committed, Core::commit → insert_block (chain.rs:45-71). The Prepare
     // and Commit phases' event steps have nothing queued. One instance per wave or workgroup (the segments of a
-    // wave share the phase index), not in the opt-in modes (they log or re-deliver every message).
+    // wave share the phase index), not in the opt-in modes (they log or re-deliver every message: MODE_EXT).
     // Segment-uniform; every lane reaches the ballots.
+    // the running validators of an active segment (Sim(): a validator below N that is not silent), from the
+    // launch parameters: the senders of every Prepare and Commit of a canonical view
+    BFT_FN M running_set() const {
+        M m = M::low(nval());
+        for (int k = 0; k < NW; ++k) m.w[k] &= ~P.silent_mask[k];
+        return m;
+    }
     BFT_FN bool canonical_pp(const PhaseSummary& ps, uint32_t path, uint32_t p, bool act) {
-        if constexpr (S < 64 || MODE == MODE_EXT) return false;
+        // workgroup segments, and the resume kernel after a FAST hand-over; the S = 64 full kernel (N = 33..63,
+        // bftsim_set_fast(h, 0)) keeps its registers (the step's code costs it 140 B/lane of scratch)
+        if constexpr (!(S > 64 || MODE == MODE_RESUME)) return false;
         else {
             if ((path != PATH_PP) | (ps.pp_eq != 0u) | (P.thr16 != 0u) | (P.byz_count != 0u) | frozen |
                 (p + 2u >= P.phase_cap))
@@ -1499,8 +1507,7 @@ struct Sim {
             const bool ok = !core_dead & (h == vh) & (r == vr) & (st == ST_ACCEPT_REQUEST) & !blk_valid(lock) &
                             (proposer == ps.pp_src) & (last + 1u == vh) & (blk_h(ps.pp_b) == vh) & !mines & !hit1 & !hit2;
             const M bad = ballot(act & !ok);
-            canon_voters = ballot(act);
-            return bad.none() && canon_voters.popc() > qval();
+            return bad.none() && running_set().popc() > qval();
         }
     }
     BFT_FN void apply_canonical_pp(const PhaseSummary& ps) {
@@ -1510,8 +1517,9 @@ struct Sim {
         c1[0] = vh; c1[LY::L] = vr; c1[2u * LY::L] = d32;     // send_prepare (the PP phase)
         c2[0] = vh; c2[LY::L] = vr; c2[2u * LY::L] = d32;     // send_commit (the Prepare phase)
         pp = ps.pp_b;
-        prep = canon_voters;                                  // every running validator's Prepare
-        comm = canon_voters;                                  // and Commit
+        const M voters = running_set();
+        prep = voters;                                        // every running validator's Prepare
+        comm = voters;                                        // and Commit
         lock_hash();
         st = ST_COMMITTED;                                    // the Commit phase: Core::commit
         in_pc = true;
@@ -1654,7 +1662,9 @@ struct Sim {
                 else outbox_clear(nx);
                 BFT_STAMP(2);
                 const bool canon = canonical_pp(ps, path, p, act);
-                if (act & seg_pending) {
+                if (canon) {                                  // this phase and the next two, applied
+                    if (act) { miner_step(); apply_canonical_pp(ps); }
+                } else if (act & seg_pending) {
                     miner_step();                             // event step
                     // the draws of the senders in flight only (a Preprepare phase: one block of 8)
                     const M present = path == PATH_PP ? M::bit(ps.pp_src)
@@ -1665,8 +1675,7 @@ struct Sim {
                     uint32_t off = (path == PATH_GENERAL || path == PATH_PC || path == PATH_RC)
                                        ? offset_from_parts(P.seed, nval(), off_tick, p, me) : 0u;
                     BFT_STAMP(5);
-                    if (canon) apply_canonical_pp(ps);
-                    else deliver_phase(ps, path, mk, off);
+                    deliver_phase(ps, path, mk, off);
                 }
                 if (canon) p += 2u;                           // the Prepare and Commit phases, applied
                 if (pub) sync();                              // records read before the next publish

@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1
-O=gpurun_out/r04x; mkdir -p $O
+O=gpurun_out/${OUT:-r04x}; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_suite.log 2>&1; rc=$?; tail -3 $O/gpu_suite.log; [ $rc -eq 0 ] || exit $rc
 b() {
   local name=$1; shift
