@@ -201,3 +201,35 @@ def test_seed_predictions_change_nothing(name, mk, first, n, monkeypatch):
     without = E.run(cfg, first, n)
     assert_same(with_spec, without, name + " predictions on / off")
     assert_same(O.run(cfg, first, n), with_spec, name)
+
+
+def test_general_body_fusions_are_taken(tmp_path, monkeypatch):
+    """The general kernel's two shortcuts (bft_wave.h: the block-gossip phase after a uniform commit fused,
+    the canonical view composed in one step) actually run: on cfg4 N = 256 (proposer crashes, no
+    drops) the emulator's phase census sees no Blocks phase and about one phase per instance-round (3.1 without
+    them), and the results equal the oracle's."""
+    import ctypes
+    import os
+    import subprocess
+    import numpy as np
+    lib_path = str(tmp_path / "libwave_emu_census.so")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unknown-pragmas", "-DBFT_CENSUS_BUILD",
+                           "-o", lib_path, os.path.join(E.EMU_DIR, "wave_emu.cpp")])
+    saved_lib, saved_path = E._lib, E.LIB
+    try:
+        E._lib, E.LIB = None, lib_path
+        L = E.lib()
+        L.emu_census.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        cfg = cfg4(256, heights=8)
+        got = E.run(cfg, 0, 1)
+        keys = np.zeros(256, np.uint32)
+        cnt = np.zeros(256, np.uint64)
+        m = L.emu_census(keys.ctypes.data, cnt.ctypes.data, 256)
+        phases = int(cnt[:m].sum())
+        kinds = [int(k) & 127 for k in keys[:m]]
+        assert all(not (k >> 6) & 1 for k in kinds), "a Blocks phase was delivered"
+        views = int(got["views"].sum())
+        assert views > 0 and phases / views < 1.3, (phases, views)
+    finally:
+        E._lib, E.LIB = saved_lib, saved_path
+    assert_same(O.run(cfg, 0, 1), got, "cfg4-n256 census run")
