@@ -257,7 +257,7 @@ def main():
                     help="launches in flight (bftsim_set_pipeline: a ring of row-table sets, each launch on its set's "
                          "stream). Default: 6 at >= 12,288 instances per GPU, 16 below (profiles/r04/ab_deep_ring)")
     ap.add_argument("--hash-batch", type=int, default=None,
-                    help="launches whose block-hash chains run as one kernel (bftsim_set_hash_batch, 1..8). Default: 2 "
+                    help="launches whose block-hash chains run as one kernel (bftsim_set_hash_batch, 1..16). Default: 2 "
                          "at >= 12,288 instances per GPU, 8 below (profiles/r04/ab_deep_ring)")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (HIP's default is 4): every set's stream needs its own "

@@ -209,7 +209,7 @@ hipError_t launch_hash_suffix(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* 
 // `wave`: one wave per instance (bft_hash_chain_wave_kernel, small shards) instead of a lane pair
 hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, bool wave, hipStream_t s, Params p);
 // the chains of up to CHAIN_MAX_SETS launches (row-table sets) of n instances each, heights 1..H, as one kernel
-constexpr uint32_t CHAIN_MAX_SETS = 8;
+constexpr uint32_t CHAIN_MAX_SETS = 16;
 struct ChainSets {
     uint32_t count;
     const uint32_t* sfx[CHAIN_MAX_SETS];

@@ -401,7 +401,7 @@ struct bftsim {
     //     whatever their number, so batching B launches per kernel gives B times the chain throughput
     //     (profiles/r04). Results are complete once bftsim_sync (or any fetch) returns; those flush a
     //     partial batch first.
-    static constexpr uint32_t MAX_SETS = 16, MAX_CS = 8, MAX_HS = 4, MAX_BATCH = bft::CHAIN_MAX_SETS;
+    static constexpr uint32_t MAX_SETS = 32, MAX_CS = 8, MAX_HS = 4, MAX_BATCH = bft::CHAIN_MAX_SETS;
     struct RowSet {
         uint32_t* ch = nullptr; uint32_t* flags = nullptr; uint32_t* ticks = nullptr; uint64_t* views = nullptr;
         uint32_t* rec = nullptr; uint8_t* hash = nullptr;
@@ -1084,7 +1084,7 @@ static int flush_batch(bftsim* h) {
 
 int bftsim_set_hash_batch(bftsim_t* h, uint32_t launches) {
     if (!h) return BFTSIM_EINVAL;
-    if (launches < 1 || launches > bftsim::MAX_BATCH) return fail(h, BFTSIM_EINVAL, "hash batch must be 1..8 launches");
+    if (launches < 1 || launches > bftsim::MAX_BATCH) return fail(h, BFTSIM_EINVAL, "hash batch must be 1..16 launches");
     if (int rc = flush_batch(h)) return rc;
     h->hash_batch = launches;
     return BFTSIM_OK;
@@ -1092,7 +1092,7 @@ int bftsim_set_hash_batch(bftsim_t* h, uint32_t launches) {
 
 int bftsim_set_pipeline(bftsim_t* h, int on) {
     if (!h) return BFTSIM_EINVAL;
-    if (on < 0 || on > (int)bftsim::MAX_SETS) return fail(h, BFTSIM_EINVAL, "pipeline depth must be 0..16");
+    if (on < 0 || on > (int)bftsim::MAX_SETS) return fail(h, BFTSIM_EINVAL, "pipeline depth must be 0..32");
     const int depth = on == 0 ? 0 : on == 1 ? 2 : on;
     if (depth == h->pipeline) return BFTSIM_OK;
     int rc = h->last_stream ? sync_all(h) : BFTSIM_OK;

@@ -149,11 +149,12 @@ int bftsim_last_kernel_ms(bftsim_t *h, float *consensus_ms, float *hash_ms);
 /* summed per-kernel device times (ms) of every launch since the previous call, without blocking
  * between launches (waits only for the launches being summed) */
 int bftsim_kernel_ms_sum(bftsim_t *h, double *consensus_ms, double *hash_ms, uint32_t *launches);
-/* pipelined launches (big-endian seeds and power-of-two N, the batch throughput mode of the
- * benchmark): a ring of `on` row-table sets (on = 1 means 2; 0 disables; at most 16), each with the scratch
- * of one launch, so that up to `on` launches are in flight. A launch's consensus kernel runs on one of two
- * internal launch streams (after the caller's earlier work on `hip_stream` and after its set's last hash
- * pass); the prev_hash chains of bftsim_set_hash_batch consecutive launches run as one kernel on one of two
+/* pipelined launches (power-of-two N; with little-endian seeds at N = 64 too, whose launches carry their own
+ * seed chain and no hash pass; the batch throughput mode of the benchmark): a ring of `on` row-table sets
+ * (on = 1 means 2; 0 disables; at most 32), each with the scratch of one launch, so that up to `on` launches
+ * are in flight. A launch's consensus kernel runs on one of two internal launch streams (four with
+ * little-endian seeds) after the caller's earlier work on `hip_stream` and after its set's last hash
+ * pass; the prev_hash chains of bftsim_set_hash_batch consecutive launches run as one kernel on one of two
  * internal hash streams (a chain is sequential in height: a launch's chains take ~1.5 ms however many
  * there are, so batching multiplies their throughput). Results of a launch are complete once bftsim_sync
  * returns (it also enqueues a partial hash batch); bftsim_fetch/_stats_get/_fetch_summary read the last
@@ -161,7 +162,7 @@ int bftsim_kernel_ms_sum(bftsim_t *h, double *consensus_ms, double *hash_ms, uin
  * two launch and two hash streams): GPU_MAX_HW_QUEUES >= 5 in the environment before HIP initialises (HIP's
  * default is 4; bench.py sets 8). Takes effect at the next bftsim_prepare (buffers are re-allocated). */
 int bftsim_set_pipeline(bftsim_t *h, int on);
-/* pipelined launches: the number of consecutive launches whose block-hash chains run as one kernel (1..8,
+/* pipelined launches: the number of consecutive launches whose block-hash chains run as one kernel (1..16,
  * default 4). A launch waiting for its batch is hashed when the batch fills, at bftsim_sync, or when the ring
  * needs its row-table set again. */
 int bftsim_set_hash_batch(bftsim_t *h, uint32_t launches);
