@@ -51,10 +51,10 @@ def test_pipelined_launches_match_oracle(depth, chain, batch, lstreams, monkeypa
     assert st["views"] == int(ref["views"].sum())
 
 
-@pytest.mark.parametrize("depth,batch,hstreams", [(16, 8, 3), (5, 8, 2), (12, 6, 4)])
+@pytest.mark.parametrize("depth,batch,hstreams", [(16, 8, 3), (5, 8, 2), (12, 6, 4), (32, 16, 2), (7, 16, 3)])
 def test_deep_ring_and_large_hash_batches(depth, batch, hstreams, monkeypatch):
-    """rings up to 16 sets and chain kernels over up to 8 launches (a set still waiting in the batch when the
-    ring comes back to it is flushed first: depth 5 < batch 8), 20 launches of the same instances"""
+    """rings up to 32 sets and chain kernels over up to 16 launches (a set still waiting in the batch when the
+    ring comes back to it is flushed first: depth 5 < batch 8, 7 < 16), 20 launches of the same instances"""
     monkeypatch.setenv("BFTSIM_TESTING", "1")
     monkeypatch.setenv("BFTSIM_HASH_STREAMS", str(hstreams))
     cfg = cfg3(heights=30)
