@@ -159,3 +159,33 @@ def test_small_shard_timed_mode(chain, monkeypatch):
     ref = O.run(cfg, 2048, n, threads=16)
     assert_same(ref, got, f"cfg3 2048 pipelined x4 ({chain})")
     assert st["views"] == int(ref["views"].sum()) == n * 100
+
+
+@pytest.mark.parametrize("name,mk,depth", [
+    ("cfg3-le", lambda: __import__("dataclasses").replace(cfg3(heights=40), seed_byte_order=1, name="cfg3-le"), 6),
+    ("n64-le-drop", lambda: BftConfig(n=64, heights=20, seed=15, byz_count=21, drop_ppm=50_000, seed_byte_order=1,
+                                      name="n64-le-drop"), 16)])
+def test_little_endian_pipelined_predictions(name, mk, depth, monkeypatch):
+    """Little-endian seeds at N = 64, pipelined: each launch runs its seed chain, FAST and resume
+    kernels on one of the seeded launch streams; the predictions are taken while they match and the wave hashes
+    from the first recorded block that differs (drops). 12 launches of the same instances; predictions on and
+    off against the oracle."""
+    monkeypatch.setenv("BFTSIM_TESTING", "1")
+    cfg = mk()
+    n = 96
+    outs = []
+    for spec in ("1", "0"):
+        monkeypatch.setenv("BFTSIM_SEED_SPEC", spec)
+        sim = _sim(cfg)
+        try:
+            sim.set_pipeline(True, depth)
+            sim.prepare(n)
+            for k in range(12):
+                sim.launch(5 * n)
+            sim.sync()
+            outs.append(sim.fetch())
+        finally:
+            sim.close()
+    ref = O.run(cfg, 5 * n, n)
+    assert_same(ref, outs[0], name + " predictions")
+    assert_same(ref, outs[1], name + " wave hash only")
