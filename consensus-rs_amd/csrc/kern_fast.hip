@@ -68,8 +68,18 @@ __constant__ uint32_t KECCAK_RC_PAIR[2][24] = {
     {0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0x80000000u, 0x80000000u, 0u, 0u, 0u, 0u, 0u, 0x80000000u,
      0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u, 0x80000000u, 0x80000000u, 0u, 0x80000000u}};
 
+// The 24 rounds fully unrolled (default): round constants become per-round constants instead of a per-lane load
+// from constant memory waited for in every round, and the rounds schedule into each other: cfg3 +5 %,
+// 2,048 per GPU +10 % (profiles/r04/ab_pair_unroll/). BFT_PAIR_UNROLL=1: the round loop (A/B arm).
+#ifndef BFT_PAIR_UNROLL
+#define BFT_PAIR_UNROLL 24
+#endif
 __device__ inline void keccak_f1600_pair(uint32_t X[25], uint32_t odd) {
+#if BFT_PAIR_UNROLL > 1
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
     for (int rnd = 0; rnd < 24; ++rnd) {
         uint32_t c[5], cs[5], d[5], t[25], b[25];
 #pragma unroll
@@ -93,7 +103,8 @@ __device__ inline void keccak_f1600_pair(uint32_t X[25], uint32_t odd) {
 #pragma unroll
             for (int x = 0; x < 5; ++x)
                 X[5 * y + x] = b[5 * y + x] ^ (~b[5 * y + (x + 1) % 5] & b[5 * y + (x + 2) % 5]);
-        X[0] ^= KECCAK_RC_PAIR[odd][rnd];
+        if (BFT_PAIR_UNROLL > 1) X[0] ^= odd ? KECCAK_RC_HI[rnd] : KECCAK_RC_LO[rnd];   // unrolled: constants
+        else X[0] ^= KECCAK_RC_PAIR[odd][rnd];
     }
 }
 
