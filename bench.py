@@ -240,8 +240,9 @@ def stub_rank(args) -> None:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: 20 for cfg3, the driver's setting; 10 for the other workloads)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps first (default: 5 for cfg3, else 2)")
     ap.add_argument("--workload", choices=("cfg3", "cfg2", "cfg4", "drop64", "cfg5", "sig", "wire", "msgpath",
                                            "crypto"),
                     default="cfg3")
@@ -274,6 +275,10 @@ def main():
                          "weak number, 16,384 per GPU, is measured too and reported in config.weak), weak for the "
                          "other workloads")
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 20 if args.workload == "cfg3" else 10
+    if args.warmup is None:
+        args.warmup = 5 if args.workload == "cfg3" else 2
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))           # before anything touches the GPU
     if os.environ.get("BFTSIM_TESTING") == "1" and os.environ.get("BFTSIM_BENCH_STUB_DIR"):
