@@ -58,6 +58,9 @@ __global__ __launch_bounds__(64) void sig_sign_kernel(const Aff* gtab, const uin
 #ifndef SIG_RECOVER_WAVES
 #define SIG_RECOVER_WAVES 2
 #endif
+#ifndef SIG_LDS_TAB
+#define SIG_LDS_TAB 1
+#endif
 __global__ __launch_bounds__(64, SIG_RECOVER_WAVES) void sig_recover_kernel(const Aff* gtab, const uint8_t* dig, const uint8_t* sig,
                                                          uint64_t n, uint8_t* pub, uint8_t* addr,
                                                          const uint8_t* addr_in, uint8_t* ok) {
@@ -67,7 +70,12 @@ __global__ __launch_bounds__(64, SIG_RECOVER_WAVES) void sig_recover_kernel(cons
     load_bytes(dig + 32 * i, m, 32);
     load_bytes(sig + 65 * i, sg, 65);
     Aff q;
+#if SIG_LDS_TAB
+    __shared__ uint32_t tab_lds[64 * 64];                 // mul_var's 1q..4q, 64 words per lane (TabLds)
+    bool good = recover(m, sg, gtab, q, TabLds{tab_lds + threadIdx.x});
+#else
     bool good = recover(m, sg, gtab, q);
+#endif
     uint8_t a[20];
     if (good) pub_address(q, a);
     if (addr_in) {

@@ -472,8 +472,8 @@ SECP_FN bool jac_to_aff(const Jac& p, Aff& a) {
 constexpr uint32_t GTAB_WINDOWS = 32, GTAB_ENTRIES = 255;
 constexpr uint32_t GTAB_POINTS = GTAB_WINDOWS * GTAB_ENTRIES;
 
-SECP_FN Jac mul_g(const U256& k, const Aff* gtab) {
-    Jac acc = jac_inf();
+// acc + k * G (acc = infinity by default; recover passes u2 * R, saving the final general addition)
+SECP_FN Jac mul_g(const U256& k, const Aff* gtab, Jac acc = jac_inf()) {
     for (uint32_t w = 0; w < GTAB_WINDOWS; ++w) {
         uint32_t j = u_byte(k, w);
         if (j) acc = jac_add_aff(acc, gtab[w * GTAB_ENTRIES + (j - 1)]);
@@ -533,11 +533,36 @@ SECP_FN Aff aff_select4(const Aff& t0, const Aff& t1, const Aff& t2, const Aff& 
     }
     return r;
 }
+// The table 1q..4q of mul_var: in registers, selected by value (TabRegs), or in the workgroup's LDS (TabLds:
+// word k of entry j of lane l at w[(16 j + k) * 64 + l], so the lanes' differing j never share a bank), which
+// frees the 64 registers the table holds across the doubling chain
+struct TabRegs {
+    Aff t[4];
+    SECP_FN void put(int j, const Aff& a) { t[j] = a; }
+    SECP_FN Aff get(uint32_t j) const { return aff_select4(t[0], t[1], t[2], t[3], j); }
+    SECP_FN Aff first() const { return t[0]; }
+};
+struct TabLds {
+    uint32_t* w;                                 // the LDS array + this lane
+    SECP_FN void put(int j, const Aff& a) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { w[(16 * j + k) * 64] = a.x.v[k]; w[(16 * j + 8 + k) * 64] = a.y.v[k]; }
+    }
+    SECP_FN Aff get(uint32_t j) const {
+        Aff r;
+        const uint32_t* b = w + 1024u * j;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { r.x.v[k] = b[k * 64]; r.y.v[k] = b[(8 + k) * 64]; }
+        return r;
+    }
+    SECP_FN Aff first() const { return get(0); }
+};
 // k * P: GLV split, then radix-8 signed digits of both 128-bit halves in one doubling chain (129
 // doublings, <= 86 mixed additions). The table 1q..4q is made affine with one shared inversion
 // (Montgomery's trick), so every addition is mixed (7M + 4S) and the table is 64 registers selected
 // by value, not a scratch-memory array; the lambda table is derived on the fly as (beta x, +-y).
-SECP_FN Jac mul_var(const U256& k, const Aff& p) {
+template <class Tab = TabRegs>
+SECP_FN Jac mul_var(const U256& k, const Aff& p, Tab tab = Tab{}) {
     U256 k1, k2;
     split_lambda(k, k1, k2);
     const bool n1 = !u_ge(c_nhalf(), k1), n2 = !u_ge(c_nhalf(), k2);
@@ -546,7 +571,7 @@ SECP_FN Jac mul_var(const U256& k, const Aff& p) {
     Aff q = p;
     if (n1) q.y = fe_neg(q.y);
     const bool flip2 = n1 != n2;                 // lambda table = lambda * (i q), negated when the signs differ
-    Aff t0 = q, t1, t2, t3;
+    tab.put(0, q);
     {
         const Jac j1 = jac_dbl(jac_from_aff(q));                 // 2q, 3q, 4q (never infinity: prime order)
         const Jac j2 = jac_add_aff(j1, q);
@@ -558,9 +583,10 @@ SECP_FN Jac mul_var(const U256& k, const Aff& p) {
         const U256 z2 = fe_mul(inv, j1.z);
         const U256 z1 = fe_mul(inv, j2.z);
         const U256 z1s = fe_sqr(z1), z2s = fe_sqr(z2), z3s = fe_sqr(z3);
-        t1.x = fe_mul(j1.x, z1s); t1.y = fe_mul(j1.y, fe_mul(z1s, z1));
-        t2.x = fe_mul(j2.x, z2s); t2.y = fe_mul(j2.y, fe_mul(z2s, z2));
-        t3.x = fe_mul(j3.x, z3s); t3.y = fe_mul(j3.y, fe_mul(z3s, z3));
+        Aff a;
+        a.x = fe_mul(j1.x, z1s); a.y = fe_mul(j1.y, fe_mul(z1s, z1)); tab.put(1, a);
+        a.x = fe_mul(j2.x, z2s); a.y = fe_mul(j2.y, fe_mul(z2s, z2)); tab.put(2, a);
+        a.x = fe_mul(j3.x, z3s); a.y = fe_mul(j3.y, fe_mul(z3s, z3)); tab.put(3, a);
     }
     const U256 bias = r8_bias();
     U256 k1p, k2p;
@@ -568,9 +594,9 @@ SECP_FN Jac mul_var(const U256& k, const Aff& p) {
     u_add(k2p, k2, bias);
     const U256 beta = c_beta();
     Jac acc = jac_inf();
-    if ((k1p.v[4] >> 1) & 1u) acc = jac_add_aff(acc, t0);       // bit 129: top = 1
+    if ((k1p.v[4] >> 1) & 1u) acc = jac_add_aff(acc, tab.first());   // bit 129: top = 1
     if ((k2p.v[4] >> 1) & 1u) {
-        Aff t = t0;
+        Aff t = tab.first();
         t.x = fe_mul(t.x, beta);
         if (flip2) t.y = fe_neg(t.y);
         acc = jac_add_aff(acc, t);
@@ -580,13 +606,13 @@ SECP_FN Jac mul_var(const U256& k, const Aff& p) {
         if (!acc.inf) { acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); }
         const int d1 = (int)r8_digit(k1p, (uint32_t)w) - 4;
         if (d1 != 0) {
-            Aff t = aff_select4(t0, t1, t2, t3, (uint32_t)((d1 > 0 ? d1 : -d1) - 1));
+            Aff t = tab.get((uint32_t)((d1 > 0 ? d1 : -d1) - 1));
             if (d1 < 0) t.y = fe_neg(t.y);
             acc = jac_add_aff(acc, t);
         }
         const int d2 = (int)r8_digit(k2p, (uint32_t)w) - 4;
         if (d2 != 0) {
-            Aff t = aff_select4(t0, t1, t2, t3, (uint32_t)((d2 > 0 ? d2 : -d2) - 1));
+            Aff t = tab.get((uint32_t)((d2 > 0 ? d2 : -d2) - 1));
             t.x = fe_mul(t.x, beta);
             if ((d2 < 0) != flip2) t.y = fe_neg(t.y);
             acc = jac_add_aff(acc, t);
@@ -780,7 +806,8 @@ SECP_FN bool sign(const uint8_t* sec32, const uint8_t* msg32, const Aff* gtab, u
     return false;
 }
 // public key of a recoverable signature (libsecp256k1 ecdsa_recover); false if invalid
-SECP_FN bool recover(const uint8_t* msg32, const uint8_t* sig65, const Aff* gtab, Aff& q) {
+template <class Tab = TabRegs>
+SECP_FN bool recover(const uint8_t* msg32, const uint8_t* sig65, const Aff* gtab, Aff& q, Tab tab = Tab{}) {
     U256 r = u_from_be(sig65), s = u_from_be(sig65 + 32);
     uint32_t recid = sig65[64];
     if (recid > 3u || u_is_zero(r) || u_is_zero(s) || u_ge(r, c_n()) || u_ge(s, c_n())) return false;
@@ -800,7 +827,7 @@ SECP_FN bool recover(const uint8_t* msg32, const uint8_t* sig65, const Aff* gtab
     U256 rinv = sc_inv(r);
     U256 u1 = sc_neg(sc_mul(e, rinv));
     U256 u2 = sc_mul(s, rinv);
-    Jac Q = jac_add(mul_g(u1, gtab), mul_var(u2, R));
+    Jac Q = mul_g(u1, gtab, mul_var(u2, R, tab));      // u1 G + u2 R, G's additions onto u2 R
     return jac_to_aff(Q, q);
 }
 
