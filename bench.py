@@ -88,6 +88,37 @@ def pmc_traffic(workload: str = "cfg3"):
         os.path.relpath(files[-1], ROOT)
 
 
+def step_traffic(workload: str, batch: int):
+    """HBM bytes of one step (one launch) from the newest PMC summary of this workload: the launch's own kernels
+    (FAST + resume, or the general consensus kernel; the seed chain; the suffix rows) plus its share of a chain
+    dispatch. Writes are the attributed ones where the summary has them (an L2 eviction after every kernel of
+    unpipelined launches, one chain dispatch per launch: scripts/gpu_profile.sh), else the pipelined pass's
+    per-dispatch bytes with the chain dispatch divided by the launches it carries. Same unit as the line's
+    `hbm.algorithmic_bytes` (per step on this rank)."""
+    files = _pmc_files(workload)
+    if not files:
+        return None
+    ks = json.load(open(files[-1])).get("kernels", {})
+    names = ["bft_consensus_fast_kernel", "bft_consensus_resume_kernel"] if "bft_consensus_fast_kernel" in ks \
+        else ["bft_consensus_kernel"]
+    names += ["bft_seed_chain_kernel", "bft_hash_suffix_kernel", "bft_hash_chain_kernel"]
+    parts, attributed = {}, True
+    for k in names:
+        e = ks.get(k)
+        if not e:
+            continue
+        if "hbm_bytes_per_dispatch_attributed" in e:
+            parts[k] = e["hbm_bytes_per_dispatch_attributed"]          # per launch (attribution pass)
+        elif "hbm_bytes_per_dispatch" in e:
+            attributed = False
+            parts[k] = e["hbm_bytes_per_dispatch"] / (batch if k == "bft_hash_chain_kernel" else 1)
+    if not parts:
+        return None
+    return {"bytes_per_step": sum(parts.values()), "per_kernel_bytes_per_step": parts,
+            "writes": "attributed (L2 eviction after every kernel)" if attributed else "as counted (pipelined pass)",
+            "source": os.path.relpath(files[-1], ROOT)}
+
+
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2   # wave64 VALU instructions/s: one per 2 cycles per SIMD (SIMD-32)
 SALU_ISSUE_PEAK = 256 * 2.4e9           # scalar instructions/s: one scalar unit per CU, one per cycle
 
@@ -131,11 +162,31 @@ def usable_cpus() -> int:
     return n
 
 
+def native_oracle():
+    """SURVEY §8d builds the CPU comparator -O3 -march=native for the host it runs on; the shipped
+    oracle/_build/liboracle.so comes from the build container (-O3 -mpopcnt, another CPU). Builds
+    `make -C oracle native` into a private temporary directory here and points the oracle loader at it.
+    Returns the build flags used (the shipped library's if the build fails)."""
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    d = tempfile.mkdtemp(prefix="bftsim_oracle_native_")
+    try:
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native", f"NATIVE={d}"], check=True,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=120)
+        if O._lib is None:
+            O.LIB_PATH = os.path.join(d, "liboracle.so")
+            return "-O3 -march=native (built on this host)"
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return "-O3 -mpopcnt (shipped build)"
+
+
 def cpu_baseline(cfg, sample: int, threads: int, name: str = "cfg3"):
     """The C oracle (oracle/, a scalar restatement of the reference handlers) timed on this
     host's cores over a bounded sample of the same workload: every usable core (`value`),
     beside a 16-thread and a single-thread rate."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    build = native_oracle()
     import oracle_lib as O
 
     def timed(n_inst, nthr):
@@ -152,7 +203,7 @@ def cpu_baseline(cfg, sample: int, threads: int, name: str = "cfg3"):
     views, secs = timed(sample, threads)
     out = dict(value=views / secs, unit="instance-rounds/s", cores=threads, kind="port",
                sample=f"{sample} {name} instances ({views} instance-rounds) on {threads} threads, "
-                      f"{secs:.1f} s", host=host_cpu())
+                      f"{secs:.1f} s", host=host_cpu(), build=build)
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else threads
     if aff > threads:                         # the affinity mask, oversubscribing the quota
         va, sa = timed(sample, aff)
@@ -343,11 +394,12 @@ def main():
     else:
         I = args.instances
         first = rank * I
+    from bftsim.configs import timed_pipeline
     auto_depth = args.pipeline_depth is None
     if auto_depth:
-        args.pipeline_depth = 6 if I >= 12_288 else 16
+        args.pipeline_depth = timed_pipeline(I)[0]
     if args.hash_batch is None:
-        args.hash_batch = 2 if I >= 12_288 else 8
+        args.hash_batch = timed_pipeline(I)[1]
     sim.set_pipeline(pipelined, args.pipeline_depth)
     sim.set_hash_batch(args.hash_batch)
     if c5:
@@ -411,8 +463,8 @@ def main():
     if args.scaling == "strong" and world > 1:
         Iw, first_w = args.instances, rank * args.instances
         if auto_depth:
-            sim.set_pipeline(pipelined, 6 if Iw >= 12_288 else 16)
-            sim.set_hash_batch(2 if Iw >= 12_288 else 8)
+            sim.set_pipeline(pipelined, timed_pipeline(Iw)[0])
+            sim.set_hash_batch(timed_pipeline(Iw)[1])
         sim.prepare(Iw)
         for _ in range(max(args.warmup, 1)):
             sim.launch(first_w, stream)
@@ -447,6 +499,7 @@ def main():
         pmc_key = f"cfg4_n{cfg.n}" if wl == "cfg4" else wl
         traffic, traffic_src = pmc_traffic(pmc_key)
         algo_bytes = ALGO_BYTES_PER_VIEW * views_rank
+        stp = step_traffic(pmc_key, args.hash_batch if pipelined else 1)
         def trim(h):
             h = list(h)
             while h and h[-1] == 0:
@@ -490,7 +543,11 @@ def main():
             "roofline": {
                 "bound": "valu", "kernel": dom, "achieved": achieved, "peak": peak,
                 "unit": "Tops/s", "frac": achieved / peak,
-                "traffic": (traffic or {}).get(dom),
+                # HBM bytes per step (PMC, all kernels of one launch), in the unit of hbm.algorithmic_bytes
+                "traffic": stp["bytes_per_step"] if stp else None,
+                "traffic_unit": "HBM bytes per step (one launch of this rank)",
+                "traffic_step": stp,
+                "traffic_dominant_per_dispatch": (traffic or {}).get(dom),
                 # what the hardware issues, beside the algorithmic model: VALU wave-instructions of
                 # the profiled launch (PMC) per second of this run's kernel time vs the issue peak
                 "issue": (lambda q: None if q is None else {
@@ -503,8 +560,12 @@ def main():
                                            "salu": q["salu"] / max(views_rank * batch, 1)}})(pmc_issue(pmc_key, dom)),
                 "dispatch": {"launches_per_dispatch": batch, "ops_per_dispatch": ops, "ms_per_dispatch": ms},
                 "traffic_source": traffic_src,
-                "hbm": {"algorithmic_bytes": algo_bytes, "achieved_GBps": algo_bytes / (ms / 1e3) / 1e9,
-                        "peak_GBps": HBM_PEAK / 1e9, "frac": algo_bytes / (ms / 1e3) / HBM_PEAK},
+                "hbm": {"algorithmic_bytes": algo_bytes, "unit": "bytes per step",
+                        "achieved_GBps": algo_bytes / (ms_step / 1e3) / 1e9,
+                        "peak_GBps": HBM_PEAK / 1e9, "frac": algo_bytes / (ms_step / 1e3) / HBM_PEAK,
+                        "traffic_bytes": stp["bytes_per_step"] if stp else None,
+                        "traffic_over_algorithmic": stp["bytes_per_step"] / algo_bytes if stp and algo_bytes else None,
+                        "traffic_GBps": stp["bytes_per_step"] / (ms_step / 1e3) / 1e9 if stp else None},
                 "kernel_ms": {"bft_consensus_kernel": cms, "bft_hash_kernel": hms},   # per launch
                 # both kernels' fractions, whichever is dominant, and the whole step against the full
                 # per-instance-round model (consensus + one header hash per committed height). The hash
@@ -543,14 +604,15 @@ MAD_PEAK = 256 * 32 * 2.4e9             # v_mad_u64_u32 per s: quarter rate (bui
 
 def sig_cpu_baseline(digs, sigs, sample: int, threads: int):
     """The C oracle (oracle/secp_oracle.c: 64-bit limbs, double-and-add) on this host's cores."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    build = native_oracle()
     import oracle_lib as O
     t = time.perf_counter()
     _, ok = O.secp_recover_batch(digs[:sample], sigs[:sample], threads)
     secs = time.perf_counter() - t
     assert ok.all()
     return dict(value=sample / secs, unit="recoveries/s", cores=threads, kind="port",
-                sample=f"{sample} recoveries of the same batch by the C oracle on {threads} threads, {secs:.1f} s")
+                sample=f"{sample} recoveries of the same batch by the C oracle on {threads} threads, {secs:.1f} s",
+                build=build)
 
 
 METRIC_CRYPTO = "real-crypto cfg3 instance-rounds/sec (whole node), N=64 f=21; every broadcast signed and recovered"
@@ -624,7 +686,7 @@ def main_crypto(args):
             try:
                 # the reference recovers each message at each of its N receivers (core.rs:314-322) and each
                 # seal at each receiver (commit.rs:94-100); priced at the C oracle's measured recovery rate
-                sys.path.insert(0, os.path.join(ROOT, "tests"))
+                build = native_oracle()
                 import oracle_lib as O
                 from bftsim.sig import Signer
                 sg = Signer(local)
@@ -644,7 +706,8 @@ def main_crypto(args):
                 out["cpu_baseline"] = dict(
                     value=rate / per_view, unit="instance-rounds/s", cores=thr, kind="port",
                     sample=f"{m} recoveries by the C oracle on {thr} threads in {secs:.1f} s ({rate:.0f}/s), "
-                           f"x {per_view:.0f} recoveries per instance-round (each message and seal at 64 receivers)")
+                           f"x {per_view:.0f} recoveries per instance-round (each message and seal at 64 receivers)",
+                    build=build)
             except Exception as e:          # noqa: BLE001
                 out["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(out), flush=True)

@@ -17,7 +17,7 @@ SHORT = {"bft_consensus_fast_kernel": "bft_consensus_fast_kernel",
          "bft_consensus_resume_kernel": "bft_consensus_resume_kernel",
          "bft_consensus_kernel": "bft_consensus_kernel", "bft_hash_pair_kernel": "bft_hash_kernel",
          "bft_hash_lane_kernel": "bft_hash_kernel", "bft_hash_suffix_kernel": "bft_hash_suffix_kernel",
-         "bft_hash_chain_kernel": "bft_hash_chain_kernel",
+         "bft_hash_chain_kernel": "bft_hash_chain_kernel", "bft_seed_chain_kernel": "bft_seed_chain_kernel",
          "bft_stats_kernel": "bft_stats_kernel", "bft_tip_kernel": "bft_tip_kernel"}
 
 
@@ -43,6 +43,30 @@ def counters(path):
     return acc, meta
 
 
+def attributed_writes(path):
+    """The attribution pass (BFTSIM_PMC_EVICT=1, unpipelined: one queue): every kernel of a launch is followed
+    by bft_l2_evict_kernel, which reads 64 MiB and so writes back what the kernel left dirty in L2. A kernel's
+    attributed WRITE_SIZE = its own + that of the eviction right after it (same queue, next dispatch)."""
+    rows = []
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == "WRITE_SIZE":
+                rows.append((int(r["Queue_Id"]), int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"])))
+    rows.sort()
+    acc = defaultdict(list)
+    for i, (q, _, name, v) in enumerate(rows):
+        k = short(name)
+        if not k or "bft_l2_evict_kernel" in name:
+            continue
+        ev = 0.0
+        if i + 1 < len(rows) and rows[i + 1][0] == q and "bft_l2_evict_kernel" in rows[i + 1][2]:
+            ev = rows[i + 1][3]
+        acc[k].append((1024.0 * v, 1024.0 * ev))
+    return {k: {"write_bytes_own": sum(a for a, _ in v) / len(v), "write_bytes_evicted_after": sum(b for _, b in v) / len(v),
+                "write_bytes_attributed": sum(a + b for a, b in v) / len(v), "dispatches": len(v)}
+            for k, v in acc.items()}
+
+
 def stats(path):
     out = {}
     for f in glob.glob(os.path.join(path, "**", "*kernel_stats.csv"), recursive=True):
@@ -61,9 +85,10 @@ def main():
     fetch, meta = counters(os.path.join(root, "fetch"))
     write, meta2 = counters(os.path.join(root, "write"))
     sq, meta3 = counters(os.path.join(root, "sq"))
+    attr = attributed_writes(os.path.join(root, "write_evict")) if os.path.isdir(os.path.join(root, "write_evict")) else {}
     meta.update(meta2)
     meta.update(meta3)
-    for k in set(st) | set(fetch) | set(write) | set(sq):
+    for k in set(st) | set(fetch) | set(write) | set(sq) | set(attr):
         e = dict(meta.get(k, {}))
         if k in st:
             e.update(avg_ms=st[k]["avg_ns"] / 1e6, calls=st[k]["calls"])
@@ -76,6 +101,12 @@ def main():
             e["write_bytes"] = 1024.0 * sum(w) / len(w)
         if f and w:
             e["hbm_bytes_per_dispatch"] = e["fetch_bytes"] + e["write_bytes"]
+        if k in attr:
+            # writes measured with an L2 eviction after every kernel (unpipelined launches): the kernel's own
+            # write-backs, none borrowed from or lent to its neighbours
+            e["write_attribution"] = attr[k]
+            if f:
+                e["hbm_bytes_per_dispatch_attributed"] = e["fetch_bytes"] + attr[k]["write_bytes_attributed"]
         for c, v in sq.get(k, {}).items():
             e[c] = sum(v) / len(v)
         res["kernels"][k] = e

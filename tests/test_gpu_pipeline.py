@@ -88,27 +88,81 @@ def test_pipeline_toggle_and_sizes():
         sim.close()
 
 
-def test_timed_mode_full_size():
-    """The exact mode bench.py times: cfg3 at 16,384 instances, pipeline depth 3 (so the hash pass is
-    the block-hash pass (bft_hash_suffix_kernel + bft_hash_chain_kernel) on its set's stream under the ring), repeated launches of the same instances;
-    the last launch's results against the oracle over every instance."""
-    from bftsim.configs import INSTANCES
-    cfg = cfg3()
-    n = INSTANCES["cfg3"]
+def _timed_run(cfg, first, n, launches=25):
+    """bench.py's timed mode for n instances per GPU: the pipeline depth and hash batch it picks
+    (bftsim.configs.timed_pipeline), then `launches` launches of the same instances (its 5 warmup + 20 timed
+    steps), the last one's results fetched."""
+    from bftsim.configs import timed_pipeline
+    depth, batch = timed_pipeline(n)
     sim = _sim(cfg)
     try:
-        sim.set_pipeline(True, 3)
+        sim.set_pipeline(True, depth)
+        sim.set_hash_batch(batch)
         sim.prepare(n)
-        for _ in range(5):                       # wraps the ring of three sets
-            sim.launch(0)
+        for _ in range(launches):
+            sim.launch(first)
         sim.sync()
         got = sim.fetch()
         st = sim.stats()
     finally:
         sim.close()
+    return got, st, (depth, batch)
+
+
+def test_timed_mode_full_size():
+    """The exact configuration of the headline number: cfg3 at 16,384 instances on one GPU with bench.py's
+    pipeline depth and hash batch (6 x 2), 25 launches of the same instances; every instance against the
+    oracle."""
+    from bftsim.configs import INSTANCES
+    cfg = cfg3()
+    n = INSTANCES["cfg3"]
+    got, st, (depth, batch) = _timed_run(cfg, 0, n)
+    assert (depth, batch) == (6, 2)
     ref = O.run(cfg, 0, n, threads=16)
-    assert_same(ref, got, "cfg3 16384 pipelined x5")
+    assert_same(ref, got, f"cfg3 {n} depth {depth} batch {batch} x25")
     assert st["views"] == int(ref["views"].sum()) == n * 100
+
+
+def test_strong_shard_timed_mode():
+    """The 8-GPU strong-scaling shard of BASELINE configs[2] (rank 7's 2,048 of 16,384 instances) with the
+    settings bench.py picks for it (depth 16 x batch 8), 25 launches; every instance against the oracle."""
+    from bftsim.distributed import strong_shard
+    cfg = cfg3()
+    first, n = strong_shard(7, 8, 16_384)
+    got, st, (depth, batch) = _timed_run(cfg, first, n)
+    assert (n, depth, batch) == (2048, 16, 8)
+    ref = O.run(cfg, first, n, threads=16)
+    assert_same(ref, got, f"cfg3 shard {first}+{n} depth {depth} batch {batch} x25")
+    assert st["views"] == int(ref["views"].sum()) == n * 100
+
+
+def test_batch_split_on_launch_size_change():
+    """A launch of another size while chains are pending in the hash batch starts a batch of its own (the
+    chain kernel runs every launch of a batch with one instance count and suffix-row stride)."""
+    cfg = cfg3(heights=30)
+    sim = _sim(cfg)
+    try:
+        sim.set_pipeline(True, 8)
+        sim.set_hash_batch(4)
+        sim.prepare(96)
+        sim.launch(0)
+        a = sim.fetch()                          # flushes the pending batch
+        sim.launch(96)
+        sim.prepare(64)                          # fits the tables: no re-allocation, no flush
+        sim.launch(300)
+        sim.sync()
+        b = sim.fetch()
+        sim.prepare(96)
+        sim.launch(500)
+        sim.launch(700)
+        sim.prepare(33)
+        sim.launch(900)
+        c = sim.fetch()
+    finally:
+        sim.close()
+    assert_same(O.run(cfg, 0, 96), a, "96 at 0")
+    assert_same(O.run(cfg, 300, 64), b, "64 after 96")
+    assert_same(O.run(cfg, 900, 33), c, "33 after 96 x2")
 
 
 @pytest.mark.gpu
@@ -138,9 +192,9 @@ def test_chunked_hash_pass(monkeypatch):
 
 
 @pytest.mark.parametrize("chain", ["wave", "pair"])
-def test_small_shard_timed_mode(chain, monkeypatch):
-    """The strong-scaling shard of 8 GPUs (2,048 cfg3 instances per GPU), as bench.py times it (pipeline depth
-    3, concurrent launches, repeated launches of the same instances), with both chain kernels."""
+def test_small_shard_both_chain_kernels(chain, monkeypatch):
+    """The 2,048-instance shard at pipeline depth 3 (concurrent launches, repeated launches of the same
+    instances) with both chain kernels: one wave per instance (an A/B arm) and lane pairs (the product)."""
     monkeypatch.setenv("BFTSIM_TESTING", "1")
     monkeypatch.setenv("BFTSIM_CHAIN_WAVE_MAX", "1000000" if chain == "wave" else "0")
     cfg = cfg3()
