@@ -360,7 +360,7 @@ def main():
     if args.heights is None:
         args.heights = 10_000 if c5 else 100
     if args.cpu_sample is None:
-        args.cpu_sample = {"cfg5": 512, "cfg2": 16_384, "cfg4": 1024 if args.n > 64 else 8192}.get(wl, 16_384)
+        args.cpu_sample = {"cfg5": 4096, "cfg2": 16_384, "cfg4": 1024 if args.n > 64 else 8192}.get(wl, 16_384)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

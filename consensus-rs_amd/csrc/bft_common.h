@@ -97,7 +97,7 @@ constexpr uint32_t MLOG_FORGED = 1u, MLOG_WILD = 2u, MLOG_EQUIV = 4u, MLOG_OLD =
 constexpr uint32_t FLAG_SAFETY = 1u, FLAG_PHASE_CAP = 2u, FLAG_CORE_PANIC = 4u, FLAG_OUTBOX = 8u,
                    FLAG_TIMEOUT = 16u, FLAG_RCS_OVERFLOW = 32u, FLAG_WINDOW = 64u;
 constexpr uint32_t HIST_BINS = 130;     // [0,65) rounds-to-commit, [65,130) commit latency (ticks)
-constexpr int NSTAMP = 16;               // diagnostic builds (BFT_STAMPS): sections per wave
+constexpr int NSTAMP = 18;               // diagnostic builds (BFT_STAMPS): sections per wave
 
 // State (src/protocol/mod.rs:25-30)
 constexpr uint32_t ST_ACCEPT_REQUEST = 1, ST_PREPREPARED = 2, ST_PREPARED = 3, ST_COMMITTED = 4;

@@ -29,6 +29,41 @@ struct WaveHip {
     __device__ static uint32_t bperm(uint32_t addr, uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)addr, (int)v); }
     // the value of lane ^ 1 (DPP quad_perm [1,0,3,2])
     __device__ static uint32_t pair_swap(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false); }
+    // Keccak-f[1600] by lane pairs: the even lane of a pair holds the low 32-bit half of every state word, the odd
+    // lane the high half (the layout of kern_fast.hip's chains). A 64-bit rotation is one v_alignbit_b32 of this
+    // lane's half and the partner's (DPP quad_perm [1,0,3,2]); theta's parities, chi and iota are half-local. The
+    // round loop is kept (the general kernels' code size); its round constant is a uniform scalar load.
+    template <uint32_t N> __device__ static uint32_t rotl_pair(uint32_t mine, uint32_t other) {
+        if constexpr (N == 0) return mine;
+        else if constexpr (N == 32) return other;
+        else if constexpr (N < 32) return __builtin_amdgcn_alignbit(mine, other, 32 - N);
+        else return __builtin_amdgcn_alignbit(other, mine, 64 - N);
+    }
+    __device__ static void keccak_pair(uint32_t X[25], uint32_t odd) {
+#pragma unroll 1
+        for (int rnd = 0; rnd < 24; ++rnd) {
+            uint32_t c[5], d[5], t[25], b[25];
+#pragma unroll
+            for (int x = 0; x < 5; ++x) c[x] = X[x] ^ X[x + 5] ^ X[x + 10] ^ X[x + 15] ^ X[x + 20];
+#pragma unroll
+            for (int x = 0; x < 5; ++x) d[x] = c[(x + 4) % 5] ^ rotl_pair<1>(c[(x + 1) % 5], pair_swap(c[(x + 1) % 5]));
+#pragma unroll
+            for (int i = 0; i < 25; ++i) t[i] = X[i] ^ d[i % 5];
+#define BFT_RHO_P(i, n, j) b[j] = rotl_pair<n>(t[i], (n) ? pair_swap(t[i]) : 0u);
+            BFT_RHO_P(0, 0, 0) BFT_RHO_P(1, 1, 10) BFT_RHO_P(2, 62, 20) BFT_RHO_P(3, 28, 5) BFT_RHO_P(4, 27, 15)
+            BFT_RHO_P(5, 36, 16) BFT_RHO_P(6, 44, 1) BFT_RHO_P(7, 6, 11) BFT_RHO_P(8, 55, 21) BFT_RHO_P(9, 20, 6)
+            BFT_RHO_P(10, 3, 7) BFT_RHO_P(11, 10, 17) BFT_RHO_P(12, 43, 2) BFT_RHO_P(13, 25, 12) BFT_RHO_P(14, 39, 22)
+            BFT_RHO_P(15, 41, 23) BFT_RHO_P(16, 45, 8) BFT_RHO_P(17, 15, 18) BFT_RHO_P(18, 21, 3) BFT_RHO_P(19, 8, 13)
+            BFT_RHO_P(20, 18, 14) BFT_RHO_P(21, 2, 24) BFT_RHO_P(22, 61, 9) BFT_RHO_P(23, 56, 19) BFT_RHO_P(24, 14, 4)
+#undef BFT_RHO_P
+#pragma unroll
+            for (int y = 0; y < 5; ++y)
+#pragma unroll
+                for (int x = 0; x < 5; ++x)
+                    X[5 * y + x] = b[5 * y + x] ^ (~b[5 * y + (x + 1) % 5] & b[5 * y + (x + 2) % 5]);
+            X[0] ^= odd ? KECCAK_RC_HI[rnd] : KECCAK_RC_LO[rnd];
+        }
+    }
     // set bits of m below this lane (v_mbcnt_lo / hi)
     __device__ static uint32_t rank_below(uint64_t m) {
         return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));

@@ -131,6 +131,9 @@ struct Sim {
     static constexpr bool EXT = MODE == MODE_EXT;
     // the wave-cooperative header hash of closed-form commits (resolve_deferred_hash)
     static constexpr bool WAVE_HASH = NEED_SEED && S == 64 && MODE == MODE_FULL;
+    // segments of 4..32 lanes (several instances per wave): a closed-form commit's header is hashed after the
+    // delivery by lane pairs of its segment (resolve_deferred_hash_seg), not by every committing lane alone
+    static constexpr bool SEG_HASH = NEED_SEED && S < 64 && MODE == MODE_FULL;
     static_assert(MODE != MODE_RESUME || S == 64, "hand-over modes are for one instance per wave");
     using LY = Layout<S>;
     static constexpr int NW = LY::NW;
@@ -382,6 +385,79 @@ struct Sim {
         sync();
     }
 
+    // the deferred hashes of this phase's closed-form Core commits, segments of S < 64 lanes: per segment the
+    // first committer's block is hashed by lane pairs (every pair of the segment computes it; its header encoded
+    // by that committer into its LDS buffer), and taken by every committer of the same block; any other block
+    // by its own lane. Same hashes and seeds as chain_insert_core's lane_block_hash.
+    BFT_FN void resolve_deferred_hash_seg() {
+        const bool pend = hash_defer;
+        const M pb = ballot(pend);
+        if (pb.none()) return;
+        hash_defer = false;
+        const uint64_t sb = (pb.w[0] >> seg_base) & ((1ull << (S & 63u)) - 1ull);
+        const uint32_t lead = seg_base + (sb ? (uint32_t)__builtin_ctzll(sb) : 0u);
+        const uint32_t x0 = wv.shfl(commit_x, lead);
+        const uint64_t b0 = (uint64_t)wv.shfl((uint32_t)commit_blk, lead) |
+                            ((uint64_t)wv.shfl((uint32_t)(commit_blk >> 32), lead) << 32);
+        const uint32_t* wb = (const uint32_t*)(lds + LDS_SCR_OFF + lead * LANE_HASH_BUF);
+        uint32_t nb = 0;
+        if ((sb != 0u) & (lane == lead)) {
+            uint32_t prev[8];
+            prev_hash_words(x0 - 1u, prev);
+            const uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b0) + 1ull);
+            nb = header_words((uint64_t*)(lds + LDS_SCR_OFF + lane * LANE_HASH_BUF), prev, P.addresses + 20u * blk_prop(b0),
+                              P.seed, inst, x0, blk_prop(b0), blk_var(b0), time);
+        }
+        BFT_STAMP(16);                                            // (diagnostic) the lead's header encoding
+        const uint32_t nbm = ballot(nb > 2u).any() ? 3u : 2u;     // rate blocks: 2 or 3 (header_words)
+        nb = wv.shfl(nb, lead);
+        sync();                                                   // the headers in LDS
+        const uint32_t odd = lane & 1u;
+        uint32_t X[25], h4[4];
+#pragma unroll
+        for (int i = 0; i < 25; ++i) X[i] = 0;
+        for (uint32_t blk = 0; blk < nbm; ++blk) {
+#pragma unroll
+            for (uint32_t i = 0; i < 17u; ++i) X[i] ^= wb[34u * blk + 2u * i + odd];
+            wv.keccak_pair(X, odd);                              // W: lane pairs (bft_hip.h), one collective (emulator)
+            const bool fin = blk + 1u == nb;                      // a 2-block header's hash is taken here
+#pragma unroll
+            for (int i = 0; i < 4; ++i) h4[i] = (fin | (blk == 0u)) ? X[i] : h4[i];
+        }
+        BFT_STAMP(17);                                            // (diagnostic) the lane-pair permutations
+        uint32_t out[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t o = wv.pair_swap(h4[i]);
+            out[2 * i] = odd ? o : h4[i];
+            out[2 * i + 1] = odd ? h4[i] : o;
+        }
+        sync();                                                   // header buffers read before any rewrite
+        const bool same = pend & (commit_x == x0) & (commit_blk == b0);
+        if (same) {
+            uint32_t* hs = (uint32_t*)(lds + LDS_CHASH_OFF + lane * 32);
+            for (int i = 0; i < 8; ++i) hs[i] = out[i];
+            const uint32_t sd = seed_from_words(out[0], out[1], nval(), P.seed_le != 0);
+            commit_seed = sd;
+            last_seed = sd;
+        }
+        if (pend & !same) {
+            uint32_t prev[8], o[8];
+            const uint64_t b = commit_blk;
+            const uint32_t x = commit_x;
+            prev_hash_words(x - 1u, prev);
+            const uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
+            lane_block_hash(lds + LDS_SCR_OFF + lane * LANE_HASH_BUF, prev, P.addresses + 20u * blk_prop(b),
+                            P.seed, inst, x, blk_prop(b), blk_var(b), time, o);
+            uint32_t* hs = (uint32_t*)(lds + LDS_CHASH_OFF + lane * 32);
+            for (int i = 0; i < 8; ++i) hs[i] = o[i];
+            const uint32_t sd = seed_from_words(o[0], o[1], nval(), P.seed_le != 0);
+            commit_seed = sd;
+            last_seed = sd;
+        }
+        sync();
+    }
+
     BFT_FN uint32_t canon_seed(uint32_t x) {
         if (x == 0) return P.genesis_seed;
         if (x == canon_h) return canon_tip_seed;
@@ -490,7 +566,7 @@ struct Sim {
 #endif
         }
         uint32_t sd = 0;
-        if (WAVE_HASH && in_pc) {
+        if ((WAVE_HASH || SEG_HASH) && in_pc) {
             // the closed form delivers the whole phase: nothing reads this commit's hash or seed before
             // resolve_commits, and resolve_deferred_hash runs just before it
             hash_defer = true;
@@ -1681,6 +1757,7 @@ struct Sim {
                 if (pub) sync();                              // records read before the next publish
                 BFT_STAMP(3);
                 if constexpr (WAVE_HASH) resolve_deferred_hash();
+                if constexpr (SEG_HASH) resolve_deferred_hash_seg();
                 const uint32_t xc = resolve_commits();
                 BFT_STAMP(4);
                 if (frozen) act = false;

@@ -27,10 +27,8 @@ __global__ __launch_bounds__(64) void sig_address_kernel(const Aff* gtab, const 
                                                          uint8_t* pub, uint8_t* addr, uint8_t* ok) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    uint8_t s[32];
-    load_bytes(sec + 32 * i, s, 32);
     Aff q;
-    bool good = secret_to_pub(s, gtab, q);
+    bool good = secret_to_pub(sec + 32 * i, gtab, q);
     uint8_t a[20];
     if (good) pub_address(q, a);
     if (pub) {
@@ -46,11 +44,9 @@ __global__ __launch_bounds__(64) void sig_sign_kernel(const Aff* gtab, const uin
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t ki = key_index ? key_index[i] : i;
-    uint8_t s[32], m[32], out[65];
-    load_bytes(sec + 32 * ki, s, 32);
-    load_bytes(dig + 32 * i, m, 32);
-    bool good = sign(s, m, gtab, out);
-    for (int k = 0; k < 65; ++k) sig[65 * i + k] = good ? out[k] : 0;
+    // records straight from / to global memory: local byte arrays indexed in loops would live in scratch
+    bool good = sign(sec + 32 * ki, dig + 32 * i, gtab, sig + 65 * i);
+    if (!good) zero_bytes(sig + 65 * i, 65);
     ok[i] = good ? 1 : 0;
 }
 
@@ -66,9 +62,8 @@ __global__ __launch_bounds__(64, SIG_RECOVER_WAVES) void sig_recover_kernel(cons
                                                          const uint8_t* addr_in, uint8_t* ok) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    uint8_t m[32], sg[65];
-    load_bytes(dig + 32 * i, m, 32);
-    load_bytes(sig + 65 * i, sg, 65);
+    const uint8_t* m = dig + 32 * i;                     // read in place (no local byte copies: scratch)
+    const uint8_t* sg = sig + 65 * i;
     Aff q;
 #if SIG_LDS_TAB
     __shared__ uint32_t tab_lds[64 * 64];                 // mul_var's 1q..4q, 64 words per lane (TabLds)

@@ -23,11 +23,20 @@ namespace bft {
 #ifndef BFT_WG_PER_CU_128
 #define BFT_WG_PER_CU_128 2
 #endif
-template <uint32_t S>
-constexpr int min_blocks_per_cu() { return S == 256 ? BFT_WG_PER_CU_256 : S == 128 ? BFT_WG_PER_CU_128 : BFT_WAVES_PER_SIMD; }
+// several instances per wave with in-kernel hashes (S < 64, N not a power of two or little-endian seeds: cfg5):
+// the header hash needs registers beside the validator state (3 waves per SIMD: 168 VGPRs + 264 B/lane of
+// scratch, 207 GB of spill writes per cfg5 launch; 2: 240 VGPRs, none: cfg5 1.80e8 -> 1.93e8, profiles/r05/ab_cfg5)
+#ifndef BFT_SEED_WAVES_PER_SIMD
+#define BFT_SEED_WAVES_PER_SIMD 2
+#endif
+template <bool NS, uint32_t S>
+constexpr int min_blocks_per_cu() {
+    return S == 256 ? BFT_WG_PER_CU_256 : S == 128 ? BFT_WG_PER_CU_128 : (NS && S < 64) ? BFT_SEED_WAVES_PER_SIMD
+                                                                                       : BFT_WAVES_PER_SIMD;
+}
 
 template <bool NEED_SEED, int MODE, uint32_t S>
-__global__ __launch_bounds__(S > 64 ? S : 64, min_blocks_per_cu<S>()) void bft_consensus_kernel(Params p) {
+__global__ __launch_bounds__(S > 64 ? S : 64, (min_blocks_per_cu<NEED_SEED, S>())) void bft_consensus_kernel(Params p) {
     extern __shared__ uint8_t lds[];
     if constexpr (S > 64) {
         Sim<GroupHip<(int)(S / 64)>, NEED_SEED, S, MODE> sim(p, lds, blockIdx.x);

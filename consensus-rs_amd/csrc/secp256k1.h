@@ -474,8 +474,14 @@ constexpr uint32_t GTAB_POINTS = GTAB_WINDOWS * GTAB_ENTRIES;
 
 // acc + k * G (acc = infinity by default; recover passes u2 * R, saving the final general addition)
 SECP_FN Jac mul_g(const U256& k, const Aff* gtab, Jac acc = jac_inf()) {
+    // window w's byte from a copy shifted right by 8 per window: u_byte(k, w) at a loop-variable w indexes the
+    // limbs dynamically, which puts k in scratch memory
+    U256 t = k;
     for (uint32_t w = 0; w < GTAB_WINDOWS; ++w) {
-        uint32_t j = u_byte(k, w);
+        const uint32_t j = t.v[0] & 255u;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) t.v[i] = (t.v[i] >> 8) | (t.v[i + 1] << 24);
+        t.v[7] >>= 8;
         if (j) acc = jac_add_aff(acc, gtab[w * GTAB_ENTRIES + (j - 1)]);
     }
     return acc;
@@ -601,16 +607,26 @@ SECP_FN Jac mul_var(const U256& k, const Aff& p, Tab tab = Tab{}) {
         if (flip2) t.y = fe_neg(t.y);
         acc = jac_add_aff(acc, t);
     }
+    // digits from the top (w = 42 .. 0) out of copies shifted left by 3 per step: bits 126..128 of the copy are
+    // digit w (r8_digit at a loop-variable w indexes the limbs dynamically: scratch memory)
+    uint32_t s1[5], s2[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) { s1[i] = k1p.v[i]; s2[i] = k2p.v[i]; }
 #pragma unroll 1
     for (int w = 42; w >= 0; --w) {
         if (!acc.inf) { acc = jac_dbl(acc); acc = jac_dbl(acc); acc = jac_dbl(acc); }
-        const int d1 = (int)r8_digit(k1p, (uint32_t)w) - 4;
+        const uint32_t r1 = ((s1[3] >> 30) | (s1[4] << 2)) & 7u, r2 = ((s2[3] >> 30) | (s2[4] << 2)) & 7u;
+#pragma unroll
+        for (int i = 4; i > 0; --i) { s1[i] = (s1[i] << 3) | (s1[i - 1] >> 29); s2[i] = (s2[i] << 3) | (s2[i - 1] >> 29); }
+        s1[0] <<= 3;
+        s2[0] <<= 3;
+        const int d1 = (int)r1 - 4;
         if (d1 != 0) {
             Aff t = tab.get((uint32_t)((d1 > 0 ? d1 : -d1) - 1));
             if (d1 < 0) t.y = fe_neg(t.y);
             acc = jac_add_aff(acc, t);
         }
-        const int d2 = (int)r8_digit(k2p, (uint32_t)w) - 4;
+        const int d2 = (int)r2 - 4;
         if (d2 != 0) {
             Aff t = tab.get((uint32_t)((d2 > 0 ? d2 : -d2) - 1));
             t.x = fe_mul(t.x, beta);
@@ -696,29 +712,66 @@ struct Sha256 {
         for (int i = 0; i < 8; ++i) out[i] = st[i];
     }
 };
-// HMAC-SHA256 with a 32-byte key (8 BE words) over V (8 words) || [sep byte] || [64 data bytes]
+// HMAC-SHA256 with a 32-byte key (8 BE words) over V (8 words) || [sep byte] || [64 data bytes], the three
+// shapes RFC 6979 uses (sep without data, neither, both). Blocks are laid out by compile-time positions and the
+// compressions run in one loop with ONE sha256_compress site: the streaming Sha256 above indexes its block by
+// the running byte count, and separate non-inlined calls pass their arrays through the stack -- both scratch
+// memory on the device (sig_sign_kernel had 368 B/lane).
 BFT_FN void hmac_kv(const uint32_t key[8], const uint32_t v[8], int sep, const uint32_t* data16, uint32_t out[8]) {
-    uint32_t pad[8];
-    Sha256 s;
-    s.init();
-    for (int i = 0; i < 8; ++i) pad[i] = key[i] ^ 0x36363636u;
-    s.words(pad, 8);
-    for (int i = 0; i < 8; ++i) pad[i] = 0x36363636u;
-    s.words(pad, 8);
-    s.words(v, 8);
-    if (sep >= 0) s.byte((uint32_t)sep);
-    if (data16) s.words(data16, 16);
-    uint32_t inner[8];
-    s.final(inner);
-    s.init();
-    for (int i = 0; i < 8; ++i) pad[i] = key[i] ^ 0x5c5c5c5cu;
-    s.words(pad, 8);
-    for (int i = 0; i < 8; ++i) pad[i] = 0x5c5c5c5cu;
-    s.words(pad, 8);
-    s.words(inner, 8);
-    s.final(out);
+    uint32_t st[8], inner[8], d[16];
+    const bool has_d = data16 != nullptr;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) d[i] = has_d ? data16[i] : 0u;
+    const uint32_t sb = (uint32_t)sep & 0xffu;
+    // steps: 0 key^ipad | 1 V... | 2 the rest of D (with data only) | 3 key^opad | 4 inner hash
+#pragma unroll 1
+    for (uint32_t step = 0; step < 5u; ++step) {
+        if ((step == 2u) & !has_d) continue;
+        if (step == 3u) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) inner[i] = st[i];
+        }
+        if ((step == 0u) | (step == 3u)) sha256_init(st);
+        uint32_t blk[16];
+        if ((step == 0u) | (step == 3u)) {
+            const uint32_t pad = step == 0u ? 0x36363636u : 0x5c5c5c5cu;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { blk[i] = key[i] ^ pad; blk[8 + i] = pad; }
+        } else if (step == 1u) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) blk[i] = v[i];
+            if (has_d) {                              // V || sep || D[0..30]
+                blk[8] = (sb << 24) | (d[0] >> 8);
+#pragma unroll
+                for (int j = 1; j < 8; ++j) blk[8 + j] = (d[j - 1] << 24) | (d[j] >> 8);
+            } else {                                  // V [|| sep] + padding: the last block
+                blk[8] = sep >= 0 ? (sb << 24) | 0x00800000u : 0x80000000u;
+#pragma unroll
+                for (int k = 9; k < 15; ++k) blk[k] = 0;
+                blk[15] = (64u + 32u + (sep >= 0 ? 1u : 0u)) * 8u;
+            }
+        } else if (step == 2u) {                      // D[31..63] + padding (97 inner bytes after the key block)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) blk[k] = (d[7 + k] << 24) | (d[8 + k] >> 8);
+            blk[8] = (d[15] << 24) | 0x00800000u;
+#pragma unroll
+            for (int k = 9; k < 15; ++k) blk[k] = 0;
+            blk[15] = (64u + 97u) * 8u;
+        } else {                                      // the inner hash + padding
+#pragma unroll
+            for (int i = 0; i < 8; ++i) blk[i] = inner[i];
+            blk[8] = 0x80000000u;
+#pragma unroll
+            for (int k = 9; k < 15; ++k) blk[k] = 0;
+            blk[15] = (64u + 32u) * 8u;
+        }
+        sha256_compress(st, blk);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[i] = st[i];
 }
-// RFC 6979 HMAC-DRBG as libsecp256k1's nonce_function_rfc6979 drives it (key32 || msg32 mod n)
+// RFC 6979 HMAC-DRBG as libsecp256k1's nonce_function_rfc6979 drives it (key32 || msg32 mod n). Each phase is a
+// loop over one hmac_kv site (inlined once per phase).
 struct Rfc6979 {
     uint32_t K[8], V[8];
     bool retry;
@@ -726,27 +779,27 @@ struct Rfc6979 {
         uint32_t kd[16];
         for (int i = 0; i < 8; ++i) { kd[i] = d.v[7 - i]; kd[8 + i] = e_mod_n.v[7 - i]; }
         for (int i = 0; i < 8; ++i) { V[i] = 0x01010101u; K[i] = 0; }
-        uint32_t t[8];
-        hmac_kv(K, V, 0x00, kd, t);
-        for (int i = 0; i < 8; ++i) K[i] = t[i];
-        hmac_kv(K, V, -1, nullptr, t);
-        for (int i = 0; i < 8; ++i) V[i] = t[i];
-        hmac_kv(K, V, 0x01, kd, t);
-        for (int i = 0; i < 8; ++i) K[i] = t[i];
-        hmac_kv(K, V, -1, nullptr, t);
-        for (int i = 0; i < 8; ++i) V[i] = t[i];
+        // K = HMAC_K(V || 0x00 || kd); V = HMAC_K(V); K = HMAC_K(V || 0x01 || kd); V = HMAC_K(V)
+#pragma unroll 1
+        for (int s = 0; s < 4; ++s) {
+            uint32_t t[8];
+            const bool to_k = (s & 1) == 0;
+            hmac_kv(K, V, to_k ? s >> 1 : -1, to_k ? kd : nullptr, t);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { K[i] = to_k ? t[i] : K[i]; V[i] = to_k ? V[i] : t[i]; }
+        }
         retry = false;
     }
     SECP_FN U256 next() {
-        uint32_t t[8];
-        if (retry) {
-            hmac_kv(K, V, 0x00, nullptr, t);
-            for (int i = 0; i < 8; ++i) K[i] = t[i];
-            hmac_kv(K, V, -1, nullptr, t);
-            for (int i = 0; i < 8; ++i) V[i] = t[i];
+        // a retry first: K = HMAC_K(V || 0x00), V = HMAC_K(V); then V = HMAC_K(V)
+#pragma unroll 1
+        for (int s = retry ? 0 : 2; s < 3; ++s) {
+            uint32_t t[8];
+            const bool to_k = s == 0;
+            hmac_kv(K, V, to_k ? 0 : -1, nullptr, t);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { K[i] = to_k ? t[i] : K[i]; V[i] = to_k ? V[i] : t[i]; }
         }
-        hmac_kv(K, V, -1, nullptr, t);
-        for (int i = 0; i < 8; ++i) V[i] = t[i];
         retry = true;
         U256 k;
         for (int i = 0; i < 8; ++i) k.v[i] = V[7 - i];
@@ -756,20 +809,21 @@ struct Rfc6979 {
 
 // ------------------------------------------------------------------------------ Keccak address
 // public_to_address: Keccak-256(X || Y)[12:32] (X, Y big-endian 32 bytes each)
+SECP_FN uint32_t bswap32(uint32_t x) { return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24); }
 SECP_FN void pub_address(const Aff& q, uint8_t addr[20]) {
-    uint8_t pub[64];
-    u_to_be(q.x, pub);
-    u_to_be(q.y, pub + 32);
+    // little-endian 64-bit word i of X || Y (big-endian): bytes 8i..8i+7 = BE limbs 7-2i and 6-2i, byte-swapped
     uint64_t a[25];
+#pragma unroll
     for (int i = 0; i < 25; ++i) a[i] = 0;
-    for (int i = 0; i < 8; ++i) {
-        uint64_t w = 0;
-        for (int b = 0; b < 8; ++b) w |= (uint64_t)pub[8 * i + b] << (8 * b);
-        a[i] = w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        a[i] = (uint64_t)bswap32(q.x.v[7 - 2 * i]) | ((uint64_t)bswap32(q.x.v[6 - 2 * i]) << 32);
+        a[4 + i] = (uint64_t)bswap32(q.y.v[7 - 2 * i]) | ((uint64_t)bswap32(q.y.v[6 - 2 * i]) << 32);
     }
     a[8] ^= 0x01ull;                 // pad10*1 at byte 64, rate 136
     a[16] ^= 0x80ull << 56;
     keccak_f1600(a);
+#pragma unroll
     for (int i = 12; i < 32; ++i) addr[i - 12] = (uint8_t)(a[i >> 3] >> (8 * (i & 7)));
 }
 

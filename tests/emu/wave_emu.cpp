@@ -96,6 +96,14 @@ struct EmuWave {
     static uint32_t readlane(uint32_t v, uint32_t src) { return shfl(v, src); }
     static uint32_t bperm(uint32_t addr, uint32_t v) { return shfl(v, (addr >> 2) & 63u); }   // ds_bpermute_b32
     static uint32_t pair_swap(uint32_t v) { return shfl(v, (uint32_t)g->cur ^ 1u); }           // DPP quad [1,0,3,2]
+    // WaveHip::keccak_pair (lane pairs: the even lane holds the low halves, the odd lane the high halves of the
+    // 25 state words) as ONE collective: the scheduler joins each pair's halves and permutes the 64-bit state
+    static void keccak_pair(uint32_t X[25], uint32_t odd) {
+        int l = g->cur;
+        if ((uint32_t)(l & 1) != odd) { fprintf(stderr, "emu: keccak_pair parity of lane %d\n", l); abort(); }
+        g->op[l] = 10; g->arg[l] = (uint64_t)(uintptr_t)X; g->seq[l]++;
+        yield_to_sched();
+    }
     static uint32_t rank_below(uint64_t m) {                                                   // mbcnt
         const uint32_t l = (uint32_t)g->cur;
         return (uint32_t)__builtin_popcountll(l ? (m & ((1ull << l) - 1ull)) : 0ull);
@@ -289,6 +297,15 @@ int run_wave(const bft::Params& P, uint32_t wave, std::vector<uint8_t>& lds, int
                 else r += v;
             }
             for (int l = 0; l < nl; ++l) s.res[l] = r;
+        } else if (op == 10) {               // keccak_pair: every lane pair's 64-bit state, permuted
+            for (int l = 0; l < nl; l += 2) {
+                uint32_t* lo = (uint32_t*)(uintptr_t)s.arg[l];
+                uint32_t* hi = (uint32_t*)(uintptr_t)s.arg[l + 1];
+                uint64_t a[25];
+                for (int i = 0; i < 25; ++i) a[i] = (uint64_t)lo[i] | ((uint64_t)hi[i] << 32);
+                bft::keccak_f1600_u64(a);
+                for (int i = 0; i < 25; ++i) { lo[i] = (uint32_t)a[i]; hi[i] = (uint32_t)(a[i] >> 32); }
+            }
         } else if (op == 4) {
             for (int l = 0; l < 64; ++l) s.res[l] = (uint32_t)s.arg[(int)(s.arg[l] >> 32)];
         } else if (op == 2) {
