@@ -67,8 +67,10 @@ BFT_FN void outbox_init(Outbox& o) {
 //                                     + the group-collective slots at +256 for S > 64)
 //   need_seed only:
 //   [.., + L*32)                      per-lane commit hash
-//   [.., + 64*LANE_HASH_BUF)          per-lane header buffer of lane_block_hash (S <= 64; the
-//                                     workgroup kernels use a private buffer)
+//   [.., + (64/S)*LANE_HASH_BUF)      one header buffer per segment (S <= 64): the header a segment's deferred
+//                                     hash absorbs (resolve_deferred_hash_seg, wave_block_hash). The one-lane
+//                                     hashes of the rare paths use a private buffer: 64 per-lane buffers
+//                                     (26 KB) held the seeded kernels to one wave per SIMD by LDS
 // (The N = 64 FAST kernel has its own, smaller layout: bft_fast64.h.)
 template <uint32_t S>
 struct Layout {
@@ -92,7 +94,7 @@ struct Layout {
     static constexpr uint32_t CHASH_OFF = GRP_OFF + GRP_BYTES;
     static constexpr uint32_t SCR_OFF = CHASH_OFF + L * 32;
     static constexpr uint32_t BYTES_POW2 = CHASH_OFF;
-    static constexpr uint32_t BYTES_SEED = S > 64 ? SCR_OFF : SCR_OFF + 64 * LANE_HASH_BUF;
+    static constexpr uint32_t BYTES_SEED = S > 64 ? SCR_OFF : SCR_OFF + (64 / S) * LANE_HASH_BUF;
     static constexpr uint32_t bytes(bool need_seed) { return need_seed ? BYTES_SEED : BYTES_POW2; }
 };
 // RoundChangeSet table words per wave / workgroup for k rounds per validator (a runtime capacity:
@@ -108,7 +110,9 @@ BFT_FN uint32_t backlog_words(uint32_t seg) {      // per wave (S <= 64) or work
 }
 BFT_FN uint32_t lds_bytes(uint32_t seg, bool need_seed) {
     return seg == 256 ? Layout<256>::bytes(need_seed) : seg == 128 ? Layout<128>::bytes(need_seed)
-                                                                 : Layout<64>::bytes(need_seed);
+         : seg == 64 ? Layout<64>::bytes(need_seed) : seg == 32 ? Layout<32>::bytes(need_seed)
+         : seg == 16 ? Layout<16>::bytes(need_seed) : seg == 8 ? Layout<8>::bytes(need_seed)
+         : Layout<4>::bytes(need_seed);
 }
 
 // Kernel modes:
@@ -319,7 +323,7 @@ struct Sim {
     // Keccak-256 of the header of canonical-parent block b at height x by the whole wave; the header is
     // encoded by lane `enc` into its scratch buffer. Returns the 8 hash words in every lane.
     BFT_FN void wave_block_hash(uint32_t enc, uint32_t x, uint64_t b, uint32_t out[8]) {
-        uint64_t* wb = (uint64_t*)(lds + LDS_SCR_OFF + enc * LANE_HASH_BUF);
+        uint64_t* wb = (uint64_t*)(lds + LDS_SCR_OFF);                  // S == 64: the one segment buffer
         uint32_t nb = 0;
         if (lane == enc) {
             uint32_t prev[8];
@@ -374,8 +378,9 @@ struct Sim {
             const uint32_t x = commit_x;
             prev_hash_words(x - 1u, prev);
             const uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
-            lane_block_hash(lds + LDS_SCR_OFF + lane * LANE_HASH_BUF, prev, P.addresses + 20u * blk_prop(b),
-                            P.seed, inst, x, blk_prop(b), blk_var(b), time, o);
+            alignas(8) uint8_t pbuf[LANE_HASH_BUF];                  // private (scratch): a rare path
+            lane_block_hash(pbuf, prev, P.addresses + 20u * blk_prop(b), P.seed, inst, x, blk_prop(b), blk_var(b),
+                            time, o);
             uint32_t* hs = (uint32_t*)(lds + LDS_CHASH_OFF + lane * 32);
             for (int i = 0; i < 8; ++i) hs[i] = o[i];
             const uint32_t sd = seed_from_words(o[0], o[1], nval(), P.seed_le != 0);
@@ -399,13 +404,14 @@ struct Sim {
         const uint32_t x0 = wv.shfl(commit_x, lead);
         const uint64_t b0 = (uint64_t)wv.shfl((uint32_t)commit_blk, lead) |
                             ((uint64_t)wv.shfl((uint32_t)(commit_blk >> 32), lead) << 32);
-        const uint32_t* wb = (const uint32_t*)(lds + LDS_SCR_OFF + lead * LANE_HASH_BUF);
+        uint8_t* sbuf = lds + LDS_SCR_OFF + (lane / S) * LANE_HASH_BUF;   // this segment's header buffer
+        const uint32_t* wb = (const uint32_t*)sbuf;
         uint32_t nb = 0;
         if ((sb != 0u) & (lane == lead)) {
             uint32_t prev[8];
             prev_hash_words(x0 - 1u, prev);
             const uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b0) + 1ull);
-            nb = header_words((uint64_t*)(lds + LDS_SCR_OFF + lane * LANE_HASH_BUF), prev, P.addresses + 20u * blk_prop(b0),
+            nb = header_words((uint64_t*)sbuf, prev, P.addresses + 20u * blk_prop(b0),
                               P.seed, inst, x0, blk_prop(b0), blk_var(b0), time);
         }
         BFT_STAMP(16);                                            // (diagnostic) the lead's header encoding
@@ -447,8 +453,9 @@ struct Sim {
             const uint32_t x = commit_x;
             prev_hash_words(x - 1u, prev);
             const uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
-            lane_block_hash(lds + LDS_SCR_OFF + lane * LANE_HASH_BUF, prev, P.addresses + 20u * blk_prop(b),
-                            P.seed, inst, x, blk_prop(b), blk_var(b), time, o);
+            alignas(8) uint8_t pbuf[LANE_HASH_BUF];                  // private (scratch): a rare path
+            lane_block_hash(pbuf, prev, P.addresses + 20u * blk_prop(b), P.seed, inst, x, blk_prop(b), blk_var(b),
+                            time, o);
             uint32_t* hs = (uint32_t*)(lds + LDS_CHASH_OFF + lane * 32);
             for (int i = 0; i < 8; ++i) hs[i] = o[i];
             const uint32_t sd = seed_from_words(o[0], o[1], nval(), P.seed_le != 0);
@@ -574,13 +581,12 @@ struct Sim {
             uint32_t prev[8], out[8];
             prev_hash_words(last, prev);
             uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
-            if (S > 64) {
-                alignas(8) uint8_t pbuf[LANE_HASH_BUF];      // private (scratch): LDS is kept for the tables
+            {
+                // private (scratch): the commits of the one-message-at-a-time path and the opt-in modes; LDS holds
+                // one header buffer per segment only (Layout)
+                alignas(8) uint8_t pbuf[LANE_HASH_BUF];
                 lane_block_hash(pbuf, prev, P.addresses + 20u * blk_prop(b), P.seed, inst, x, blk_prop(b),
                                 blk_var(b), time, out);
-            } else {
-                lane_block_hash(lds + LDS_SCR_OFF + lane * LANE_HASH_BUF, prev, P.addresses + 20u * blk_prop(b),
-                                P.seed, inst, x, blk_prop(b), blk_var(b), time, out);
             }
             uint32_t* hs = (uint32_t*)(lds + LDS_CHASH_OFF + lane * 32);
             for (int i = 0; i < 8; ++i) hs[i] = out[i];
