@@ -39,16 +39,24 @@ struct WaveHip {
         else if constexpr (N < 32) return __builtin_amdgcn_alignbit(mine, other, 32 - N);
         else return __builtin_amdgcn_alignbit(other, mine, 64 - N);
     }
+    __device__ static uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {   // v_bitop3_b32 0x96
+#if defined(__HIP_DEVICE_COMPILE__)
+        return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+        return a ^ b ^ c;
+#endif
+    }
     __device__ static void keccak_pair(uint32_t X[25], uint32_t odd) {
 #pragma unroll 1
         for (int rnd = 0; rnd < 24; ++rnd) {
-            uint32_t c[5], d[5], t[25], b[25];
+            uint32_t c[5], r1[5], t[25], b[25];
+            // theta with 3-input XORs (v_bitop3_b32): two per column parity, one per word (X ^ C[x-1] ^ rot(C[x+1]))
 #pragma unroll
-            for (int x = 0; x < 5; ++x) c[x] = X[x] ^ X[x + 5] ^ X[x + 10] ^ X[x + 15] ^ X[x + 20];
+            for (int x = 0; x < 5; ++x) c[x] = xor3(xor3(X[x], X[x + 5], X[x + 10]), X[x + 15], X[x + 20]);
 #pragma unroll
-            for (int x = 0; x < 5; ++x) d[x] = c[(x + 4) % 5] ^ rotl_pair<1>(c[(x + 1) % 5], pair_swap(c[(x + 1) % 5]));
+            for (int x = 0; x < 5; ++x) r1[x] = rotl_pair<1>(c[(x + 1) % 5], pair_swap(c[(x + 1) % 5]));
 #pragma unroll
-            for (int i = 0; i < 25; ++i) t[i] = X[i] ^ d[i % 5];
+            for (int i = 0; i < 25; ++i) t[i] = xor3(X[i], c[(i % 5 + 4) % 5], r1[i % 5]);
 #define BFT_RHO_P(i, n, j) b[j] = rotl_pair<n>(t[i], (n) ? pair_swap(t[i]) : 0u);
             BFT_RHO_P(0, 0, 0) BFT_RHO_P(1, 1, 10) BFT_RHO_P(2, 62, 20) BFT_RHO_P(3, 28, 5) BFT_RHO_P(4, 27, 15)
             BFT_RHO_P(5, 36, 16) BFT_RHO_P(6, 44, 1) BFT_RHO_P(7, 6, 11) BFT_RHO_P(8, 55, 21) BFT_RHO_P(9, 20, 6)
@@ -61,7 +69,11 @@ struct WaveHip {
 #pragma unroll
                 for (int x = 0; x < 5; ++x)
                     X[5 * y + x] = b[5 * y + x] ^ (~b[5 * y + (x + 1) % 5] & b[5 * y + (x + 2) % 5]);
-            X[0] ^= odd ? KECCAK_RC_HI[rnd] : KECCAK_RC_LO[rnd];
+            // both halves' round constants as uniform (scalar) loads, then a select: a per-lane address would be
+            // a vector load waited for in every round
+            const uint32_t rlo = __builtin_amdgcn_readfirstlane(KECCAK_RC_LO[rnd]);
+            const uint32_t rhi = __builtin_amdgcn_readfirstlane(KECCAK_RC_HI[rnd]);
+            X[0] ^= odd ? rhi : rlo;
         }
     }
     // set bits of m below this lane (v_mbcnt_lo / hi)

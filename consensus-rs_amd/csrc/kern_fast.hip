@@ -81,15 +81,16 @@ __device__ inline void keccak_f1600_pair(uint32_t X[25], uint32_t odd) {
 #pragma unroll 1
 #endif
     for (int rnd = 0; rnd < 24; ++rnd) {
-        uint32_t c[5], cs[5], d[5], t[25], b[25];
+        uint32_t c[5], cs[5], r1[5], t[25], b[25];
 #pragma unroll
         for (int x = 0; x < 5; ++x) c[x] = xor3_32(xor3_32(X[x], X[x + 5], X[x + 10]), X[x + 15], X[x + 20]);
 #pragma unroll
         for (int x = 0; x < 5; ++x) cs[x] = pair_swap(c[x]);
 #pragma unroll
-        for (int x = 0; x < 5; ++x) d[x] = c[(x + 4) % 5] ^ rotl_pair<1>(c[(x + 1) % 5], cs[(x + 1) % 5]);
+        for (int x = 0; x < 5; ++x) r1[x] = rotl_pair<1>(c[(x + 1) % 5], cs[(x + 1) % 5]);
+        // theta's D folded into one 3-input XOR per word (X ^ C[x-1] ^ rot(C[x+1])): 25 v_bitop3 instead of 5 + 25 XORs
 #pragma unroll
-        for (int i = 0; i < 25; ++i) t[i] = X[i] ^ d[i % 5];
+        for (int i = 0; i < 25; ++i) t[i] = xor3_32(X[i], c[(i % 5 + 4) % 5], r1[i % 5]);
         // rho + pi: b[y + 5*((2x+3y)%5)] = rotl(t[x+5y], r[x+5y])
 #define BFT_RHO2(i, n, j) b[j] = rotl_pair<n>(t[i], (n) ? pair_swap(t[i]) : 0u);
         BFT_RHO2(0, 0, 0) BFT_RHO2(1, 1, 10) BFT_RHO2(2, 62, 20) BFT_RHO2(3, 28, 5) BFT_RHO2(4, 27, 15)
