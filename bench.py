@@ -107,8 +107,8 @@ def step_traffic(workload: str, batch: int):
         e = ks.get(k)
         if not e:
             continue
-        if "hbm_bytes_per_dispatch_attributed" in e:
-            parts[k] = e["hbm_bytes_per_dispatch_attributed"]          # per launch (attribution pass)
+        if "hbm_bytes_per_launch_attributed" in e:
+            parts[k] = e["hbm_bytes_per_launch_attributed"]            # per launch (attribution pass)
         elif "hbm_bytes_per_dispatch" in e:
             attributed = False
             parts[k] = e["hbm_bytes_per_dispatch"] / (batch if k == "bft_hash_chain_kernel" else 1)

@@ -82,6 +82,7 @@ struct Params {
     uint32_t* sfx;                    // [n_inst][sfx_rows][SFX_DWORDS]
     uint32_t sfx_x0, sfx_rows;
     uint32_t chain_prio;              // s_setprio of the block-hash chain waves (0..3)
+    uint32_t fast_lds_pad;            // A/B arms only (BFTSIM_TESTING + BFTSIM_FAST_LDS_PAD): extra LDS per FAST wave
     uint32_t rcs_k;                   // RoundChangeSet rounds per validator (bftsim_set_rcs_capacity)
     uint32_t pad5;
     // little-endian seeds, N = 64: the predicted canonical blocks (bft_seed_chain_kernel; nullptr: none)

@@ -437,6 +437,7 @@ struct bftsim {
     // (BFTSIM_TESTING + BFTSIM_CHAIN_WAVE_MAX)
     uint64_t chain_wave_max = 0;
     uint32_t chain_prio = 0;          // s_setprio of the chain waves (BFTSIM_TESTING + BFTSIM_CHAIN_PRIO)
+    uint32_t fast_lds_pad = 0;        // extra LDS per FAST wave: fewer resident FAST waves (BFTSIM_TESTING + BFTSIM_FAST_LDS_PAD)
     bool seed_spec = true;            // little-endian seeds, N = 64: predicted blocks (BFTSIM_TESTING + BFTSIM_SEED_SPEC=0: off)
     int pipeline = 0;                 // number of row-table sets (0: no pipelining)
     uint32_t sfx_rows = 0;            // heights per hash-pass chunk (0: no hash pass)
@@ -800,6 +801,8 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         if (testing && cw) h->chain_wave_max = strtoull(cw, nullptr, 10);
         const char* cp = getenv("BFTSIM_CHAIN_PRIO");
         if (testing && cp) h->chain_prio = (uint32_t)atoi(cp);
+        const char* lp = getenv("BFTSIM_FAST_LDS_PAD");
+        if (testing && lp) h->fast_lds_pad = (uint32_t)atoi(lp) > 60000u ? 60000u : (uint32_t)atoi(lp);
         auto knob = [&](const char* name, uint32_t& v, uint32_t lo, uint32_t hi) {
             const char* e = getenv(name);
             if (testing && e) { const uint32_t x = (uint32_t)atoi(e); v = x < lo ? lo : x > hi ? hi : x; }
@@ -912,6 +915,7 @@ static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
     p.rcs = h->d_rcs;
     p.rcs_k = h->rcs_k;
     p.chain_prio = h->chain_prio;
+    p.fast_lds_pad = h->fast_lds_pad;
     p.backlog = h->d_backlog;
     if (h->crypto && h->d_mlog) {
         p.mlog = h->d_mlog;

@@ -30,7 +30,7 @@ hipError_t launch_fast(dim3 grid, hipStream_t s, const Params& p) {
     // the lossless build for schedules without drops and proposer crashes (cfg3): masks are constants;
     // SEEDED (little-endian seeds): the proposer follows the block hashes, computed in-kernel
     const bool lossy = !(p.thr16 == 0 && p.crash_on == 0), seeded = p.need_seed != 0;
-    const size_t lds = lds_bytes_fast64(seeded);
+    const size_t lds = lds_bytes_fast64(seeded) + p.fast_lds_pad;   // the pad: A/B arms of FAST residency only
     if (seeded) {
         if (lossy) hipLaunchKernelGGL((bft_consensus_fast_kernel<true, true>), grid, dim3(64), lds, s, p);
         else hipLaunchKernelGGL((bft_consensus_fast_kernel<false, true>), grid, dim3(64), lds, s, p);

@@ -86,6 +86,14 @@ def main():
     write, meta2 = counters(os.path.join(root, "write"))
     sq, meta3 = counters(os.path.join(root, "sq"))
     attr = attributed_writes(os.path.join(root, "write_evict")) if os.path.isdir(os.path.join(root, "write_evict")) else {}
+    # launches per chain dispatch in the (pipelined) FETCH pass: the bench line it printed
+    batch = 1
+    try:
+        cfg = json.load(open(os.path.join(root, "fetch.json"))).get("config", {})
+        batch = max(1, int(cfg.get("hash_batch") or 1)) if cfg.get("pipelined") else 1
+    except (OSError, ValueError):
+        pass
+    res["fetch_pass_hash_batch"] = batch
     meta.update(meta2)
     meta.update(meta3)
     for k in set(st) | set(fetch) | set(write) | set(sq) | set(attr):
@@ -102,11 +110,15 @@ def main():
         if f and w:
             e["hbm_bytes_per_dispatch"] = e["fetch_bytes"] + e["write_bytes"]
         if k in attr:
-            # writes measured with an L2 eviction after every kernel (unpipelined launches): the kernel's own
-            # write-backs, none borrowed from or lent to its neighbours
+            # writes measured with an L2 eviction after every kernel of unpipelined launches (one dispatch of each
+            # kernel per launch): the kernel's own write-backs, none borrowed from or lent to kernels running
+            # beside it; with the FETCH pass's bytes per launch (a chain dispatch of that pass carries `batch`
+            # launches) this is the kernel's HBM traffic per launch
             e["write_attribution"] = attr[k]
             if f:
-                e["hbm_bytes_per_dispatch_attributed"] = e["fetch_bytes"] + attr[k]["write_bytes_attributed"]
+                per = batch if k == "bft_hash_chain_kernel" else 1
+                e["fetch_bytes_per_launch"] = e["fetch_bytes"] / per
+                e["hbm_bytes_per_launch_attributed"] = e["fetch_bytes_per_launch"] + attr[k]["write_bytes_attributed"]
         for c, v in sq.get(k, {}).items():
             e[c] = sum(v) / len(v)
         res["kernels"][k] = e
