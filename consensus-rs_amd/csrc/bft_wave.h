@@ -182,6 +182,10 @@ struct Sim {
     // (S == 64, NEED_SEED, MODE_FULL) a Core commit of the Prepare/Commit closed form whose header hash
     // is computed after the delivery by the whole wave (resolve_deferred_hash)
     bool hash_defer, in_pc;
+    // (SEG_HASH) a hash deferred past its phase (resolve_deferred_hash_seg, end_phase_hashes): the canonical tip
+    // was recorded with that stale seed and hash (canon_stale, segment-uniform), this lane's tip seed was taken
+    // from it by block gossip (seed_stale)
+    bool canon_stale, seed_stale;
     uint32_t lane_flags;
     uint32_t* rcs_base;      // this wave's RoundChangeSet table (global)
     uint32_t rcs_k;          // its capacity in rounds (Params::rcs_k)
@@ -230,6 +234,7 @@ struct Sim {
         outbox_init(nx);
         commit_x = 0; commit_round = 0; commit_seed = 0; commit_blk = 0;
         hash_defer = false; in_pc = false;
+        canon_stale = false; seed_stale = false;
         mlog_cnt = 0;
         lane_flags = 0;
         off_inst = offset_inst_part(p.seed, inst);
@@ -401,9 +406,10 @@ struct Sim {
         hash_defer = false;
         const uint64_t sb = (pb.w[0] >> seg_base) & ((1ull << (S & 63u)) - 1ull);
         const uint32_t lead = seg_base + (sb ? (uint32_t)__builtin_ctzll(sb) : 0u);
-        const uint32_t x0 = wv.shfl(commit_x, lead);
+        // the pending commit is commit_blk (its height blk_h: resolve_commits has cleared commit_x by now)
         const uint64_t b0 = (uint64_t)wv.shfl((uint32_t)commit_blk, lead) |
                             ((uint64_t)wv.shfl((uint32_t)(commit_blk >> 32), lead) << 32);
+        const uint32_t x0 = blk_h(b0);
         uint8_t* sbuf = lds + LDS_SCR_OFF + (lane / S) * LANE_HASH_BUF;   // this segment's header buffer
         const uint32_t* wb = (const uint32_t*)sbuf;
         uint32_t nb = 0;
@@ -439,7 +445,7 @@ struct Sim {
             out[2 * i + 1] = odd ? h4[i] : o;
         }
         sync();                                                   // header buffers read before any rewrite
-        const bool same = pend & (commit_x == x0) & (commit_blk == b0);
+        const bool same = pend & (commit_blk == b0);
         if (same) {
             uint32_t* hs = (uint32_t*)(lds + LDS_CHASH_OFF + lane * 32);
             for (int i = 0; i < 8; ++i) hs[i] = out[i];
@@ -450,7 +456,7 @@ struct Sim {
         if (pend & !same) {
             uint32_t prev[8], o[8];
             const uint64_t b = commit_blk;
-            const uint32_t x = commit_x;
+            const uint32_t x = blk_h(b);
             prev_hash_words(x - 1u, prev);
             const uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b) + 1ull);
             alignas(8) uint8_t pbuf[LANE_HASH_BUF];                  // private (scratch): a rare path
@@ -462,7 +468,43 @@ struct Sim {
             commit_seed = sd;
             last_seed = sd;
         }
+        // The canonical tip recorded this tick by resolve_commits before its hash was known (a hash deferred
+        // past its phase): its seed word and hash row are written now by the lowest pending lane that holds
+        // that block, and its seed becomes the segment's canonical tip seed and the tip seed of every lane
+        // that took the tip by block gossip in the meantime (refresh_tip_from_table).
+        const bool holds = pend & (commit_blk == canon_tip) & (canon_tick == (uint32_t)tick);
+        const uint64_t hb = (ballot(holds).w[0] >> seg_base) & ((1ull << (S & 63u)) - 1ull);
+        const uint32_t hl = seg_base + (hb ? (uint32_t)__builtin_ctzll(hb) : 0u);
+        const uint32_t csd = wv.shfl(commit_seed, hl);
+        if (hb != 0u) {
+            if (lane == hl) {
+                rec_row(canon_h)[3] = commit_seed;
+                const uint32_t* hs = (const uint32_t*)(lds + LDS_CHASH_OFF + lane * 32);
+                uint32_t* dst = (uint32_t*)hash_row(canon_h);
+                wv.gstore4(dst, hs[0], hs[1], hs[2], hs[3]);
+                wv.gstore4(dst + 4, hs[4], hs[5], hs[6], hs[7]);
+            }
+            canon_tip_seed = csd;
+            if (seed_stale) last_seed = csd;
+        }
+        canon_stale = false;
+        seed_stale = false;
         sync();
+    }
+    // (SEG_HASH) at the top of every phase: the closed-form commits of the phases before keep their hashes
+    // pending while nothing in the tick can read them, so that the commits of one height spread over several
+    // phases of a tick share one segment hash. They are resolved when the tick's phases end (`fin`); when a
+    // pending block was minted before this tick, since its successor can be minted within the tick (miner_mine:
+    // T = max(tick, last_T + 1)), while a block of this tick cannot (T > tick); and before a phase that carries a
+    // Round Change, which can start a round at the committed height and read its tip seed (start_new_round).
+    // One call site of resolve_deferred_hash_seg (it is inlined).
+    BFT_FN void phase_hashes(bool fin) {
+        const bool pend = hash_defer;
+        if (ballot(pend).none()) return;
+        const bool now = fin | (pend & (blk_T(commit_blk) < (uint32_t)tick)) | ((nx.f & F_RC) != 0u);
+        if (ballot(now).any()) { resolve_deferred_hash_seg(); return; }
+        const bool holds = pend & (commit_blk == canon_tip) & (canon_tick == (uint32_t)tick);
+        canon_stale = ((ballot(holds).w[0] >> seg_base) & ((1ull << (S & 63u)) - 1ull)) != 0u;
     }
 
     BFT_FN uint32_t canon_seed(uint32_t x) {
@@ -549,11 +591,13 @@ struct Sim {
         if (last == canon_h && canon_h != 0) {            // the common case: tip = canonical tip
             last_T = (int32_t)blk_T(canon_tip);
             last_seed = canon_tip_seed;
+            if constexpr (SEG_HASH) seed_stale = canon_stale;
             return;
         }
         check_window(last);
         last_T = (int32_t)wv.gload(rec_row(last) + 2);
         last_seed = wv.gload(rec_row(last) + 3);
+        if constexpr (SEG_HASH) seed_stale = false;
     }
 
     // Chain::insert_block for a Core commit (core/chain.rs:45-71 via backend.rs:163-200)
@@ -596,6 +640,7 @@ struct Sim {
         last = x;
         last_T = (int32_t)blk_T(b);
         last_seed = sd;
+        if constexpr (SEG_HASH) seed_stale = false;         // a deferred hash: resolve_deferred_hash_seg sets it
         out_blocks(x, x);                                   // ChainEvent::NewBlock (chain.rs:61)
         if (x > miner_queue) miner_queue = x;               // ChainEvent::NewHeader (chain.rs:62)
     }
@@ -1713,6 +1758,7 @@ struct Sim {
             for (uint32_t p = pstart;; ++p) {
                 bool pend_l = act & !frozen & pending_local();
                 M bal = ballot(pend_l);
+                if constexpr (SEG_HASH) phase_hashes(bal.none() || p >= P.phase_cap);
                 if (bal.none()) break;
                 bool seg_pending = (bal & seg_mask).any();
                 if (EXT && P.mlog) crypto_log(act && !frozen, p);   // real-crypto mode (SPEC.md §11)
@@ -1763,7 +1809,6 @@ struct Sim {
                 if (pub) sync();                              // records read before the next publish
                 BFT_STAMP(3);
                 if constexpr (WAVE_HASH) resolve_deferred_hash();
-                if constexpr (SEG_HASH) resolve_deferred_hash_seg();
                 const uint32_t xc = resolve_commits();
                 BFT_STAMP(4);
                 if (frozen) act = false;
