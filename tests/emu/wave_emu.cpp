@@ -465,6 +465,17 @@ extern "C" int emu_run(const bftsim_config* cfg, uint64_t first, uint64_t n, bft
         if (run_wave(P, w, lds, seg > 64 ? (int)seg : 64)) return -1;
     }
     P.resume_mode = 0;
+    // invariant of the in-kernel hashes (segments of S < 64 lanes, whose canonical rows a deferred hash patches
+    // after they are recorded): every recorded row's seed word is the seed of its hash row
+    if (P.need_seed && seg < 64) {
+        for (uint64_t i = 0; i < n; ++i)
+            for (uint32_t x = 1; x <= ch[i] && x < hcap; ++x) {
+                uint32_t w[2];
+                memcpy(w, &hs[(i * hcap + x) * 32], 8);
+                if (rec[(i * hcap + x) * 4 + 3] != bft::seed_from_words(w[0], w[1], cfg->n, cfg->seed_byte_order == BFTSIM_SEED_LE))
+                    return -7;
+            }
+    }
     if (fast && getenv("BFT_EMU_FAST_REPORT")) {
         uint64_t nb = 0;
         for (uint64_t i = 0; i < n; ++i) nb += resume[i];
