@@ -94,7 +94,10 @@ struct Layout {
     static constexpr uint32_t CHASH_OFF = GRP_OFF + GRP_BYTES;
     static constexpr uint32_t SCR_OFF = CHASH_OFF + L * 32;
     static constexpr uint32_t BYTES_POW2 = CHASH_OFF;
-    static constexpr uint32_t BYTES_SEED = S > 64 ? SCR_OFF : SCR_OFF + (64 / S) * LANE_HASH_BUF;
+    // (S < 64, seeded) per segment the hash of its last canonical block whose hash a deferred hash patched:
+    // {height, 8 words}, the next header's prev_hash without global loads (resolve_deferred_hash_seg)
+    static constexpr uint32_t TIPC_OFF = SCR_OFF + (64 / S) * LANE_HASH_BUF, TIPC_BYTES = 48;
+    static constexpr uint32_t BYTES_SEED = S > 64 ? SCR_OFF : TIPC_OFF + (64 / S) * TIPC_BYTES;
     static constexpr uint32_t bytes(bool need_seed) { return need_seed ? BYTES_SEED : BYTES_POW2; }
 };
 // RoundChangeSet table words per wave / workgroup for k rounds per validator (a runtime capacity:
@@ -413,9 +416,15 @@ struct Sim {
         uint8_t* sbuf = lds + LDS_SCR_OFF + (lane / S) * LANE_HASH_BUF;   // this segment's header buffer
         const uint32_t* wb = (const uint32_t*)sbuf;
         uint32_t nb = 0;
+        uint32_t* tipc = (uint32_t*)(lds + LY::TIPC_OFF + (lane / S) * LY::TIPC_BYTES);
         if ((sb != 0u) & (lane == lead)) {
             uint32_t prev[8];
-            prev_hash_words(x0 - 1u, prev);
+            if (tipc[0] == x0 - 1u) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) prev[i] = tipc[1 + i];
+            } else {
+                prev_hash_words(x0 - 1u, prev);
+            }
             const uint64_t time = P.genesis_time + (uint64_t)P.block_period * ((uint64_t)blk_T(b0) + 1ull);
             nb = header_words((uint64_t*)sbuf, prev, P.addresses + 20u * blk_prop(b0),
                               P.seed, inst, x0, blk_prop(b0), blk_var(b0), time);
@@ -483,6 +492,9 @@ struct Sim {
                 uint32_t* dst = (uint32_t*)hash_row(canon_h);
                 wv.gstore4(dst, hs[0], hs[1], hs[2], hs[3]);
                 wv.gstore4(dst + 4, hs[4], hs[5], hs[6], hs[7]);
+                tipc[0] = canon_h;                        // the next height's prev_hash
+#pragma unroll
+                for (int i = 0; i < 8; ++i) tipc[1 + i] = hs[i];
             }
             canon_tip_seed = csd;
             if (seed_stale) last_seed = csd;
@@ -1744,6 +1756,7 @@ struct Sim {
         }
         if (!resuming && P.byz_count > 0) init_byzantine();
         for (uint32_t b = lane; b < HIST_BINS; b += LY::L) *hist_slot(b) = 0;
+        if constexpr (SEG_HASH) if (me == 0) *(uint32_t*)(lds + LY::TIPC_OFF + (lane / S) * LY::TIPC_BYTES) = ~0u;
         sync();
         for (tick = tick0; tick < (int32_t)P.max_ticks; ++tick) {
             if (ballot(!seg_done).none()) break;
