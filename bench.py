@@ -309,7 +309,7 @@ def main():
                     help="launches in flight (bftsim_set_pipeline: a ring of row-table sets, each launch on its set's "
                          "stream). Default: 6 at >= 12,288 instances per GPU, 16 below (profiles/r04/ab_deep_ring)")
     ap.add_argument("--hash-batch", type=int, default=None,
-                    help="launches whose block-hash chains run as one kernel (bftsim_set_hash_batch, 1..16). Default: 2 "
+                    help="launches whose block-hash chains run as one kernel (bftsim_set_hash_batch, 1..32). Default: 2 "
                          "at >= 12,288 instances per GPU, 8 below (profiles/r04/ab_deep_ring)")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (HIP's default is 4): every set's stream needs its own "
@@ -407,6 +407,8 @@ def main():
     sim.prepare(I)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
+    enqueue_s = []
+
     def timed_steps(first_id):
         """K launches between two barriers + device synchronisations; the max over ranks (s)"""
         if world > 1:
@@ -415,6 +417,7 @@ def main():
         t0 = time.perf_counter()
         for _ in range(args.steps):
             sim.launch(first_id, stream)
+        enqueue_s.append(time.perf_counter() - t0)   # host time of the K launch calls (diagnostic)
         sim.sync()                        # enqueues the last partial hash batch and waits for every stream
         torch.cuda.synchronize(dev)
         if world > 1:
@@ -533,6 +536,7 @@ def main():
                 "heights": args.heights, "parallelism": f"instance-sharded x{world}",
                 "pipelined": pipelined, "pipeline_depth": args.pipeline_depth if pipelined else 0,
                 "hash_batch": args.hash_batch if pipelined else 0,
+                "host_enqueue_ms": round(1e3 * enqueue_s[0], 3),
                 "instance_rounds_per_step": views_all,
                 "stats_allreduce": reduce_via,
                 "committed_heights_per_step": heights_all,

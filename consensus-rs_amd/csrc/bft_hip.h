@@ -256,14 +256,30 @@ hipError_t launch_hash_suffix(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* 
 // `wave`: one wave per instance (bft_hash_chain_wave_kernel, small shards) instead of a lane pair
 hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, bool wave, hipStream_t s, Params p);
 // the chains of up to CHAIN_MAX_SETS launches (row-table sets) of n instances each, heights 1..H, as one kernel
-constexpr uint32_t CHAIN_MAX_SETS = 16;
+constexpr uint32_t CHAIN_MAX_SETS = 32;
 struct ChainSets {
     uint32_t count;
     const uint32_t* sfx[CHAIN_MAX_SETS];
     const uint32_t* ch[CHAIN_MAX_SETS];
     uint8_t* hash[CHAIN_MAX_SETS];
+    // predicted chains (big-endian seeds, N = 64): each launch's instance ids, its Byzantine masks,
+    // first height whose recorded block differs from the prediction, recorded rows
+    uint32_t first[CHAIN_MAX_SETS];
+    uint64_t* byz[CHAIN_MAX_SETS];
+    uint32_t* bad[CHAIN_MAX_SETS];
+    const uint32_t* rec[CHAIN_MAX_SETS];
+    uint32_t* pred[CHAIN_MAX_SETS];       // [n][H] SPEC_VALID | proposer | variant << 16 of each height, or 0
 };
+// chain kernel modes (Params::chain_mode)
+constexpr uint32_t CHAIN_RECORDED = 0;    // heights [x0, min(ch, x0 + rows - 1)] from the recorded rows' suffixes
+constexpr uint32_t CHAIN_PREDICTED = 1;   // heights 1..H of the predicted blocks, up to the first without one
+constexpr uint32_t CHAIN_REPAIR = 2;      // heights [bad, ch]: from the first recorded block that differs
 hipError_t launch_hash_chain_batch(uint32_t n, const ChainSets& cs, bool wave, hipStream_t s, Params p);
+// predicted chains: per launch of the batch, the Byzantine masks + the predicted suffix rows (one launch, on
+// the stream its chains will run on, ahead of its consensus kernel's completion); per batch, the check of the
+// recorded blocks against the predictions (rewriting the suffix rows that differ)
+hipError_t launch_spec_suffix(uint32_t n, const ChainSets& cs, hipStream_t s, const Params& p);
+hipError_t launch_spec_verify(uint32_t n, const ChainSets& cs, hipStream_t s, const Params& p);
 // little-endian seeds, N = 64: the predicted canonical blocks into p.spec / p.hash (kern_fast.hip)
 hipError_t launch_seed_chain(uint32_t n, hipStream_t s, const Params& p);
 hipError_t launch_resume(dim3 grid, size_t lds, hipStream_t s, const Params& p);  // kern_resume.hip

@@ -345,6 +345,17 @@ using bft::host_genesis_hash;
 // borrow each other's write-backs (a resume kernel with no hand-overs charged 30.8 MB). After
 // every kernel of a launch this kernel reads 64 MiB (twice the eight XCDs' L2), evicting what the kernel left
 // dirty; scripts/pmc_summary.py adds its WRITE_SIZE to the kernel before it.
+// a launch's zeroed state in one dispatch (instead of one memset each): the record rows (16 B each), the
+// histogram, the FAST kernel's hand-over flags and queue head (null when not a FAST launch)
+__global__ __launch_bounds__(256) void bft_clear_kernel(uint4* rec, uint64_t n_rec, uint64_t* hist, uint32_t* resume,
+                                                        uint32_t n_resume, uint32_t* resume_q) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x, stride = (uint64_t)gridDim.x * 256u;
+    for (uint64_t i = t; i < n_rec; i += stride) rec[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (resume)
+        for (uint64_t i = t; i < n_resume; i += stride) resume[i] = 0u;
+    if (t < bft::HIST_BINS) hist[t] = 0ull;
+    if (resume_q && t < 2u) resume_q[t] = 0u;
+}
 __global__ __launch_bounds__(256) void bft_l2_evict_kernel(const uint4* buf, uint64_t n16, uint32_t* sink) {
     uint32_t acc = 0;
     for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256ull) {
@@ -417,12 +428,16 @@ struct bftsim {
     //     whatever their number, so batching B launches per kernel gives B times the chain throughput
     //     (profiles/r04). Results are complete once bftsim_sync (or any fetch) returns; those flush a
     //     partial batch first.
-    static constexpr uint32_t MAX_SETS = 32, MAX_CS = 8, MAX_HS = 4, MAX_BATCH = bft::CHAIN_MAX_SETS;
+    static constexpr uint32_t MAX_SETS = 32, MAX_CS = 8, MAX_HS = 8, MAX_BATCH = bft::CHAIN_MAX_SETS;
     struct RowSet {
         uint32_t* ch = nullptr; uint32_t* flags = nullptr; uint32_t* ticks = nullptr; uint64_t* views = nullptr;
         uint32_t* rec = nullptr; uint8_t* hash = nullptr;
         uint32_t* sfx = nullptr;      // header suffix rows of the hash pass (sfx_rows per instance)
         uint32_t* spec = nullptr;     // little-endian seeds, N = 64: predicted blocks [H + 1][n] (seed chain)
+        // big-endian seeds, N = 64: predicted chains: Byzantine masks [n], first height whose
+        // recorded block differs from its prediction [n]
+        uint64_t* byz = nullptr; uint32_t* bad = nullptr;
+        uint32_t* pred = nullptr;     // [n][H] the predicted block of each height (bft_spec_suffix_kernel)
         // a launch's own scratch (set 0: the handle's buffers)
         uint64_t* hist = nullptr; uint32_t* rcs = nullptr; uint32_t* backlog = nullptr;
         uint32_t* resume = nullptr; uint32_t* save = nullptr; uint32_t* resume_q = nullptr;
@@ -449,9 +464,17 @@ struct bftsim {
     // and there is no hash pass, so more launches run side by side (profiles/r04/ab_le_streams)
     uint32_t n_cs_seeded = 4;
     uint32_t hash_batch = 4;          // launches per chain kernel (BFTSIM_TESTING + BFTSIM_HASH_BATCH overrides)
-    struct Pending { uint32_t set, ev; } pend[MAX_BATCH];
+    // big-endian seeds, N = 64, pipelined: the chains of a batch run on predicted blocks from launch time on
+    // (BFTSIM_TESTING + BFTSIM_HASH_SPEC=0: off), over up to n_hs_spec hash streams so that the
+    // batches of a burst of launches run side by side
+    // on for launches of fewer than hash_spec_max instances: a small shard is bound by the latency of its chains,
+    // a large one by the chip's issue, which the checks only add to (profiles/r06/ab_spec)
+    uint64_t hash_spec_max = 12288;
+    uint32_t n_hs_spec = 3;
+    struct Pending { uint32_t set, ev, first; } pend[MAX_BATCH];
     uint32_t n_pend = 0;
     bft::Params batch_p{};            // the launch parameters of the pending batch (sizes, genesis, prio)
+    bool batch_spec = false;          // the pending batch runs predicted chains
     // per-launch kernel timing: a ring of event quadruples, read by bftsim_kernel_ms_sum
     static constexpr uint32_t RING = 64;
     struct LaunchEv { hipEvent_t c0, c1, h0, h1, sx; bool has_hash, pending; } ring[RING] = {};
@@ -510,12 +533,13 @@ static void free_bufs(bftsim* h) {
         bftsim::RowSet& r = h->sets[k];
         (void)hipFree(r.ch); (void)hipFree(r.flags); (void)hipFree(r.ticks); (void)hipFree(r.views);
         (void)hipFree(r.rec); (void)hipFree(r.hash); (void)hipFree(r.sfx); (void)hipFree(r.spec);
+        (void)hipFree(r.byz); (void)hipFree(r.bad); (void)hipFree(r.pred);
         if (k > 0) {                                   // set 0's scratch is the handle's own
             (void)hipFree(r.hist); (void)hipFree(r.rcs); (void)hipFree(r.backlog); (void)hipFree(r.resume);
             (void)hipFree(r.save); (void)hipFree(r.resume_q);
         }
         r.ch = r.flags = r.ticks = nullptr; r.views = nullptr; r.rec = nullptr; r.hash = nullptr; r.sfx = nullptr;
-        r.spec = nullptr;
+        r.spec = nullptr; r.byz = nullptr; r.bad = nullptr; r.pred = nullptr;
         r.hist = nullptr; r.rcs = r.backlog = r.resume = r.save = r.resume_q = nullptr;
     }
 
@@ -649,15 +673,19 @@ SigApi& sig_api() {
 extern "C" {
 
 #ifdef BFT_STAMPS
-// diagnostic builds only: per-section cycle sums of the last launch, summed over waves
-int bftsim_debug_stamps(uint64_t out[bft::NSTAMP]) {
+// diagnostic builds only: per-section cycle sums of the last launch, summed over waves, into out[0 .. cap);
+// returns the number of sections the build stamps (bft::NSTAMP), so a caller sizes its buffer from the library
+// (out = nullptr, cap = 0: the count alone) instead of a copy of the constant
+int bftsim_debug_stamps(uint64_t* out, uint32_t cap) {
+    if (!out || cap == 0) return bft::NSTAMP;
     std::vector<uint64_t> v(g_stamp_waves * bft::NSTAMP);
     if (hipDeviceSynchronize() != hipSuccess) return -2;
     if (hipMemcpy(v.data(), g_stamps, v.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return -2;
-    for (int k = 0; k < bft::NSTAMP; ++k) out[k] = 0;
+    const uint32_t m = cap < (uint32_t)bft::NSTAMP ? cap : (uint32_t)bft::NSTAMP;
+    for (uint32_t k = 0; k < m; ++k) out[k] = 0;
     for (uint64_t w = 0; w < g_stamp_waves; ++w)
-        for (int k = 0; k < bft::NSTAMP; ++k) out[k] += v[w * bft::NSTAMP + k];
-    return 0;
+        for (uint32_t k = 0; k < m; ++k) out[k] += v[w * bft::NSTAMP + k];
+    return bft::NSTAMP;
 }
 #endif
 
@@ -811,8 +839,11 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         knob("BFTSIM_LAUNCH_STREAMS_SEEDED", h->n_cs_seeded, 1, bftsim::MAX_CS);
         knob("BFTSIM_HASH_STREAMS", h->n_hs, 1, bftsim::MAX_HS);   // A/B arms
         knob("BFTSIM_HASH_BATCH", h->hash_batch, 1, bftsim::MAX_BATCH);   // A/B arms (bftsim_set_hash_batch)
+        knob("BFTSIM_HASH_STREAMS_SPEC", h->n_hs_spec, 1, bftsim::MAX_HS);
         const char* ss = getenv("BFTSIM_SEED_SPEC");
         if (testing && ss) h->seed_spec = atoi(ss) != 0;
+        const char* hs = getenv("BFTSIM_HASH_SPEC");   // 0: off, 1: at every size
+        if (testing && hs) h->hash_spec_max = atoi(hs) != 0 ? ~0ull : 0ull;
         const char* pe = getenv("BFTSIM_PMC_EVICT");
         h->pmc_evict = testing && pe && atoi(pe) != 0;   // scripts/gpu_profile.sh's attribution pass
     }
@@ -852,6 +883,21 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         if (rows * n >= (1ull << 32)) rows = ((1ull << 32) - 1) / n;
         h->sfx_rows = (uint32_t)rows;
         for (uint32_t k = 0; k < h->n_sets; ++k) HIPCHECK(h, hipMalloc(&h->sets[k].sfx, rows * per_row));
+        if (h->seg == 64 && h->cfg.n == 64 && h->n_sets >= 2 && rows >= h->cfg.heights)
+            for (uint32_t k = 0; k < h->n_sets; ++k) {   // predicted chains of pipelined FAST launches
+                HIPCHECK(h, hipMalloc(&h->sets[k].byz, n * 8));
+                HIPCHECK(h, hipMalloc(&h->sets[k].bad, n * 4));
+                HIPCHECK(h, hipMalloc(&h->sets[k].pred, n * h->cfg.heights * 4ull));
+            }
+        // every stream of the pipelined mode now, while the HIP runtime still has hardware queues of its own to
+        // give each (streams created later in a busy process can share one, which serializes their batches)
+        if (h->n_sets >= 2) {
+            for (uint32_t k = 0; k < h->n_cs && k < bftsim::MAX_CS; ++k)
+                if (!h->cs[k]) HIPCHECK(h, hipStreamCreateWithFlags(&h->cs[k], hipStreamNonBlocking));
+            const uint32_t nh = h->n_hs > h->n_hs_spec ? h->n_hs : h->n_hs_spec;
+            for (uint32_t k = 0; k < nh && k < bftsim::MAX_HS; ++k)
+                if (!h->hstr[k]) HIPCHECK(h, hipStreamCreateWithFlags(&h->hstr[k], hipStreamNonBlocking));
+        }
     } else if (h->seg == 64 && h->cfg.n == 64 && !h->window) {
         // little-endian seeds at N = 64: the seed chain's predicted blocks
         for (uint32_t k = 0; k < h->n_sets; ++k)
@@ -935,6 +981,11 @@ static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
     return p;
 }
 
+static uint32_t clear_blocks(uint64_t n_rec) {   // bft_clear_kernel's grid: grid-stride, at least one block
+    const uint64_t b = (n_rec + 255u) / 256u;
+    return (uint32_t)(b < 1 ? 1 : b > 4096 ? 4096 : b);
+}
+
 int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     if (!h || h->cap_inst == 0 || h->n_req == 0) return fail(h, BFTSIM_EINVAL, "bftsim_prepare not called");
     const uint64_t n = h->n_req;
@@ -956,6 +1007,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     // the opt-in modes
     const bool fast = h->fast && p.fast && !p.mlog && h->d_save && !h->window && !h->h_trace && h->seg == 64 &&
                       h->cfg.n == 64;
+    const bool fast_launch = fast;
     const bool spec = fast && p.need_seed && h->seed_spec && h->sets[0].spec;
     const bool pipe = h->pipeline >= 2 && (!p.need_seed || spec) && h->n_sets >= 2 && !h->h_trace && !p.mlog;
     if (h->last_pipe && !pipe) {
@@ -1012,8 +1064,11 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         ev.pending = false;
     }
     h->ring_head += 1;
-    HIPCHECK(h, hipMemsetAsync(h->d_rec, 0, n * h->hcap * 16, s));
-    HIPCHECK(h, hipMemsetAsync(h->d_hist, 0, bft::HIST_BINS * sizeof(uint64_t), s));
+    // the record rows, the histogram and (FAST launches) the hand-over flags and queue, zeroed by one dispatch
+    hipLaunchKernelGGL(bft_clear_kernel, dim3(clear_blocks(n * h->hcap)), dim3(256), 0, s, (uint4*)h->d_rec,
+                       (uint64_t)n * h->hcap, h->d_hist, fast_launch ? h->d_resume : nullptr, (uint32_t)n,
+                       fast_launch ? h->d_resume_q : nullptr);
+    HIPCHECK(h, hipGetLastError());
     if (h->d_backlog) HIPCHECK(h, hipMemsetAsync(h->d_backlog, 0, h->backlog_bytes, s));
     uint32_t per_block = h->seg > 64 ? 1u : 64u / h->seg;      // instances per workgroup
     uint32_t grid = (uint32_t)((n + per_block - 1) / per_block);
@@ -1026,13 +1081,16 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         p.resume_q = h->d_resume_q;
         p.save = h->d_save;
         p.save_stride = n * 64;
-        HIPCHECK(h, hipMemsetAsync(h->d_resume, 0, n * 4, s));
-        HIPCHECK(h, hipMemsetAsync(h->d_resume_q, 0, 8, s));
         {
             bftsim::RowSet& r = h->sets[pipe ? h->cur_set : 0];
             if (!r.hint) {
                 HIPCHECK(h, hipHostMalloc((void**)&r.hint, 4, hipHostMallocMapped | hipHostMallocCoherent));
-                *r.hint = 0xffffffffu;                    // unknown: the full grid
+                *r.hint = 0xffffffffu;                    // unknown: the full grid, or another set's last count
+                for (uint32_t k = 0; k < h->n_sets; ++k)  // (the grid only paces the persistent waves)
+                    if (h->sets[k].hint && &h->sets[k] != &r && *h->sets[k].hint != 0xffffffffu) {
+                        *r.hint = __atomic_load_n(h->sets[k].hint, __ATOMIC_RELAXED);
+                        break;
+                    }
             }
             p.resume_hint = r.hint;
         }
@@ -1062,17 +1120,24 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         // than the chains, so a thread per instance over its heights runs on the hash stream beside them.
         const bool on_launch = fast;
         if (pipe && K >= H && on_launch) {
-            // suffix rows now; the chains in the next batch (flush_batch)
-            HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, 1, K, sfx, false, s, p));
-            HIPCHECK(h, pmc_evict(h, s));
-            HIPCHECK(h, hipEventRecord(ev.sx, s));
+            bftsim::RowSet& r = h->sets[h->cur_set];
+            const bool hspec = r.byz && n < h->hash_spec_max;   // big-endian seeds: predicted chains
+            if (!hspec) {
+                // suffix rows now; the chains in the next batch (flush_batch)
+                HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, 1, K, sfx, false, s, p));
+                HIPCHECK(h, pmc_evict(h, s));
+                HIPCHECK(h, hipEventRecord(ev.sx, s));
+            }
             ev.has_hash = false;                          // the batch's last launch carries the chain time
             // one chain kernel runs every pending launch with the batch's sizes (suffix-row stride, grid):
             // a launch of another size starts a batch of its own
-            if (h->n_pend > 0 && h->batch_p.n_instances != p.n_instances)
+            if (h->n_pend > 0 && (h->batch_p.n_instances != p.n_instances || h->batch_spec != hspec))
                 if (int rc = flush_batch(h)) return rc;
-            if (h->n_pend == 0) h->batch_p = p;
-            h->pend[h->n_pend++] = {h->cur_set, (h->ring_head - 1) % bftsim::RING};
+            if (h->n_pend == 0) {
+                h->batch_p = p;
+                h->batch_spec = hspec;
+            }
+            h->pend[h->n_pend++] = {h->cur_set, (h->ring_head - 1) % bftsim::RING, (uint32_t)first};
             if (h->n_pend >= h->hash_batch) if (int rc = flush_batch(h)) return rc;
         } else {
             // one launch's hash pass: on a hash stream (pipelined) or the launch stream; chunks of K heights
@@ -1112,20 +1177,44 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
 // the chains of the pending launches as one kernel on the next hash stream, after each launch's suffix rows
 static int flush_batch(bftsim* h) {
     if (h->n_pend == 0) return BFTSIM_OK;
-    h->cur_hs = (h->cur_hs + 1) % h->n_hs;
+    h->cur_hs = (h->cur_hs + 1) % (h->batch_spec ? h->n_hs_spec : h->n_hs);
     if (!h->hstr[h->cur_hs]) HIPCHECK(h, hipStreamCreateWithFlags(&h->hstr[h->cur_hs], hipStreamNonBlocking));
     hipStream_t t = h->hstr[h->cur_hs];
     bft::ChainSets cs{};
     cs.count = h->n_pend;
     for (uint32_t i = 0; i < h->n_pend; ++i) {
-        HIPCHECK(h, hipStreamWaitEvent(t, h->ring[h->pend[i].ev].sx, 0));
         const bftsim::RowSet& r = h->sets[h->pend[i].set];
+        if (!h->batch_spec) {
+            HIPCHECK(h, hipStreamWaitEvent(t, h->ring[h->pend[i].ev].sx, 0));   // the launch's suffix rows
+        } else {                                       // the set is free: the caller's work before the launch,
+            HIPCHECK(h, hipStreamWaitEvent(t, r.entry, 0));   // the set's previous hash pass
+            if (r.busy) HIPCHECK(h, hipStreamWaitEvent(t, r.done, 0));
+        }
         cs.sfx[i] = r.sfx; cs.ch[i] = r.ch; cs.hash[i] = r.hash;
+        cs.rec[i] = r.rec; cs.byz[i] = r.byz; cs.bad[i] = r.bad; cs.pred[i] = r.pred; cs.first[i] = h->pend[i].first;
     }
     bftsim::LaunchEv& last = h->ring[h->pend[h->n_pend - 1].ev];
-    const bft::Params& p = h->batch_p;
+    bft::Params p = h->batch_p;
     HIPCHECK(h, hipEventRecord(last.h0, t));
-    HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, p.n_instances <= h->chain_wave_max, t, p));
+    if (h->batch_spec) {
+        // the predicted blocks' suffix rows and chains, which need nothing of the consensus kernels (one suffix
+        // pass for the whole batch: per launch on a stream of their own they fell behind the launches); once
+        // every launch's consensus kernel is done, the check of its recorded blocks against the predictions, and
+        // the chains again from the first height that differs
+        HIPCHECK(h, bft::launch_spec_suffix(p.n_instances, cs, t, p));
+        HIPCHECK(h, pmc_evict(h, t));
+        p.chain_mode = bft::CHAIN_PREDICTED;
+        HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, false, t, p));
+        HIPCHECK(h, pmc_evict(h, t));
+        for (uint32_t i = 0; i < h->n_pend; ++i) HIPCHECK(h, hipStreamWaitEvent(t, h->ring[h->pend[i].ev].c1, 0));
+        HIPCHECK(h, bft::launch_spec_verify(p.n_instances, cs, t, p));
+        HIPCHECK(h, pmc_evict(h, t));
+        p.chain_mode = bft::CHAIN_REPAIR;
+        HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, false, t, p));
+    } else {
+        p.chain_mode = bft::CHAIN_RECORDED;
+        HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, p.n_instances <= h->chain_wave_max, t, p));
+    }
     HIPCHECK(h, pmc_evict(h, t));
     HIPCHECK(h, hipEventRecord(last.h1, t));
     last.has_hash = true;
@@ -1140,7 +1229,7 @@ static int flush_batch(bftsim* h) {
 
 int bftsim_set_hash_batch(bftsim_t* h, uint32_t launches) {
     if (!h) return BFTSIM_EINVAL;
-    if (launches < 1 || launches > bftsim::MAX_BATCH) return fail(h, BFTSIM_EINVAL, "hash batch must be 1..16 launches");
+    if (launches < 1 || launches > bftsim::MAX_BATCH) return fail(h, BFTSIM_EINVAL, "hash batch must be 1..32 launches");
     if (int rc = flush_batch(h)) return rc;
     h->hash_batch = launches;
     return BFTSIM_OK;

@@ -236,14 +236,25 @@ __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params
     const uint32_t il = blk * 32u + pair;
     if (il >= p.n_instances) return;                  // both lanes of a pair leave together
     const uint32_t K = p.sfx_rows, x0 = p.sfx_x0;
-    const uint32_t ch = p.committed_height[il];
-    const uint32_t x1 = ch < x0 + K - 1u ? ch : x0 + K - 1u;
-    if (x1 < x0) return;
+    // CHAIN_RECORDED: heights x0 .. min(ch, x0 + K - 1); CHAIN_PREDICTED: every height of the chunk, until the
+    // first one without a prediction (suffix length 0); CHAIN_REPAIR: from the first recorded block that differs
+    // from its prediction (bft_spec_verify_kernel) up to ch
+    uint32_t x1 = x0 + K - 1u, xs = x0;
+    if (p.chain_mode != CHAIN_PREDICTED) {
+        const uint32_t ch = p.committed_height[il];
+        x1 = ch < x1 ? ch : x1;
+        if (p.chain_mode == CHAIN_REPAIR) {
+            const uint32_t b = cs.bad[blockIdx.x / ((p.n_instances + 31u) / 32u)][il];
+            xs = b > x0 ? b : x0;
+        }
+    }
+    if (x1 < xs) return;
     uint32_t* sb = sbuf + pair * CHAIN_SB;
     for (uint32_t i = odd; i < SFX_PAD; i += 2u) sb[i] = 0;
     for (uint32_t i = SFX_PAD + SFX_BODY_DW + odd; i < CHAIN_SB; i += 2u) sb[i] = 0;
-    // the parent of x0: genesis, or the previous chunk's last hash (same stream, already written)
-    const uint8_t* ph = x0 == 1u ? p.genesis_hash : p.hash + ((uint64_t)il * p.rows + x0 - 1u) * 32;
+    // the parent of xs: genesis, or the hash of xs - 1 (the previous chunk's last, or a verified prediction;
+    // written before this kernel on the same stream)
+    const uint8_t* ph = xs == 1u ? p.genesis_hash : p.hash + ((uint64_t)il * p.rows + xs - 1u) * 32;
     uint32_t prev[8];
     for (int i = 0; i < 8; ++i)
         prev[i] = (uint32_t)ph[4 * i] | ((uint32_t)ph[4 * i + 1] << 8) | ((uint32_t)ph[4 * i + 2] << 16) |
@@ -254,15 +265,19 @@ __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params
     const uint64_t rstride = (uint64_t)SFX_DEV_DW * n;   // suffix rows: [height][dword][instance]
     const uint32_t* srow = p.sfx + il + (uint64_t)odd * HALF * n;
     uint32_t s[HALF], slen;
+    {
+        const uint64_t ro = (uint64_t)(xs - x0) * rstride;
 #pragma unroll
-    for (uint32_t i = 0; i < HALF; ++i) s[i] = srow[(uint64_t)i * n];
-    slen = p.sfx[il + (uint64_t)SFX_DEV_LEN_DW * n];
+        for (uint32_t i = 0; i < HALF; ++i) s[i] = srow[ro + (uint64_t)i * n];
+        slen = p.sfx[il + ro + (uint64_t)SFX_DEV_LEN_DW * n];
+    }
     uint64_t* pb = pbuf + (BFT_CHAIN_COMPACT ? pair : threadIdx.x) * (PFX_WORDS + 4);   // both lanes write the same words
     const uint32_t* pw = (const uint32_t*)pb + odd;
-    for (uint32_t x = x0; x <= x1; ++x) {
+    for (uint32_t x = xs; x <= x1; ++x) {
+        const uint32_t len_s = slen;
+        if (len_s == 0u) break;                       // no prediction for x (CHAIN_PREDICTED only; both lanes)
 #pragma unroll
         for (uint32_t i = 0; i < HALF; ++i) sb[SFX_PAD + odd * HALF + i] = s[i];
-        const uint32_t len_s = slen;
         if (x < x1) {                                 // prefetch height x + 1
             const uint64_t ro = (uint64_t)(x + 1u - x0) * rstride;
 #pragma unroll
@@ -275,6 +290,76 @@ __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params
         __syncthreads();                              // splice buffer read before the next height's write
     }
 #endif
+}
+
+// Predicted chains (big-endian seeds, N = 64). With big-endian seeds the round-0 proposer of an
+// N = 64 instance is validator 0 at every height (validator.rs:33-48: the seed is 0 mod 64), so the block the
+// canonical tick commits at height x (spec_block64: proposer 0, the variant the SPLIT draw of view (x, 0) lets
+// commit, time tick x - 1) depends on no hash. Its suffix row is encoded and the prev_hash chains run before the
+// consensus kernel has recorded anything, i.e. from launch time instead of behind the consensus kernel.
+// bft_spec_verify_kernel then compares every recorded block with its prediction, rewrites the suffix rows of
+// those that differ and notes the first such height; the chains are re-run from there (CHAIN_REPAIR). A
+// predicted hash is kept only where its block and all of its ancestors were predicted right, so every hash is
+// the recorded block's by construction.
+__global__ __launch_bounds__(256) void bft_spec_byz_kernel(Params p, ChainSets cs) {
+    __shared__ uint8_t perm[256 * 64];                // byz_mask64's permutation, per thread
+    const uint32_t n = p.n_instances, bpl = (n + 255u) / 256u, k = blockIdx.x / bpl;
+    const uint32_t il = (blockIdx.x % bpl) * 256u + threadIdx.x;
+    if (il >= n) return;
+    cs.byz[k][il] = byz_mask64(p.seed, cs.first[k] + il, p.byz_count, perm + 64u * threadIdx.x);
+    cs.bad[k][il] = 0xffffffffu;
+}
+__device__ inline uint64_t spec_time(const Params& p, uint32_t tick) {
+    return p.genesis_time + (uint64_t)p.block_period * ((uint64_t)tick + 1ull);
+}
+// thread per (launch, height, instance), consecutive threads = consecutive instances (the row layout)
+__global__ __launch_bounds__(256) void bft_spec_suffix_kernel(Params p, ChainSets cs) {
+    const uint32_t n = p.n_instances, H = p.heights;
+    const uint32_t bpl = (uint32_t)(((uint64_t)n * H + 255u) / 256u), k = blockIdx.x / bpl;
+    const uint32_t t = (blockIdx.x % bpl) * 256u + threadIdx.x;   // n * H < 2^32 (bftsim.hip)
+    const uint32_t j = t / n, il = t - j * n;
+    if (j >= H) return;
+    const uint32_t x = j + 1u, inst = cs.first[k] + il;
+    uint32_t* row = const_cast<uint32_t*>(cs.sfx[k]) + (uint64_t)j * SFX_DEV_DW * n + il;
+    uint32_t prop, var;
+    if (!spec_block64(p.seed, inst, x, cs.byz[k][il], 0u, prop, var)) {
+        row[(uint64_t)SFX_DEV_LEN_DW * n] = 0u;       // no prediction: the predicted chain stops here
+        cs.pred[k][(uint64_t)il * H + j] = 0u;
+        return;
+    }
+    cs.pred[k][(uint64_t)il * H + j] = SPEC_VALID | prop | (var << 16);
+    header_suffix_strided(row, n, p.addresses + 20u * prop, p.seed, inst, x, prop, var, spec_time(p, x - 1u));
+}
+// thread per (launch, instance, height), consecutive threads = consecutive heights (coalesced record rows)
+__global__ __launch_bounds__(256) void bft_spec_verify_kernel(Params p, ChainSets cs) {
+    const uint32_t n = p.n_instances, H = p.heights;
+    const uint32_t bpl = (uint32_t)(((uint64_t)n * H + 255u) / 256u), k = blockIdx.x / bpl;
+    const uint32_t t = (blockIdx.x % bpl) * 256u + threadIdx.x;
+    const uint32_t il = t / H, x = t - il * H + 1u;
+    if (il >= n) return;
+    if (x > cs.ch[k][il]) return;
+    const uint4 row = *(const uint4*)(cs.rec[k] + ((uint64_t)il * p.rows + x) * 4);
+    const uint32_t pw = cs.pred[k][(uint64_t)il * H + x - 1u], inst = cs.first[k] + il;
+    if (((pw & SPEC_VALID) != 0u) & ((row.y & 0x1ffffu) == (pw & 0x1ffffu)) & (row.z + 1u == x)) return;
+    // the recorded block differs: its own suffix row (as bft_hash_suffix_kernel writes it), and the repair
+    // starts at the first such height
+    const uint32_t rp = row.y & 0xffffu, rv = (row.y >> 16) & 1u;
+    header_suffix_strided(const_cast<uint32_t*>(cs.sfx[k]) + (uint64_t)(x - 1u) * SFX_DEV_DW * n + il, n,
+                          p.addresses + 20u * rp, p.seed, inst, x, rp, rv, spec_time(p, row.z));
+    atomicMin(&cs.bad[k][il], x);
+}
+hipError_t launch_spec_suffix(uint32_t n, const ChainSets& cs, hipStream_t s, const Params& p) {
+    if (cs.count < 1 || cs.count > CHAIN_MAX_SETS || p.n_instances != n) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bft_spec_byz_kernel, dim3(cs.count * ((n + 255u) / 256u)), dim3(256), 0, s, p, cs);
+    const uint32_t bpl = (uint32_t)(((uint64_t)n * p.heights + 255u) / 256u);
+    hipLaunchKernelGGL(bft_spec_suffix_kernel, dim3(cs.count * bpl), dim3(256), 0, s, p, cs);
+    return hipGetLastError();
+}
+hipError_t launch_spec_verify(uint32_t n, const ChainSets& cs, hipStream_t s, const Params& p) {
+    if (cs.count < 1 || cs.count > CHAIN_MAX_SETS || p.n_instances != n) return hipErrorInvalidValue;
+    const uint32_t bpl = (uint32_t)(((uint64_t)n * p.heights + 255u) / 256u);
+    hipLaunchKernelGGL(bft_spec_verify_kernel, dim3(cs.count * bpl), dim3(256), 0, s, p, cs);
+    return hipGetLastError();
 }
 
 // Little-endian seeds, N = 64: the canonical blocks predicted ahead of the consensus kernel by a

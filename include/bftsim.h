@@ -159,12 +159,14 @@ int bftsim_kernel_ms_sum(bftsim_t *h, double *consensus_ms, double *hash_ms, uin
  * there are, so batching multiplies their throughput). Results of a launch are complete once bftsim_sync
  * returns (it also enqueues a partial hash batch); bftsim_fetch/_stats_get/_fetch_summary read the last
  * launch (and sync as they need). The HIP runtime needs a hardware queue per stream in use (the caller's,
- * two launch and two hash streams): GPU_MAX_HW_QUEUES >= 5 in the environment before HIP initialises (HIP's
+ * two launch and two to four hash streams): GPU_MAX_HW_QUEUES >= 5 in the environment before HIP initialises (HIP's
  * default is 4; bench.py sets 8). Takes effect at the next bftsim_prepare (buffers are re-allocated). */
 int bftsim_set_pipeline(bftsim_t *h, int on);
-/* pipelined launches: the number of consecutive launches whose block-hash chains run as one kernel (1..16,
+/* pipelined launches: the number of consecutive launches whose block-hash chains run as one kernel (1..32,
  * default 4). A launch waiting for its batch is hashed when the batch fills, at bftsim_sync, or when the ring
- * needs its row-table set again. */
+ * needs its row-table set again. With big-endian seeds at N = 64 the chains of a batch run on the predicted
+ * canonical blocks from the batch's first launch on, and are checked against the recorded blocks (and re-run
+ * from the first one that differs) once the batch's consensus kernels are done. */
 int bftsim_set_hash_batch(bftsim_t *h, uint32_t launches);
 /* verification switch: 0 runs N = 64 through the full kernel alone instead of the FAST kernel +
  * resume (results are identical; the default 1 is the fast path) */

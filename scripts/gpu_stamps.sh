@@ -12,8 +12,11 @@ sim.prepare(16384)
 for _ in range(2):
     sim.launch(0)
     sim.sync()
-out = (ctypes.c_uint64 * 16)()
-runtime.lib().bftsim_debug_stamps(out)
+L = runtime.lib()
+L.bftsim_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+ns = L.bftsim_debug_stamps(None, 0)           # the build's section count (bft::NSTAMP)
+out = (ctypes.c_uint64 * ns)()
+assert L.bftsim_debug_stamps(out, ns) == ns
 names = ["t_step", "classify", "event_step", "deliver_pp", "deliver_pc", "deliver_blk", "resolve", "loop/other", "#phases", "#pp", "#pc", "#blk"]
 cnt = (8, 9, 10, 11)
 tot = sum(out[k] for k in range(12) if k not in cnt)

@@ -26,8 +26,11 @@ for name in want:
         sim.set_window(window)
     sim.prepare(2048)
     sim.launch(0); sim.sync()
-    out = (ctypes.c_uint64 * 18)()
-    runtime.lib().bftsim_debug_stamps(out)
+    L = runtime.lib()
+    L.bftsim_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    ns = L.bftsim_debug_stamps(None, 0)           # the build's section count (bft::NSTAMP)
+    out = (ctypes.c_uint64 * ns)()
+    assert L.bftsim_debug_stamps(out, ns) == ns
     cnt = (6, 11, 14, 15)
     tot = sum(out[k] for k in range(18) if k not in cnt)
     views = int(sim.stats()["views"])

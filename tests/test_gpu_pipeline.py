@@ -125,12 +125,13 @@ def test_timed_mode_full_size():
 
 def test_strong_shard_timed_mode():
     """The 8-GPU strong-scaling shard of BASELINE configs[2] (rank 7's 2,048 of 16,384 instances) with the
-    settings bench.py picks for it (depth 16 x batch 8), 25 launches; every instance against the oracle."""
+    settings bench.py picks for it (depth 32 x batch 8, predicted chains), 25 launches; every instance against the
+    oracle."""
     from bftsim.distributed import strong_shard
     cfg = cfg3()
     first, n = strong_shard(7, 8, 16_384)
     got, st, (depth, batch) = _timed_run(cfg, first, n)
-    assert (n, depth, batch) == (2048, 16, 8)
+    assert (n, depth, batch) == (2048, 32, 8)
     ref = O.run(cfg, first, n, threads=16)
     assert_same(ref, got, f"cfg3 shard {first}+{n} depth {depth} batch {batch} x25")
     assert st["views"] == int(ref["views"].sum()) == n * 100
@@ -215,8 +216,43 @@ def test_small_shard_both_chain_kernels(chain, monkeypatch):
     assert st["views"] == int(ref["views"].sum()) == n * 100
 
 
+@pytest.mark.parametrize("name,mk,depth,batch", [
+    ("cfg3-30", lambda: cfg3(heights=30), 6, 2),
+    ("n64-drop", lambda: BftConfig(n=64, heights=30, seed=17, byz_count=21, drop_ppm=50_000, name="n64-drop"), 8, 4),
+    ("n64-crash", lambda: BftConfig(n=64, heights=30, seed=18, proposer_crash_ppm=300_000, name="n64-crash"), 4, 3),
+    ("n64-silent0", lambda: BftConfig(n=64, heights=25, seed=19, byz_count=10, silent=[0, 5], name="n64-silent0"),
+     5, 2),
+    ("n64-fork", lambda: BftConfig(n=64, heights=30, seed=20, byz_count=30, drop_ppm=20_000, name="n64-fork"), 3, 5)])
+def test_predicted_chains_match_oracle(name, mk, depth, batch, monkeypatch):
+    """Big-endian seeds at N = 64, pipelined: the chains of a batch run on the predicted canonical
+    blocks from launch time on; the recorded blocks are checked against the predictions and the chains re-run from
+    the first one that differs. Lossless cfg3 (every prediction right), drops and forks (the repair from a height
+    inside the chain), proposer crashes and a silent validator 0 (wrong from height 1: the whole chain repaired).
+    12 launches of the same instances, with predictions on and off, against the oracle."""
+    monkeypatch.setenv("BFTSIM_TESTING", "1")
+    cfg = mk()
+    n = 96
+    outs = []
+    for spec in ("1", "0"):
+        monkeypatch.setenv("BFTSIM_HASH_SPEC", spec)
+        sim = _sim(cfg)
+        try:
+            sim.set_pipeline(True, depth)
+            sim.set_hash_batch(batch)
+            sim.prepare(n)
+            for k in range(12):
+                sim.launch(7 * n)
+            sim.sync()
+            outs.append(sim.fetch())
+        finally:
+            sim.close()
+    ref = O.run(cfg, 7 * n, n)
+    assert_same(ref, outs[0], name + " predicted chains")
+    assert_same(ref, outs[1], name + " recorded chains")
+
+
 @pytest.mark.parametrize("name,mk,depth", [
-    ("cfg3-le", lambda: __import__("dataclasses").replace(cfg3(heights=40), seed_byte_order=1, name="cfg3-le"), 6),
+    ("cfg3-le",lambda: __import__("dataclasses").replace(cfg3(heights=40), seed_byte_order=1, name="cfg3-le"), 6),
     ("n64-le-drop", lambda: BftConfig(n=64, heights=20, seed=15, byz_count=21, drop_ppm=50_000, seed_byte_order=1,
                                       name="n64-le-drop"), 16)])
 def test_little_endian_pipelined_predictions(name, mk, depth, monkeypatch):
