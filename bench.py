@@ -165,21 +165,27 @@ def usable_cpus() -> int:
 def native_oracle():
     """SURVEY §8d builds the CPU comparator -O3 -march=native for the host it runs on; the shipped
     oracle/_build/liboracle.so comes from the build container (-O3 -mpopcnt, another CPU). Builds
-    `make -C oracle native` into a private temporary directory here and points the oracle loader at it.
-    Returns the build flags used (the shipped library's if the build fails)."""
-    import tempfile
+    `make -C oracle native` once into oracle/_build_native (git- and gpurun-ignored; rebuilt when the host CPU
+    differs from the one recorded beside it) and points the oracle loader at it, unless a library is loaded
+    already. Returns the build flags of the library the oracle actually runs."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as O
-    d = tempfile.mkdtemp(prefix="bftsim_oracle_native_")
+    d = os.path.join(ROOT, "oracle", "_build_native")
+    lib, stamp = os.path.join(d, "liboracle.so"), os.path.join(d, "host_cpu.txt")
+    cpu = host_cpu()
     try:
-        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native", f"NATIVE={d}"], check=True,
-                       stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=120)
+        built_for = open(stamp).read() if os.path.exists(lib) and os.path.exists(stamp) else None
+        if built_for != cpu:
+            subprocess.run(["make", "-s", "-B", "-C", os.path.join(ROOT, "oracle"), "native", f"NATIVE={d}"], check=True,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=120)
+            open(stamp, "w").write(cpu)
         if O._lib is None:
-            O.LIB_PATH = os.path.join(d, "liboracle.so")
-            return "-O3 -march=native (built on this host)"
+            O.LIB_PATH = lib
     except (OSError, subprocess.SubprocessError):
         pass
-    return "-O3 -mpopcnt (shipped build)"
+    O.lib()                                   # loads LIB_PATH now: the flags below are those of the running library
+    return "-O3 -march=native (built on this host)" if os.path.abspath(O.LIB_PATH) == os.path.abspath(lib) \
+        else "-O3 -mpopcnt (shipped build)"
 
 
 def cpu_baseline(cfg, sample: int, threads: int, name: str = "cfg3"):

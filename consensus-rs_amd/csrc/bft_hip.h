@@ -253,8 +253,10 @@ hipError_t launch_fast(dim3 grid, hipStream_t s, const Params& p);              
 // (loop: a thread per instance over its heights instead of a thread per (instance, height))
 hipError_t launch_hash_suffix(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, bool loop, hipStream_t s,
                               Params p);
-// `wave`: one wave per instance (bft_hash_chain_wave_kernel, small shards) instead of a lane pair
-hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, bool wave, hipStream_t s, Params p);
+// chain kernels: lane pairs (small shards), one wave per instance (kw50, A/B arm), one lane per instance (large)
+constexpr uint32_t CHAIN_KERNEL_PAIR = 0, CHAIN_KERNEL_WAVE = 1, CHAIN_KERNEL_LANE = 2;
+hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, uint32_t kind, hipStream_t s,
+                             Params p);
 // the chains of up to CHAIN_MAX_SETS launches (row-table sets) of n instances each, heights 1..H, as one kernel
 constexpr uint32_t CHAIN_MAX_SETS = 32;
 struct ChainSets {
@@ -274,7 +276,7 @@ struct ChainSets {
 constexpr uint32_t CHAIN_RECORDED = 0;    // heights [x0, min(ch, x0 + rows - 1)] from the recorded rows' suffixes
 constexpr uint32_t CHAIN_PREDICTED = 1;   // heights 1..H of the predicted blocks, up to the first without one
 constexpr uint32_t CHAIN_REPAIR = 2;      // heights [bad, ch]: from the first recorded block that differs
-hipError_t launch_hash_chain_batch(uint32_t n, const ChainSets& cs, bool wave, hipStream_t s, Params p);
+hipError_t launch_hash_chain_batch(uint32_t n, const ChainSets& cs, uint32_t kind, hipStream_t s, Params p);
 // predicted chains: per launch of the batch, the Byzantine masks + the predicted suffix rows (one launch, on
 // the stream its chains will run on, ahead of its consensus kernel's completion); per batch, the check of the
 // recorded blocks against the predictions (rewriting the suffix rows that differ)

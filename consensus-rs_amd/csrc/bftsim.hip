@@ -451,6 +451,9 @@ struct bftsim {
     // shard size (ds_bpermute latency and LDS issue at low occupancy), kept as an A/B arm
     // (BFTSIM_TESTING + BFTSIM_CHAIN_WAVE_MAX)
     uint64_t chain_wave_max = 0;
+    // one lane per instance from this many instances per launch (kern_fast.hip bft_hash_chain_lane_kernel: fewer
+    // instructions per header, longer chains; BFTSIM_TESTING + BFTSIM_CHAIN_LANE_MIN overrides)
+    uint64_t chain_lane_min = 12288;
     uint32_t chain_prio = 0;          // s_setprio of the chain waves (BFTSIM_TESTING + BFTSIM_CHAIN_PRIO)
     uint32_t fast_lds_pad = 0;        // extra LDS per FAST wave: fewer resident FAST waves (BFTSIM_TESTING + BFTSIM_FAST_LDS_PAD)
     bool seed_spec = true;            // little-endian seeds, N = 64: predicted blocks (BFTSIM_TESTING + BFTSIM_SEED_SPEC=0: off)
@@ -497,11 +500,7 @@ static int fail(bftsim* h, int code, const std::string& msg) {
 static constexpr uint64_t EVICT_BYTES = 64ull << 20;
 static hipError_t pmc_evict(bftsim* h, hipStream_t s) {
     if (!h->pmc_evict) return hipSuccess;
-    if (!h->d_evict) {
-        hipError_t e = hipMalloc(&h->d_evict, EVICT_BYTES + 16);
-        if (e == hipSuccess) e = hipMemset(h->d_evict, 0, EVICT_BYTES + 16);
-        if (e != hipSuccess) return e;
-    }
+    if (!h->d_evict) return hipErrorNotInitialized;   // allocated and zeroed by bftsim_prepare
     hipLaunchKernelGGL(bft_l2_evict_kernel, dim3(2048), dim3(256), 0, s, (const uint4*)h->d_evict, EVICT_BYTES / 16,
                        (uint32_t*)(h->d_evict + EVICT_BYTES / 16));
     return hipGetLastError();
@@ -827,6 +826,8 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         const bool testing = tst && strcmp(tst, "1") == 0;
         const char* cw = getenv("BFTSIM_CHAIN_WAVE_MAX");
         if (testing && cw) h->chain_wave_max = strtoull(cw, nullptr, 10);
+        const char* cl = getenv("BFTSIM_CHAIN_LANE_MIN");
+        if (testing && cl) h->chain_lane_min = strtoull(cl, nullptr, 10);
         const char* cp = getenv("BFTSIM_CHAIN_PRIO");
         if (testing && cp) h->chain_prio = (uint32_t)atoi(cp);
         const char* lp = getenv("BFTSIM_FAST_LDS_PAD");
@@ -846,6 +847,10 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         if (testing && hs) h->hash_spec_max = atoi(hs) != 0 ? ~0ull : 0ull;
         const char* pe = getenv("BFTSIM_PMC_EVICT");
         h->pmc_evict = testing && pe && atoi(pe) != 0;   // scripts/gpu_profile.sh's attribution pass
+        if (h->pmc_evict && !h->d_evict) {          // before any launch, so every eviction is the same dispatch
+            HIPCHECK(h, hipMalloc(&h->d_evict, EVICT_BYTES + 16));
+            HIPCHECK(h, hipMemset(h->d_evict, 0, EVICT_BYTES + 16));
+        }
     }
     const uint64_t per_block = h->seg > 64 ? 1 : 64 / h->seg, blocks = (n + per_block - 1) / per_block;
     for (uint32_t k = 1; k < (uint32_t)h->pipeline; ++k) {
@@ -981,6 +986,13 @@ static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
     return p;
 }
 
+// which chain kernel hashes a batch of launches of n instances (the wave kernel has no predicted / repair mode)
+static uint32_t chain_kind(const bftsim* h, uint64_t n, bool spec) {
+    if (n >= h->chain_lane_min) return bft::CHAIN_KERNEL_LANE;
+    if (!spec && n <= h->chain_wave_max) return bft::CHAIN_KERNEL_WAVE;
+    return bft::CHAIN_KERNEL_PAIR;
+}
+
 static uint32_t clear_blocks(uint64_t n_rec) {   // bft_clear_kernel's grid: grid-stride, at least one block
     const uint64_t b = (n_rec + 255u) / 256u;
     return (uint32_t)(b < 1 ? 1 : b > 4096 ? 4096 : b);
@@ -1113,7 +1125,6 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     if (!p.need_seed) {
         uint32_t* sfx = h->sets[pipe ? h->cur_set : 0].sfx;
         const uint32_t H = h->cfg.heights, K = h->sfx_rows;
-        const bool wave = n <= h->chain_wave_max;
         // Where the suffix rows go depends on how long the consensus kernel runs against the chains
         // (A/B, profiles/r03/ab_sfx): the N = 64 FAST kernel is short, so a full-chip pass by a thread per
         // (instance, height) runs on the launch stream right behind it; the general kernels run far longer
@@ -1153,7 +1164,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
             for (uint32_t x0 = 1; x0 <= H; x0 += K) {
                 HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, x0, K, sfx, !on_launch, t, p));
                 HIPCHECK(h, pmc_evict(h, t));
-                HIPCHECK(h, bft::launch_hash_chain((uint32_t)n, x0, K, sfx, wave, t, p));
+                HIPCHECK(h, bft::launch_hash_chain((uint32_t)n, x0, K, sfx, chain_kind(h, n, false), t, p));
                 HIPCHECK(h, pmc_evict(h, t));
             }
             HIPCHECK(h, hipEventRecord(ev.h1, t));
@@ -1204,16 +1215,16 @@ static int flush_batch(bftsim* h) {
         HIPCHECK(h, bft::launch_spec_suffix(p.n_instances, cs, t, p));
         HIPCHECK(h, pmc_evict(h, t));
         p.chain_mode = bft::CHAIN_PREDICTED;
-        HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, false, t, p));
+        HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, chain_kind(h, p.n_instances, true), t, p));
         HIPCHECK(h, pmc_evict(h, t));
         for (uint32_t i = 0; i < h->n_pend; ++i) HIPCHECK(h, hipStreamWaitEvent(t, h->ring[h->pend[i].ev].c1, 0));
         HIPCHECK(h, bft::launch_spec_verify(p.n_instances, cs, t, p));
         HIPCHECK(h, pmc_evict(h, t));
         p.chain_mode = bft::CHAIN_REPAIR;
-        HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, false, t, p));
+        HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, chain_kind(h, p.n_instances, true), t, p));
     } else {
         p.chain_mode = bft::CHAIN_RECORDED;
-        HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, p.n_instances <= h->chain_wave_max, t, p));
+        HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, chain_kind(h, p.n_instances, false), t, p));
     }
     HIPCHECK(h, pmc_evict(h, t));
     HIPCHECK(h, hipEventRecord(last.h1, t));

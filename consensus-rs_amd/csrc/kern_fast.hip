@@ -292,6 +292,135 @@ __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params
 #endif
 }
 
+// Keccak-f[1600] with the whole state in one lane as 32-bit halves (L low, H high): theta's D folded into one
+// 3-input XOR per half-word (v_bitop3_b32), rotations as two v_alignbit_b32, chi one v_bitop3_b32 per half-word:
+// ~180 VALU per round (+~80 v_mov: rho-pi permutes the 25 words with period 24, so a round loop moves them back to
+// their registers every round). Unrolling 2, 4 or all 24 rounds measured the same (24: 203 VGPRs instead of 118;
+// profiles/r06/ab_lane), so the loop is kept (code size); one call site in the kernel.
+#if defined(__HIP_DEVICE_COMPILE__)
+#ifndef BFT_LANE_UNROLL
+#define BFT_LANE_UNROLL 1
+#endif
+__device__ inline void keccak_f1600_lane(uint32_t L[25], uint32_t H[25]) {
+#pragma unroll BFT_LANE_UNROLL
+    for (int rnd = 0; rnd < 24; ++rnd) {
+        uint32_t cl[5], ch[5], rl[5], rh[5], bl[25], bh[25];
+#pragma unroll
+        for (int x = 0; x < 5; ++x) {
+            cl[x] = xor3_32(xor3_32(L[x], L[x + 5], L[x + 10]), L[x + 15], L[x + 20]);
+            ch[x] = xor3_32(xor3_32(H[x], H[x + 5], H[x + 10]), H[x + 15], H[x + 20]);
+        }
+#pragma unroll
+        for (int x = 0; x < 5; ++x) rotl_halves<1>(cl[(x + 1) % 5], ch[(x + 1) % 5], rl[x], rh[x]);
+#define BFT_RHO_L(i, n, j) rotl_halves<n>(xor3_32(L[i], cl[((i) % 5 + 4) % 5], rl[(i) % 5]), \
+                                          xor3_32(H[i], ch[((i) % 5 + 4) % 5], rh[(i) % 5]), bl[j], bh[j]);
+        BFT_RHO_L(0, 0, 0) BFT_RHO_L(1, 1, 10) BFT_RHO_L(2, 62, 20) BFT_RHO_L(3, 28, 5) BFT_RHO_L(4, 27, 15)
+        BFT_RHO_L(5, 36, 16) BFT_RHO_L(6, 44, 1) BFT_RHO_L(7, 6, 11) BFT_RHO_L(8, 55, 21) BFT_RHO_L(9, 20, 6)
+        BFT_RHO_L(10, 3, 7) BFT_RHO_L(11, 10, 17) BFT_RHO_L(12, 43, 2) BFT_RHO_L(13, 25, 12) BFT_RHO_L(14, 39, 22)
+        BFT_RHO_L(15, 41, 23) BFT_RHO_L(16, 45, 8) BFT_RHO_L(17, 15, 18) BFT_RHO_L(18, 21, 3) BFT_RHO_L(19, 8, 13)
+        BFT_RHO_L(20, 18, 14) BFT_RHO_L(21, 2, 24) BFT_RHO_L(22, 61, 9) BFT_RHO_L(23, 56, 19) BFT_RHO_L(24, 14, 4)
+#undef BFT_RHO_L
+#pragma unroll
+        for (int y = 0; y < 5; ++y)
+#pragma unroll
+            for (int x = 0; x < 5; ++x) {
+                L[5 * y + x] = bl[5 * y + x] ^ (~bl[5 * y + (x + 1) % 5] & bl[5 * y + (x + 2) % 5]);
+                H[5 * y + x] = bh[5 * y + x] ^ (~bh[5 * y + (x + 1) % 5] & bh[5 * y + (x + 2) % 5]);
+            }
+        L[0] ^= KECCAK_RC_LO[rnd];
+        H[0] ^= KECCAK_RC_HI[rnd];
+    }
+}
+#endif
+
+// Large shards (>= 12,288 instances per launch, bftsim.hip chain_lane_min): a LANE per instance. The whole state in
+// one lane: ~180 VALU per round instead of 2 x 118 for a lane pair, i.e. ~24 % fewer instructions per header for
+// ~1.5x the chain latency, which a large shard's throughput-bound pipeline hides (cfg3 at 16,384: 1.70e9 with lane
+// pairs, 1.82e9-1.85e9 with lanes in batches of 12; profiles/r06/ab_lane).
+// The splice reads the suffix row straight from global memory (rows are dword-major across instances, so a load
+// instruction touches one row per distinct prefix length in the wave) instead of an LDS splice buffer per lane.
+__global__ __launch_bounds__(64) void bft_hash_chain_lane_kernel(Params p, ChainSets cs) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    set_prio(p.chain_prio);
+    const uint32_t bps = (p.n_instances + 63u) / 64u, k = blockIdx.x / bps;
+    __shared__ __attribute__((aligned(16))) uint64_t pbuf[64 * (PFX_WORDS + 4)];   // prefix words per lane
+    __shared__ PfxSel ptbl[16];
+    if (threadIdx.x < 16) ptbl[threadIdx.x] = PFX_TBL[threadIdx.x];
+    __syncthreads();
+    const uint32_t n = p.n_instances, il = (blockIdx.x % bps) * 64u + threadIdx.x;
+    if (il >= n) return;
+    const uint32_t K = p.sfx_rows, x0 = p.sfx_x0;
+    uint32_t x1 = x0 + K - 1u, xs = x0;
+    if (p.chain_mode != CHAIN_PREDICTED) {
+        const uint32_t ch = cs.ch[k][il];
+        x1 = ch < x1 ? ch : x1;
+        if (p.chain_mode == CHAIN_REPAIR) {
+            const uint32_t b = cs.bad[k][il];
+            xs = b > x0 ? b : x0;
+        }
+    }
+    if (x1 < xs) return;
+    uint8_t* const hash = cs.hash[k];
+    const uint32_t* ph = (const uint32_t*)(xs == 1u ? p.genesis_hash : hash + ((uint64_t)il * p.rows + xs - 1u) * 32);
+    uint32_t prev[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) prev[i] = ph[i];
+    // suffix rows: byte offsets from the set's base (uniform, so the loads take saddr + a 32-bit voffset; a set's
+    // rows are < 2 GiB, bftsim.hip); dword j of the row of height x at 4 (il + ((x - x0) SFX_DEV_DW + j) n)
+    const char* const sbase = (const char*)cs.sfx[k];
+    const uint32_t n4 = 4u * n;                      // < 2^24 (launch_hash_chain_batch): 24-bit multiplies
+    const uint64_t* pb = pbuf + threadIdx.x * (PFX_WORDS + 4);
+    for (uint32_t x = xs; x <= x1; ++x) {
+        const uint32_t rowoff = 4u * il + (x - x0) * SFX_DEV_DW * n4;
+        const uint32_t len_s = *(const uint32_t*)(sbase + rowoff + SFX_DEV_LEN_DW * n4);
+        if (len_s == 0u) break;                      // no prediction for x (CHAIN_PREDICTED only)
+        const uint32_t len_p = header_prefix_perm(pbuf + threadIdx.x * (PFX_WORDS + 4), prev, ptbl);
+        uint32_t pw[2 * PFX_WORDS];
+#pragma unroll
+        for (uint32_t i = 0; i < PFX_WORDS; ++i) { const uint64_t v = pb[i]; pw[2 * i] = (uint32_t)v; pw[2 * i + 1] = (uint32_t)(v >> 32); }
+        const uint32_t c = 72u - len_p, r = c & 3u, nb = splice_blocks(len_p, len_s);
+        const int j0 = (int)(c >> 2) - (int)SFX_PAD;   // body dword of splice dword q0: -17 .. -9
+        // splice-buffer dword j0 + i: the body dword, zero outside [0, SFX_BODY_DW) (the pad and the tail)
+        auto S = [&](int j) -> uint32_t {
+            const uint32_t jj = (uint32_t)(j < 0 ? 0 : j > (int)SFX_BODY_DW - 1 ? (int)SFX_BODY_DW - 1 : j);
+            const uint32_t v = *(const uint32_t*)(sbase + rowoff + __umul24(jj, n4));
+            return (j >= 0) & (j < (int)SFX_BODY_DW) ? v : 0u;
+        };
+        uint32_t L[25], H[25];
+#pragma unroll
+        for (int i = 0; i < 25; ++i) L[i] = H[i] = 0u;
+        for (uint32_t blk = 0; blk < nb; ++blk) {     // one permutation site (code size)
+            uint32_t d[35];
+            if (blk == 0u) {                         // the prefix lies here; dwords from 17 on are in the body
+#pragma unroll
+                for (int i = 0; i < 17; ++i) d[i] = S(j0 + i);
+                uint32_t vo = rowoff + __umul24((uint32_t)(j0 + 17), n4);
+#pragma unroll
+                for (int i = 17; i < 35; ++i, vo += n4) d[i] = *(const uint32_t*)(sbase + vo);
+#pragma unroll
+                for (int i = 0; i < 2 * (int)PFX_WORDS; ++i) d[i] = align_bytes(d[i + 1], d[i], r) | pw[i];
+#pragma unroll
+                for (int i = 2 * (int)PFX_WORDS; i < 34; ++i) d[i] = align_bytes(d[i + 1], d[i], r);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 35; ++i) d[i] = S(j0 + 34 * (int)blk + i);
+#pragma unroll
+                for (int i = 0; i < 34; ++i) d[i] = align_bytes(d[i + 1], d[i], r);
+            }
+#pragma unroll
+            for (int i = 0; i < 17; ++i) { L[i] ^= d[2 * i]; H[i] ^= d[2 * i + 1]; }
+            if (blk + 1u == nb) H[16] ^= 0x80000000u;
+            keccak_f1600_lane(L, H);
+        }
+        uint32_t* dst = (uint32_t*)(hash + ((uint64_t)il * p.rows + x) * 32);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { prev[2 * i] = L[i]; prev[2 * i + 1] = H[i]; }
+        *(uint4*)dst = make_uint4(prev[0], prev[1], prev[2], prev[3]);
+        *(uint4*)(dst + 4) = make_uint4(prev[4], prev[5], prev[6], prev[7]);
+    }
+#endif
+}
+
 // Predicted chains (big-endian seeds, N = 64). With big-endian seeds the round-0 proposer of an
 // N = 64 instance is validator 0 at every height (validator.rs:33-48: the seed is 0 mod 64), so the block the
 // canonical tick commits at height x (spec_block64: proposer 0, the variant the SPLIT draw of view (x, 0) lets
@@ -458,21 +587,30 @@ hipError_t launch_hash_suffix(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* 
     else hipLaunchKernelGGL(bft_hash_suffix_kernel, dim3((uint32_t)(((uint64_t)n * rows + 255u) / 256u)), dim3(256), 0, s, p);
     return hipGetLastError();
 }
-hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, bool wave, hipStream_t s, Params p) {
+hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* sfx, uint32_t kind, hipStream_t s,
+                             Params p) {
     p.sfx = sfx;
     p.sfx_rows = rows;
     p.sfx_x0 = x0;
     ChainSets cs{};
     cs.count = 1; cs.sfx[0] = sfx; cs.ch[0] = p.committed_height; cs.hash[0] = p.hash;
-    if (wave) hipLaunchKernelGGL(bft_hash_chain_wave_kernel, dim3(8u * ((n + 7u) / 8u)), dim3(64), 0, s, p, cs);
+    if (kind == CHAIN_KERNEL_LANE && 4ull * n >= (1ull << 24)) kind = CHAIN_KERNEL_PAIR;   // its 24-bit offsets
+    if (kind == CHAIN_KERNEL_LANE)
+        hipLaunchKernelGGL(bft_hash_chain_lane_kernel, dim3((n + 63u) / 64u), dim3(64), 0, s, p, cs);
+    else if (kind == CHAIN_KERNEL_WAVE)
+        hipLaunchKernelGGL(bft_hash_chain_wave_kernel, dim3(8u * ((n + 7u) / 8u)), dim3(64), 0, s, p, cs);
     else hipLaunchKernelGGL(bft_hash_chain_kernel, dim3((n + 31u) / 32u), dim3(CHAIN_PAIR_BLOCK), 0, s, p, cs);
     return hipGetLastError();
 }
-hipError_t launch_hash_chain_batch(uint32_t n, const ChainSets& cs, bool wave, hipStream_t s, Params p) {
+hipError_t launch_hash_chain_batch(uint32_t n, const ChainSets& cs, uint32_t kind, hipStream_t s, Params p) {
     p.sfx_rows = p.heights;                               // every height in one chunk (bftsim.hip)
     p.sfx_x0 = 1;
     if (cs.count < 1 || cs.count > CHAIN_MAX_SETS) return hipErrorInvalidValue;
-    if (wave) hipLaunchKernelGGL(bft_hash_chain_wave_kernel, dim3(cs.count * 8u * ((n + 7u) / 8u)), dim3(64), 0, s, p, cs);
+    const bool wave = kind == CHAIN_KERNEL_WAVE;
+    if (kind == CHAIN_KERNEL_LANE && 4ull * n >= (1ull << 24)) kind = CHAIN_KERNEL_PAIR;   // its 24-bit offsets
+    if (kind == CHAIN_KERNEL_LANE)
+        hipLaunchKernelGGL(bft_hash_chain_lane_kernel, dim3(cs.count * ((n + 63u) / 64u)), dim3(64), 0, s, p, cs);
+    else if (wave) hipLaunchKernelGGL(bft_hash_chain_wave_kernel, dim3(cs.count * 8u * ((n + 7u) / 8u)), dim3(64), 0, s, p, cs);
     else hipLaunchKernelGGL(bft_hash_chain_kernel, dim3(cs.count * ((n + 31u) / 32u)), dim3(CHAIN_PAIR_BLOCK), 0, s, p, cs);
     return hipGetLastError();
 }

@@ -13,7 +13,10 @@ import os
 import sys
 from collections import defaultdict
 
-SHORT = {"bft_consensus_fast_kernel": "bft_consensus_fast_kernel",
+SHORT = {"bft_hash_chain_lane_kernel": "bft_hash_chain_kernel",     # the chain dispatch, whichever kernel runs it
+         "bft_spec_byz_kernel": "bft_spec_byz_kernel", "bft_spec_suffix_kernel": "bft_spec_suffix_kernel",
+         "bft_spec_verify_kernel": "bft_spec_verify_kernel", "bft_clear_kernel": "bft_clear_kernel",
+         "bft_consensus_fast_kernel": "bft_consensus_fast_kernel",
          "bft_consensus_resume_kernel": "bft_consensus_resume_kernel",
          "bft_consensus_kernel": "bft_consensus_kernel", "bft_hash_pair_kernel": "bft_hash_kernel",
          "bft_hash_lane_kernel": "bft_hash_kernel", "bft_hash_suffix_kernel": "bft_hash_suffix_kernel",
@@ -62,9 +65,16 @@ def attributed_writes(path):
         if i + 1 < len(rows) and rows[i + 1][0] == q and "bft_l2_evict_kernel" in rows[i + 1][2]:
             ev = rows[i + 1][3]
         acc[k].append((1024.0 * v, 1024.0 * ev))
-    return {k: {"write_bytes_own": sum(a for a, _ in v) / len(v), "write_bytes_evicted_after": sum(b for _, b in v) / len(v),
-                "write_bytes_attributed": sum(a + b for a, b in v) / len(v), "dispatches": len(v)}
-            for k, v in acc.items()}
+    # per LAUNCH, not per dispatch: a launch whose heights exceed the suffix rows of one chunk runs a suffix + chain
+    # dispatch per chunk, so each kernel's bytes are summed and divided by the launches (consensus dispatches)
+    launches = len(acc.get("bft_consensus_fast_kernel") or acc.get("bft_consensus_kernel") or []) or None
+    out = {}
+    for k, v in acc.items():
+        nl = launches or len(v)
+        out[k] = {"write_bytes_own": sum(a for a, _ in v) / nl, "write_bytes_evicted_after": sum(b for _, b in v) / nl,
+                  "write_bytes_attributed": sum(a + b for a, b in v) / nl, "dispatches": len(v),
+                  "dispatches_per_launch": len(v) / nl}
+    return out
 
 
 def stats(path):
