@@ -109,6 +109,9 @@ def step_traffic(workload: str, batch: int):
             continue
         if "hbm_bytes_per_launch_attributed" in e:
             parts[k] = e["hbm_bytes_per_launch_attributed"]            # per launch (attribution pass)
+        elif "hbm_bytes_per_launch" in e:                              # per launch (the pass's launches)
+            attributed = False
+            parts[k] = e["hbm_bytes_per_launch"]
         elif "hbm_bytes_per_dispatch" in e:
             attributed = False
             parts[k] = e["hbm_bytes_per_dispatch"] / (batch if k == "bft_hash_chain_kernel" else 1)
@@ -124,7 +127,7 @@ SALU_ISSUE_PEAK = 256 * 2.4e9           # scalar instructions/s: one scalar unit
 
 
 def pmc_issue(workload: str = "cfg3", kernel: str = "bft_consensus_kernel"):
-    """Per dispatch VALU / SALU wave-instructions of a kernel (the consensus kernel: its FAST body) from the
+    """Per launch VALU / SALU wave-instructions of a kernel (the consensus kernel: its FAST body) from the
     newest PMC summary of this workload (SQ_INSTS_VALU, SQ_INSTS_SALU of scripts/gpu_profile.sh's SQ pass),
     or None."""
     files = _pmc_files(workload)
@@ -135,7 +138,9 @@ def pmc_issue(workload: str = "cfg3", kernel: str = "bft_consensus_kernel"):
          else k.get(kernel) or {})
     if "SQ_INSTS_VALU" not in e:
         return None
-    return {"valu": e["SQ_INSTS_VALU"], "salu": e.get("SQ_INSTS_SALU")}
+    # per launch where the summary has it (a chain dispatch carries several launches), else per dispatch
+    return {"valu": e.get("SQ_INSTS_VALU_per_launch", e["SQ_INSTS_VALU"]),
+            "salu": e.get("SQ_INSTS_SALU_per_launch", e.get("SQ_INSTS_SALU"))}
 
 
 def cfg_desc(cfg) -> str:
@@ -499,10 +504,13 @@ def main():
         # pipelined, one dispatch hashes `hash_batch` launches and its time is shared among them). Launches
         # overlap when pipelined, so these are stretched durations, as rocprof reports them.
         batch = args.hash_batch if (pipelined and h_ops) else 1
+        # Everything is priced per LAUNCH (one step): a chain dispatch's time is shared among the launches it
+        # carries (bftsim_kernel_ms_sum), as rocprof's total chain time over the launches of a pass is
+        # (pmc_summary.json ms_per_launch)
         if cms >= hms:
             dom, ops, ms = "bft_consensus_kernel", c_ops, cms
         else:
-            dom, ops, ms = "bft_hash_chain_kernel", h_ops * batch, hms * batch   # per chain dispatch
+            dom, ops, ms = "bft_hash_chain_kernel", h_ops, hms
         achieved = ops / (ms / 1e3) / 1e12
         peak = VALU_PEAK / 1e12
         pmc_key = f"cfg4_n{cfg.n}" if wl == "cfg4" else wl
@@ -566,9 +574,10 @@ def main():
                     "valu_frac": q["valu"] / (ms / 1e3) / VALU_ISSUE_PEAK,
                     "salu_per_s": q["salu"] / (ms / 1e3), "salu_peak_per_s": SALU_ISSUE_PEAK,
                     "salu_frac": q["salu"] / (ms / 1e3) / SALU_ISSUE_PEAK,
-                    "per_instance_round": {"valu": q["valu"] / max(views_rank * batch, 1),
-                                           "salu": q["salu"] / max(views_rank * batch, 1)}})(pmc_issue(pmc_key, dom)),
-                "dispatch": {"launches_per_dispatch": batch, "ops_per_dispatch": ops, "ms_per_dispatch": ms},
+                    "per_instance_round": {"valu": q["valu"] / max(views_rank, 1),
+                                           "salu": q["salu"] / max(views_rank, 1)}})(pmc_issue(pmc_key, dom)),
+                "per": "launch (one step; a chain dispatch's time and counters shared among the launches it carries)",
+                "dispatch": {"launches_per_dispatch": batch, "ops_per_dispatch": ops * batch, "ms_per_dispatch": ms * batch},
                 "traffic_source": traffic_src,
                 "hbm": {"algorithmic_bytes": algo_bytes, "unit": "bytes per step",
                         "achieved_GBps": algo_bytes / (ms_step / 1e3) / 1e9,

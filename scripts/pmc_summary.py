@@ -106,31 +106,49 @@ def main():
     res["fetch_pass_hash_batch"] = batch
     meta.update(meta2)
     meta.update(meta3)
+
+    # launches of each pass = its consensus dispatches (one FAST or general kernel per launch); a chain dispatch
+    # carries however many launches its batch held in that pass (a short pass flushes partial batches), so the
+    # per-launch figures are each kernel's sum over the pass divided by the pass's launches
+    def launches(acc):
+        c = acc.get("bft_consensus_fast_kernel") or acc.get("bft_consensus_kernel") or {}
+        return max((len(v) for v in c.values()), default=0) or None
+    nl_fetch, nl_write, nl_sq = launches(fetch), launches(write), launches(sq)
+    res["launches_per_pass"] = {"fetch": nl_fetch, "write": nl_write, "sq": nl_sq}
+    st_launches = (st.get("bft_consensus_fast_kernel") or st.get("bft_consensus_kernel") or {}).get("calls")
     for k in set(st) | set(fetch) | set(write) | set(sq) | set(attr):
         e = dict(meta.get(k, {}))
         if k in st:
             e.update(avg_ms=st[k]["avg_ns"] / 1e6, calls=st[k]["calls"])
+            if st_launches:                              # device time per launch (the stats pass's own launches)
+                e["ms_per_launch"] = st[k]["avg_ns"] * st[k]["calls"] / st_launches / 1e6
         f = fetch.get(k, {}).get("FETCH_SIZE")
         w = write.get(k, {}).get("WRITE_SIZE")
         if f:
             e["fetch_bytes_raw"] = 1024.0 * sum(f) / len(f)
             e["fetch_bytes"] = 2.0 * e["fetch_bytes_raw"]      # gfx950 FETCH_SIZE correction
+            if nl_fetch:
+                e["fetch_bytes_per_launch"] = 2.0 * 1024.0 * sum(f) / nl_fetch
         if w:
             e["write_bytes"] = 1024.0 * sum(w) / len(w)
+            if nl_write:
+                e["write_bytes_per_launch"] = 1024.0 * sum(w) / nl_write
         if f and w:
             e["hbm_bytes_per_dispatch"] = e["fetch_bytes"] + e["write_bytes"]
+            if nl_fetch and nl_write:
+                e["hbm_bytes_per_launch"] = e["fetch_bytes_per_launch"] + e["write_bytes_per_launch"]
         if k in attr:
             # writes measured with an L2 eviction after every kernel of unpipelined launches (one dispatch of each
             # kernel per launch): the kernel's own write-backs, none borrowed from or lent to kernels running
             # beside it; with the FETCH pass's bytes per launch (a chain dispatch of that pass carries `batch`
             # launches) this is the kernel's HBM traffic per launch
             e["write_attribution"] = attr[k]
-            if f:
-                per = batch if k == "bft_hash_chain_kernel" else 1
-                e["fetch_bytes_per_launch"] = e["fetch_bytes"] / per
+            if f and nl_fetch:
                 e["hbm_bytes_per_launch_attributed"] = e["fetch_bytes_per_launch"] + attr[k]["write_bytes_attributed"]
         for c, v in sq.get(k, {}).items():
             e[c] = sum(v) / len(v)
+            if nl_sq:
+                e[c + "_per_launch"] = sum(v) / nl_sq
         res["kernels"][k] = e
     # N = 64 launches run the FAST kernel then the resume kernel (one dispatch each per launch):
     # bench.py's HIP events bracket both, so the consensus entry is their per-launch sum
