@@ -89,7 +89,9 @@ struct Params {
     uint32_t* spec;                   // [heights + 1][n_inst] spec_word or 0
     // block-hash chains (kern_fast.hip): CHAIN_RECORDED / CHAIN_PREDICTED / CHAIN_REPAIR (bft_hip.h)
     uint32_t chain_mode;
-    uint32_t pad6;
+    uint32_t chain_grid;              // lane-chain kernel: at most this many (persistent) waves; 0: one per task
+    uint32_t chain_inline;            // lane-chain kernel: each lane encodes its suffixes (no suffix rows)
+    uint32_t pad7;
 };
 constexpr uint32_t RCS_DEFAULT_K = 16, RCS_MAX_K = 4096;
 // one logged broadcast: {tick, phase | code << 8 | sender << 16, height, round, block id lo, hi,

@@ -454,6 +454,13 @@ struct bftsim {
     // one lane per instance from this many instances per launch (kern_fast.hip bft_hash_chain_lane_kernel: fewer
     // instructions per header, longer chains; BFTSIM_TESTING + BFTSIM_CHAIN_LANE_MIN overrides)
     uint64_t chain_lane_min = 12288;
+    // persistent lane-chain waves per dispatch, 0: a wave per 64 instances (BFTSIM_TESTING + BFTSIM_CHAIN_GRID; an A/B
+    // arm: capping the chain waves so that the consensus kernels keep SIMD slots measured the same or slower)
+    uint32_t chain_grid = 0;
+    // lane chains encode each height's suffix themselves from the recorded rows: no suffix-row kernel on the launch
+    // streams (0.3-0.45 ms per cfg3 launch beside the FAST kernels), no 400 MB of rows written and read back
+    // (BFTSIM_TESTING + BFTSIM_CHAIN_INLINE=0: the suffix rows)
+    uint32_t chain_inline = 1;
     uint32_t chain_prio = 0;          // s_setprio of the chain waves (BFTSIM_TESTING + BFTSIM_CHAIN_PRIO)
     uint32_t fast_lds_pad = 0;        // extra LDS per FAST wave: fewer resident FAST waves (BFTSIM_TESTING + BFTSIM_FAST_LDS_PAD)
     bool seed_spec = true;            // little-endian seeds, N = 64: predicted blocks (BFTSIM_TESTING + BFTSIM_SEED_SPEC=0: off)
@@ -837,6 +844,8 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
             if (testing && e) { const uint32_t x = (uint32_t)atoi(e); v = x < lo ? lo : x > hi ? hi : x; }
         };
         knob("BFTSIM_LAUNCH_STREAMS", h->n_cs, 1, bftsim::MAX_CS);
+        knob("BFTSIM_CHAIN_GRID", h->chain_grid, 0, 1u << 20);
+        knob("BFTSIM_CHAIN_INLINE", h->chain_inline, 0, 1);
         knob("BFTSIM_LAUNCH_STREAMS_SEEDED", h->n_cs_seeded, 1, bftsim::MAX_CS);
         knob("BFTSIM_HASH_STREAMS", h->n_hs, 1, bftsim::MAX_HS);   // A/B arms
         knob("BFTSIM_HASH_BATCH", h->hash_batch, 1, bftsim::MAX_BATCH);   // A/B arms (bftsim_set_hash_batch)
@@ -966,6 +975,8 @@ static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
     p.rcs = h->d_rcs;
     p.rcs_k = h->rcs_k;
     p.chain_prio = h->chain_prio;
+    p.chain_grid = h->chain_grid;
+    p.chain_inline = h->chain_inline;
     p.fast_lds_pad = h->fast_lds_pad;
     p.backlog = h->d_backlog;
     if (h->crypto && h->d_mlog) {
@@ -988,7 +999,7 @@ static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
 
 // which chain kernel hashes a batch of launches of n instances (the wave kernel has no predicted / repair mode)
 static uint32_t chain_kind(const bftsim* h, uint64_t n, bool spec) {
-    if (n >= h->chain_lane_min) return bft::CHAIN_KERNEL_LANE;
+    if (n >= h->chain_lane_min && 4ull * n < (1ull << 24)) return bft::CHAIN_KERNEL_LANE;   // its 24-bit offsets
     if (!spec && n <= h->chain_wave_max) return bft::CHAIN_KERNEL_WAVE;
     return bft::CHAIN_KERNEL_PAIR;
 }
@@ -1134,9 +1145,11 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
             bftsim::RowSet& r = h->sets[h->cur_set];
             const bool hspec = r.byz && n < h->hash_spec_max;   // big-endian seeds: predicted chains
             if (!hspec) {
-                // suffix rows now; the chains in the next batch (flush_batch)
-                HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, 1, K, sfx, false, s, p));
-                HIPCHECK(h, pmc_evict(h, s));
+                // suffix rows now (unless the lane chains encode them); the chains in the next batch (flush_batch)
+                if (!(h->chain_inline && chain_kind(h, n, false) == bft::CHAIN_KERNEL_LANE)) {
+                    HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, 1, K, sfx, false, s, p));
+                    HIPCHECK(h, pmc_evict(h, s));
+                }
                 HIPCHECK(h, hipEventRecord(ev.sx, s));
             }
             ev.has_hash = false;                          // the batch's last launch carries the chain time
@@ -1161,10 +1174,13 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
                 HIPCHECK(h, hipStreamWaitEvent(t, ev.c1, 0));
             }
             HIPCHECK(h, hipEventRecord(ev.h0, t));
+            const uint32_t kind = chain_kind(h, n, false);
             for (uint32_t x0 = 1; x0 <= H; x0 += K) {
-                HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, x0, K, sfx, !on_launch, t, p));
-                HIPCHECK(h, pmc_evict(h, t));
-                HIPCHECK(h, bft::launch_hash_chain((uint32_t)n, x0, K, sfx, chain_kind(h, n, false), t, p));
+                if (!(h->chain_inline && kind == bft::CHAIN_KERNEL_LANE)) {
+                    HIPCHECK(h, bft::launch_hash_suffix((uint32_t)n, x0, K, sfx, !on_launch, t, p));
+                    HIPCHECK(h, pmc_evict(h, t));
+                }
+                HIPCHECK(h, bft::launch_hash_chain((uint32_t)n, x0, K, sfx, kind, t, p));
                 HIPCHECK(h, pmc_evict(h, t));
             }
             HIPCHECK(h, hipEventRecord(ev.h1, t));

@@ -294,12 +294,12 @@ __global__ __launch_bounds__(CHAIN_PAIR_BLOCK) void bft_hash_chain_kernel(Params
 
 // Keccak-f[1600] with the whole state in one lane as 32-bit halves (L low, H high): theta's D folded into one
 // 3-input XOR per half-word (v_bitop3_b32), rotations as two v_alignbit_b32, chi one v_bitop3_b32 per half-word:
-// ~180 VALU per round (+~80 v_mov: rho-pi permutes the 25 words with period 24, so a round loop moves them back to
-// their registers every round). Unrolling 2, 4 or all 24 rounds measured the same (24: 203 VGPRs instead of 118;
-// profiles/r06/ab_lane), so the loop is kept (code size); one call site in the kernel.
+// ~180 VALU per round. The 24 rounds unrolled: rho-pi permutes the 25 words with period 24, so a round loop pays
+// ~80 v_mov per round to move them back to their registers (cfg3 with inline suffixes: 1.81e9-1.84e9 with the loop,
+// 1.90e9-1.94e9 unrolled; profiles/r06/ab_lane); one call site in the kernel (code size).
 #if defined(__HIP_DEVICE_COMPILE__)
 #ifndef BFT_LANE_UNROLL
-#define BFT_LANE_UNROLL 1
+#define BFT_LANE_UNROLL 24
 #endif
 __device__ inline void keccak_f1600_lane(uint32_t L[25], uint32_t H[25]) {
 #pragma unroll BFT_LANE_UNROLL
@@ -339,16 +339,15 @@ __device__ inline void keccak_f1600_lane(uint32_t L[25], uint32_t H[25]) {
 // pairs, 1.82e9-1.85e9 with lanes in batches of 12; profiles/r06/ab_lane).
 // The splice reads the suffix row straight from global memory (rows are dword-major across instances, so a load
 // instruction touches one row per distinct prefix length in the wave) instead of an LDS splice buffer per lane.
-__global__ __launch_bounds__(64) void bft_hash_chain_lane_kernel(Params p, ChainSets cs) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    set_prio(p.chain_prio);
-    const uint32_t bps = (p.n_instances + 63u) / 64u, k = blockIdx.x / bps;
-    __shared__ __attribute__((aligned(16))) uint64_t pbuf[64 * (PFX_WORDS + 4)];   // prefix words per lane
-    __shared__ PfxSel ptbl[16];
-    if (threadIdx.x < 16) ptbl[threadIdx.x] = PFX_TBL[threadIdx.x];
-    __syncthreads();
-    const uint32_t n = p.n_instances, il = (blockIdx.x % bps) * 64u + threadIdx.x;
-    if (il >= n) return;
+// one instance's chain (launch k of the batch, instance il) by one lane
+// INLINE: the lane encodes each height's suffix itself from the recorded row (proposer, variant, time tick) into its
+// column of `sl` (LDS, dword j at sl[64 j]) instead of reading a suffix row of bft_hash_suffix_kernel (RECORDED and
+// REPAIR modes only)
+template <bool INLINE>
+__device__ inline void lane_chain(const Params& p, const ChainSets& cs, uint32_t k, uint32_t il, uint64_t* pbuf,
+                                  const PfxSel* ptbl, uint32_t* sl) {
+    const uint32_t n = p.n_instances;
     const uint32_t K = p.sfx_rows, x0 = p.sfx_x0;
     uint32_t x1 = x0 + K - 1u, xs = x0;
     if (p.chain_mode != CHAIN_PREDICTED) {
@@ -369,21 +368,37 @@ __global__ __launch_bounds__(64) void bft_hash_chain_lane_kernel(Params p, Chain
     // rows are < 2 GiB, bftsim.hip); dword j of the row of height x at 4 (il + ((x - x0) SFX_DEV_DW + j) n)
     const char* const sbase = (const char*)cs.sfx[k];
     const uint32_t n4 = 4u * n;                      // < 2^24 (launch_hash_chain_batch): 24-bit multiplies
-    const uint64_t* pb = pbuf + threadIdx.x * (PFX_WORDS + 4);
+    const uint64_t* pb = pbuf;
+    const uint32_t* const rec = cs.rec[k] + (uint64_t)il * p.rows * 4u;
     for (uint32_t x = xs; x <= x1; ++x) {
         const uint32_t rowoff = 4u * il + (x - x0) * SFX_DEV_DW * n4;
-        const uint32_t len_s = *(const uint32_t*)(sbase + rowoff + SFX_DEV_LEN_DW * n4);
+        uint32_t len_s;
+        if constexpr (INLINE) {                      // the suffix of the recorded block x (bft_hash_suffix_kernel's)
+            const uint4 row = *(const uint4*)(rec + 4u * x);
+            const uint32_t prop = row.y & 0xffffu, var = (row.y >> 16) & 1u;
+            HdrWriter w(sl, 64u);
+            header_suffix_fields(w, p.addresses + 20u * prop, p.seed, cs.first[k] + il, x, prop, var,
+                                 p.genesis_time + (uint64_t)p.block_period * ((uint64_t)row.z + 1ull));
+            len_s = 8u * w.wi + w.fill;
+            w.store(w.wi++, w.acc | (0x01ull << (8u * w.fill)));
+            while (w.wi < SFX_BODY_DW / 2u) w.store(w.wi++, 0);
+        } else {
+            len_s = *(const uint32_t*)(sbase + rowoff + SFX_DEV_LEN_DW * n4);
+        }
         if (len_s == 0u) break;                      // no prediction for x (CHAIN_PREDICTED only)
-        const uint32_t len_p = header_prefix_perm(pbuf + threadIdx.x * (PFX_WORDS + 4), prev, ptbl);
+        const uint32_t len_p = header_prefix_perm(pbuf, prev, ptbl);
         uint32_t pw[2 * PFX_WORDS];
 #pragma unroll
         for (uint32_t i = 0; i < PFX_WORDS; ++i) { const uint64_t v = pb[i]; pw[2 * i] = (uint32_t)v; pw[2 * i + 1] = (uint32_t)(v >> 32); }
         const uint32_t c = 72u - len_p, r = c & 3u, nb = splice_blocks(len_p, len_s);
         const int j0 = (int)(c >> 2) - (int)SFX_PAD;   // body dword of splice dword q0: -17 .. -9
         // splice-buffer dword j0 + i: the body dword, zero outside [0, SFX_BODY_DW) (the pad and the tail)
+        auto G = [&](uint32_t jj) -> uint32_t {      // body dword jj < SFX_BODY_DW
+            if constexpr (INLINE) return sl[64u * jj];
+            else return *(const uint32_t*)(sbase + rowoff + __umul24(jj, n4));
+        };
         auto S = [&](int j) -> uint32_t {
-            const uint32_t jj = (uint32_t)(j < 0 ? 0 : j > (int)SFX_BODY_DW - 1 ? (int)SFX_BODY_DW - 1 : j);
-            const uint32_t v = *(const uint32_t*)(sbase + rowoff + __umul24(jj, n4));
+            const uint32_t v = G((uint32_t)(j < 0 ? 0 : j > (int)SFX_BODY_DW - 1 ? (int)SFX_BODY_DW - 1 : j));
             return (j >= 0) & (j < (int)SFX_BODY_DW) ? v : 0u;
         };
         uint32_t L[25], H[25];
@@ -394,9 +409,14 @@ __global__ __launch_bounds__(64) void bft_hash_chain_lane_kernel(Params p, Chain
             if (blk == 0u) {                         // the prefix lies here; dwords from 17 on are in the body
 #pragma unroll
                 for (int i = 0; i < 17; ++i) d[i] = S(j0 + i);
-                uint32_t vo = rowoff + __umul24((uint32_t)(j0 + 17), n4);
+                if constexpr (INLINE) {
 #pragma unroll
-                for (int i = 17; i < 35; ++i, vo += n4) d[i] = *(const uint32_t*)(sbase + vo);
+                    for (int i = 17; i < 35; ++i) d[i] = G((uint32_t)(j0 + i));
+                } else {
+                    uint32_t vo = rowoff + __umul24((uint32_t)(j0 + 17), n4);
+#pragma unroll
+                    for (int i = 17; i < 35; ++i, vo += n4) d[i] = *(const uint32_t*)(sbase + vo);
+                }
 #pragma unroll
                 for (int i = 0; i < 2 * (int)PFX_WORDS; ++i) d[i] = align_bytes(d[i + 1], d[i], r) | pw[i];
 #pragma unroll
@@ -418,7 +438,39 @@ __global__ __launch_bounds__(64) void bft_hash_chain_lane_kernel(Params p, Chain
         *(uint4*)dst = make_uint4(prev[0], prev[1], prev[2], prev[3]);
         *(uint4*)(dst + 4) = make_uint4(prev[4], prev[5], prev[6], prev[7]);
     }
+}
 #endif
+// Persistent: at most p.chain_grid workgroups (one wave each), each taking 64 instances after another. A chain wave
+// runs its instances' 100 heights back to back, so a grid of every task at once held every SIMD slot for the whole
+// dispatch and the consensus kernels beside it got none (cfg3: a FAST kernel 0.40 -> 4.6 ms under a 12-launch chain
+// dispatch, profiles/r06/trace_k16); capped, the chain waves leave slots to them.
+// register budget: a chain wave beside the FAST kernel's waves (4 per SIMD) on the same SIMD
+#ifndef BFT_LANE_WAVES_PER_SIMD
+#define BFT_LANE_WAVES_PER_SIMD 3
+#endif
+template <bool INLINE>
+__global__ __launch_bounds__(64, BFT_LANE_WAVES_PER_SIMD) void bft_hash_chain_lane_kernel(Params p, ChainSets cs) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    set_prio(p.chain_prio);
+    __shared__ __attribute__((aligned(16))) uint64_t pbuf[64 * (PFX_WORDS + 4)];   // prefix words per lane
+    __shared__ PfxSel ptbl[16];
+    extern __shared__ uint32_t sfx_lds[];             // INLINE: [SFX_BODY_DW][64] suffix dwords (launch's dynamic LDS)
+    if (threadIdx.x < 16) ptbl[threadIdx.x] = PFX_TBL[threadIdx.x];
+    __syncthreads();
+    const uint32_t bps = (p.n_instances + 63u) / 64u, tasks = cs.count * bps;
+    for (uint32_t t = blockIdx.x; t < tasks; t += gridDim.x) {   // every wave reaches the end of the task list
+        const uint32_t k = t / bps, il = (t % bps) * 64u + threadIdx.x;
+        if (il < p.n_instances)
+            lane_chain<INLINE>(p, cs, k, il, pbuf + threadIdx.x * (PFX_WORDS + 4), ptbl, INLINE ? sfx_lds + threadIdx.x : nullptr);
+    }
+#endif
+}
+static hipError_t launch_lane(uint32_t tasks, const ChainSets& cs, hipStream_t s, const Params& p) {
+    const uint32_t g = p.chain_grid && p.chain_grid < tasks ? p.chain_grid : tasks;   // persistent waves
+    if (p.chain_inline && p.chain_mode != CHAIN_PREDICTED)   // the inline suffix columns in dynamic LDS
+        hipLaunchKernelGGL(bft_hash_chain_lane_kernel<true>, dim3(g), dim3(64), (size_t)SFX_BODY_DW * 64u * 4u, s, p, cs);
+    else hipLaunchKernelGGL(bft_hash_chain_lane_kernel<false>, dim3(g), dim3(64), 0, s, p, cs);
+    return hipGetLastError();
 }
 
 // Predicted chains (big-endian seeds, N = 64). With big-endian seeds the round-0 proposer of an
@@ -594,9 +646,9 @@ hipError_t launch_hash_chain(uint32_t n, uint32_t x0, uint32_t rows, uint32_t* s
     p.sfx_x0 = x0;
     ChainSets cs{};
     cs.count = 1; cs.sfx[0] = sfx; cs.ch[0] = p.committed_height; cs.hash[0] = p.hash;
+    cs.rec[0] = p.rec; cs.first[0] = p.first_instance;
     if (kind == CHAIN_KERNEL_LANE && 4ull * n >= (1ull << 24)) kind = CHAIN_KERNEL_PAIR;   // its 24-bit offsets
-    if (kind == CHAIN_KERNEL_LANE)
-        hipLaunchKernelGGL(bft_hash_chain_lane_kernel, dim3((n + 63u) / 64u), dim3(64), 0, s, p, cs);
+    if (kind == CHAIN_KERNEL_LANE) return launch_lane((n + 63u) / 64u, cs, s, p);
     else if (kind == CHAIN_KERNEL_WAVE)
         hipLaunchKernelGGL(bft_hash_chain_wave_kernel, dim3(8u * ((n + 7u) / 8u)), dim3(64), 0, s, p, cs);
     else hipLaunchKernelGGL(bft_hash_chain_kernel, dim3((n + 31u) / 32u), dim3(CHAIN_PAIR_BLOCK), 0, s, p, cs);
@@ -608,9 +660,8 @@ hipError_t launch_hash_chain_batch(uint32_t n, const ChainSets& cs, uint32_t kin
     if (cs.count < 1 || cs.count > CHAIN_MAX_SETS) return hipErrorInvalidValue;
     const bool wave = kind == CHAIN_KERNEL_WAVE;
     if (kind == CHAIN_KERNEL_LANE && 4ull * n >= (1ull << 24)) kind = CHAIN_KERNEL_PAIR;   // its 24-bit offsets
-    if (kind == CHAIN_KERNEL_LANE)
-        hipLaunchKernelGGL(bft_hash_chain_lane_kernel, dim3(cs.count * ((n + 63u) / 64u)), dim3(64), 0, s, p, cs);
-    else if (wave) hipLaunchKernelGGL(bft_hash_chain_wave_kernel, dim3(cs.count * 8u * ((n + 7u) / 8u)), dim3(64), 0, s, p, cs);
+    if (kind == CHAIN_KERNEL_LANE) return launch_lane(cs.count * ((n + 63u) / 64u), cs, s, p);
+    if (wave) hipLaunchKernelGGL(bft_hash_chain_wave_kernel, dim3(cs.count * 8u * ((n + 7u) / 8u)), dim3(64), 0, s, p, cs);
     else hipLaunchKernelGGL(bft_hash_chain_kernel, dim3(cs.count * ((n + 31u) / 32u)), dim3(CHAIN_PAIR_BLOCK), 0, s, p, cs);
     return hipGetLastError();
 }

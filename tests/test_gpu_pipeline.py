@@ -111,13 +111,13 @@ def _timed_run(cfg, first, n, launches=25):
 
 def test_timed_mode_full_size():
     """The exact configuration of the headline number: cfg3 at 16,384 instances on one GPU with bench.py's
-    pipeline depth and hash batch (24 x 12, lane-per-instance chains), 25 launches of the same instances; every
+    pipeline depth and hash batch (16 x 8, lane-per-instance chains), 25 launches of the same instances; every
     instance against the oracle."""
     from bftsim.configs import INSTANCES
     cfg = cfg3()
     n = INSTANCES["cfg3"]
     got, st, (depth, batch) = _timed_run(cfg, 0, n)
-    assert (depth, batch) == (24, 12)
+    assert (depth, batch) == (16, 8)
     ref = O.run(cfg, 0, n, threads=16)
     assert_same(ref, got, f"cfg3 {n} depth {depth} batch {batch} x25")
     assert st["views"] == int(ref["views"].sum()) == n * 100
@@ -251,16 +251,22 @@ def test_predicted_chains_match_oracle(name, mk, depth, batch, monkeypatch):
     assert_same(ref, outs[1], name + " recorded chains")
 
 
+@pytest.mark.parametrize("grid", ["0", "3"])
+@pytest.mark.parametrize("inline", ["0", "1"])
 @pytest.mark.parametrize("spec", ["1", "0"])
 @pytest.mark.parametrize("name,mk", [("cfg3-30", lambda: cfg3(heights=30)),
                                      ("n64-drop", lambda: BftConfig(n=64, heights=30, seed=17, byz_count=21,
                                                                     drop_ppm=50_000, name="n64-drop"))])
-def test_lane_chain_kernel(name, mk, spec, monkeypatch):
-    """The lane-per-instance chain kernel (BFTSIM_CHAIN_LANE_MIN; the suffix spliced straight from the global rows) in
-    all three chain modes: recorded blocks, and predicted blocks with the repair from the first one that differs."""
+def test_lane_chain_kernel(name, mk, spec, inline, grid, monkeypatch):
+    """The lane-per-instance chain kernel (BFTSIM_CHAIN_LANE_MIN) in all three chain modes: recorded blocks, and
+    predicted blocks with the repair from the first one that differs; the suffix spliced from the suffix rows or
+    encoded by each lane from the recorded row (BFTSIM_CHAIN_INLINE); one wave per task or 3 persistent waves for
+    the whole batch (BFTSIM_CHAIN_GRID)."""
     monkeypatch.setenv("BFTSIM_TESTING", "1")
     monkeypatch.setenv("BFTSIM_CHAIN_LANE_MIN", "1")
     monkeypatch.setenv("BFTSIM_HASH_SPEC", spec)
+    monkeypatch.setenv("BFTSIM_CHAIN_INLINE", inline)
+    monkeypatch.setenv("BFTSIM_CHAIN_GRID", grid)
     cfg = mk()
     n = 160
     sim = _sim(cfg)
