@@ -311,7 +311,8 @@ def main():
     ap.add_argument("--n", type=int, default=256, help="cfg4: validators per instance")
     ap.add_argument("--instances", type=int, default=None, help="instances per GPU")
     ap.add_argument("--heights", type=int, default=None)
-    ap.add_argument("--window", type=int, default=256, help="cfg5: canonical rows kept per instance")
+    ap.add_argument("--window", type=int, default=None, help="cfg5: canonical rows kept per instance (default "
+                    "bftsim.configs.CFG5_WINDOW)")
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -337,12 +338,16 @@ def main():
                          "weak number, 16,384 per GPU, is measured too and reported in config.weak), weak for the "
                          "other workloads")
     args = ap.parse_args()
-    if args.steps is None:
-        args.steps = 20 if args.workload == "cfg3" else 10
-    if args.warmup is None:
-        args.warmup = 5 if args.workload == "cfg3" else 2
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args.gpus))           # before anything touches the GPU
+        sys.exit(spawn_ranks(args.gpus))           # before anything touches the GPU (or imports bftsim)
+    from bftsim.configs import bench_steps, bench_instances, bench_config
+    if args.window is None:
+        from bftsim.configs import CFG5_WINDOW
+        args.window = CFG5_WINDOW
+    if args.steps is None:
+        args.steps = bench_steps(args.workload)[0]
+    if args.warmup is None:
+        args.warmup = bench_steps(args.workload)[1]
     if os.environ.get("BFTSIM_TESTING") == "1" and os.environ.get("BFTSIM_BENCH_STUB_DIR"):
         return stub_rank(args)
     if args.hw_queues > 0:                         # read by the HIP runtime at its initialisation (below)
@@ -367,7 +372,7 @@ def main():
     c5 = args.workload == "cfg5"
     wl = args.workload
     if args.instances is None:
-        args.instances = {"cfg5": 131_072, "cfg2": 65_536}.get(wl, 16_384)
+        args.instances = bench_instances(wl)
     if args.heights is None:
         args.heights = 10_000 if c5 else 100
     if args.cpu_sample is None:
@@ -382,16 +387,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    if wl == "cfg5":
-        cfg = cfg5(heights=args.heights, byz=args.byz or 0)
-    elif wl == "cfg2":
-        cfg = cfg2(heights=args.heights, byz=args.byz or 0)
-    elif wl == "cfg4":
-        cfg = cfg4(args.n, heights=args.heights)
-    elif wl == "drop64":
-        cfg = BftConfig(n=64, heights=args.heights, seed=15, byz_count=21, drop_ppm=50_000, name="drop64")
-    else:
-        cfg = cfg3(heights=args.heights)
+    cfg = bench_config(wl, n=args.n, heights=args.heights, byz=args.byz or 0)
     if args.seed_order == "le":
         import dataclasses
         cfg = dataclasses.replace(cfg, seed_byte_order=1, name=cfg.name + "-le")

@@ -142,3 +142,37 @@ def timed_pipeline(instances_per_gpu: int):
     set) with chain batches of 8. tests/test_gpu_pipeline.py runs exactly these settings at full
     size."""
     return (16, 8) if instances_per_gpu >= 12_288 else (32, 8)
+
+
+# ---- the benchmark's workloads (bench.py --workload), shared with the tests that pin each timed mode ----
+def drop64(heights: int = 100) -> BftConfig:
+    """cfg3 with 5 % link drops (N = 64, f = 21 equivocating): the lossy FAST / resume path."""
+    return BftConfig(n=64, heights=heights, seed=15, byz_count=21, drop_ppm=50_000, name="drop64")
+
+
+BENCH_INSTANCES = {"cfg5": 131_072, "cfg2": 65_536}    # per GPU; every other workload 16,384
+CFG5_WINDOW = 256                                      # canonical rows kept per instance (bftsim_set_window)
+
+
+def bench_instances(workload: str) -> int:
+    return BENCH_INSTANCES.get(workload, 16_384)
+
+
+def bench_steps(workload: str):
+    """(timed steps, warmup steps) bench.py defaults to: the driver's 20 / 5 for the headline, 10 / 2 otherwise."""
+    return (20, 5) if workload == "cfg3" else (10, 2)
+
+
+def bench_config(workload: str, n: int = 256, heights: int = None, byz: int = 0) -> BftConfig:
+    """The BftConfig bench.py times a workload on (cfg4: `n` validators)."""
+    if workload == "cfg5":
+        return cfg5(heights=heights or 10_000, byz=byz)
+    h = heights or 100
+    if workload == "cfg2":
+        return cfg2(heights=h, byz=byz)
+    if workload == "cfg4":
+        return cfg4(n, heights=h)
+    if workload == "drop64":
+        return drop64(heights=h)
+    return cfg3(heights=h)
+

@@ -443,6 +443,7 @@ struct bftsim {
         uint32_t* resume = nullptr; uint32_t* save = nullptr; uint32_t* resume_q = nullptr;
         uint32_t* hint = nullptr;     // host-mapped: the hand-over count of the set's last launch (resume grid)
         hipEvent_t done = nullptr;    // hash pass of the last launch that used the set
+        hipEvent_t batch_done = nullptr;   // or: the event of the chain batch that hashed it (flush_batch)
         hipEvent_t entry = nullptr;   // the caller's stream at the launch call
         bool busy = false;
     } sets[MAX_SETS];
@@ -481,7 +482,12 @@ struct bftsim {
     // a large one by the chip's issue, which the checks only add to (profiles/r06/ab_spec)
     uint64_t hash_spec_max = 12288;
     uint32_t n_hs_spec = 3;
-    struct Pending { uint32_t set, ev, first; } pend[MAX_BATCH];
+    struct Pending { uint32_t set, ev, first, cs; } pend[MAX_BATCH];   // cs: the launch stream it ran on
+    // one event per chain batch (flush_batch) instead of one per set: a ring, re-recorded after BATCH_EVS batches (a set
+    // still pointing at a re-recorded event waits for a later batch: later, never wrong)
+    static constexpr uint32_t BATCH_EVS = 64;
+    hipEvent_t batch_ev[BATCH_EVS] = {};
+    uint32_t batch_ev_head = 0;
     uint32_t n_pend = 0;
     bft::Params batch_p{};            // the launch parameters of the pending batch (sizes, genesis, prio)
     bool batch_spec = false;          // the pending batch runs predicted chains
@@ -778,9 +784,12 @@ void bftsim_destroy(bftsim_t* h) {
     }
     for (uint32_t i = 0; i < bftsim::MAX_SETS; ++i) {
         if (h->sets[i].done) (void)hipEventDestroy(h->sets[i].done);
+        h->sets[i].batch_done = nullptr;
         if (h->sets[i].entry) (void)hipEventDestroy(h->sets[i].entry);
         if (h->sets[i].hint) (void)hipHostFree(h->sets[i].hint);
     }
+    for (uint32_t i = 0; i < bftsim::BATCH_EVS; ++i)
+        if (h->batch_ev[i]) (void)hipEventDestroy(h->batch_ev[i]);
     for (uint32_t i = 0; i < bftsim::MAX_CS; ++i)
         if (h->cs[i]) (void)hipStreamDestroy(h->cs[i]);
     for (uint32_t i = 0; i < bftsim::MAX_HS; ++i)
@@ -1013,7 +1022,10 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     if (!h || h->cap_inst == 0 || h->n_req == 0) return fail(h, BFTSIM_EINVAL, "bftsim_prepare not called");
     const uint64_t n = h->n_req;
     if (first + n > (1ull << 32)) return fail(h, BFTSIM_EINVAL, "instance ids must fit in 32 bits");
-    HIPCHECK(h, hipSetDevice(h->device));
+    {   // the device current already (the common case): hipGetDevice is a thread-local read, hipSetDevice is not
+        int d = -1;
+        if (hipGetDevice(&d) != hipSuccess || d != h->device) HIPCHECK(h, hipSetDevice(h->device));
+    }
     hipStream_t s = (hipStream_t)stream;
     if (h->h_trace) {
         if (h->d_trace) (void)hipFree(h->d_trace);
@@ -1066,7 +1078,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         if (!h->cs[h->cur_cs]) HIPCHECK(h, hipStreamCreateWithFlags(&h->cs[h->cur_cs], hipStreamNonBlocking));
         hipStream_t ls = h->cs[h->cur_cs];
         HIPCHECK(h, hipStreamWaitEvent(ls, r.entry, 0));
-        if (r.busy) HIPCHECK(h, hipStreamWaitEvent(ls, r.done, 0));
+        if (r.busy) HIPCHECK(h, hipStreamWaitEvent(ls, r.batch_done ? r.batch_done : r.done, 0));
         s = ls;
         h->d_hist = r.hist; h->d_rcs = r.rcs; h->d_backlog = r.backlog; h->d_resume = r.resume; h->d_save = r.save;
         h->d_resume_q = r.resume_q;
@@ -1161,7 +1173,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
                 h->batch_p = p;
                 h->batch_spec = hspec;
             }
-            h->pend[h->n_pend++] = {h->cur_set, (h->ring_head - 1) % bftsim::RING, (uint32_t)first};
+            h->pend[h->n_pend++] = {h->cur_set, (h->ring_head - 1) % bftsim::RING, (uint32_t)first, h->cur_cs};
             if (h->n_pend >= h->hash_batch) if (int rc = flush_batch(h)) return rc;
         } else {
             // one launch's hash pass: on a hash stream (pipelined) or the launch stream; chunks of K heights
@@ -1186,12 +1198,14 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
             HIPCHECK(h, hipEventRecord(ev.h1, t));
             if (pipe) {
                 HIPCHECK(h, hipEventRecord(h->sets[h->cur_set].done, t));
+                h->sets[h->cur_set].batch_done = nullptr;
                 h->sets[h->cur_set].busy = true;
             }
         }
     }
     if (pipe && p.need_seed) {                          // no hash pass: the set is free once this launch is done
         HIPCHECK(h, hipEventRecord(h->sets[h->cur_set].done, s));
+        h->sets[h->cur_set].batch_done = nullptr;
         h->sets[h->cur_set].busy = true;
     }
     h->last_n = n;
@@ -1209,14 +1223,35 @@ static int flush_batch(bftsim* h) {
     hipStream_t t = h->hstr[h->cur_hs];
     bft::ChainSets cs{};
     cs.count = h->n_pend;
+    // a launch stream runs its launches in order, so the last pending launch of each launch stream stands for the
+    // others: per stream one wait on its sx (recorded after the consensus kernels and, unless the lane chains encode
+    // them, the suffix rows) instead of one wait per launch
+    int32_t last_on[bftsim::MAX_CS];
+    for (uint32_t k = 0; k < bftsim::MAX_CS; ++k) last_on[k] = -1;
+    for (uint32_t i = 0; i < h->n_pend; ++i) last_on[h->pend[i].cs] = (int32_t)i;
+    if (!h->batch_spec) {
+        for (uint32_t k = 0; k < bftsim::MAX_CS; ++k)
+            if (last_on[k] >= 0) HIPCHECK(h, hipStreamWaitEvent(t, h->ring[h->pend[last_on[k]].ev].sx, 0));
+    } else {
+        // predicted chains need only their sets free, not the launch streams' earlier kernels: the caller's work
+        // before the last pending launch (its entry event: the caller's stream is in order) and each distinct
+        // previous hash pass of the sets
+        HIPCHECK(h, hipStreamWaitEvent(t, h->sets[h->pend[h->n_pend - 1].set].entry, 0));
+        hipEvent_t seen[bftsim::MAX_BATCH];
+        uint32_t ns = 0;
+        for (uint32_t i = 0; i < h->n_pend; ++i) {
+            const bftsim::RowSet& r = h->sets[h->pend[i].set];
+            if (!r.busy) continue;
+            const hipEvent_t e = r.batch_done ? r.batch_done : r.done;
+            bool dup = false;
+            for (uint32_t j = 0; j < ns; ++j) dup |= seen[j] == e;
+            if (dup) continue;
+            seen[ns++] = e;
+            HIPCHECK(h, hipStreamWaitEvent(t, e, 0));
+        }
+    }
     for (uint32_t i = 0; i < h->n_pend; ++i) {
         const bftsim::RowSet& r = h->sets[h->pend[i].set];
-        if (!h->batch_spec) {
-            HIPCHECK(h, hipStreamWaitEvent(t, h->ring[h->pend[i].ev].sx, 0));   // the launch's suffix rows
-        } else {                                       // the set is free: the caller's work before the launch,
-            HIPCHECK(h, hipStreamWaitEvent(t, r.entry, 0));   // the set's previous hash pass
-            if (r.busy) HIPCHECK(h, hipStreamWaitEvent(t, r.done, 0));
-        }
         cs.sfx[i] = r.sfx; cs.ch[i] = r.ch; cs.hash[i] = r.hash;
         cs.rec[i] = r.rec; cs.byz[i] = r.byz; cs.bad[i] = r.bad; cs.pred[i] = r.pred; cs.first[i] = h->pend[i].first;
     }
@@ -1233,7 +1268,8 @@ static int flush_batch(bftsim* h) {
         p.chain_mode = bft::CHAIN_PREDICTED;
         HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, chain_kind(h, p.n_instances, true), t, p));
         HIPCHECK(h, pmc_evict(h, t));
-        for (uint32_t i = 0; i < h->n_pend; ++i) HIPCHECK(h, hipStreamWaitEvent(t, h->ring[h->pend[i].ev].c1, 0));
+        for (uint32_t k = 0; k < bftsim::MAX_CS; ++k)   // every launch's consensus kernels (per launch stream)
+            if (last_on[k] >= 0) HIPCHECK(h, hipStreamWaitEvent(t, h->ring[h->pend[last_on[k]].ev].c1, 0));
         HIPCHECK(h, bft::launch_spec_verify(p.n_instances, cs, t, p));
         HIPCHECK(h, pmc_evict(h, t));
         p.chain_mode = bft::CHAIN_REPAIR;
@@ -1245,9 +1281,12 @@ static int flush_batch(bftsim* h) {
     HIPCHECK(h, pmc_evict(h, t));
     HIPCHECK(h, hipEventRecord(last.h1, t));
     last.has_hash = true;
+    hipEvent_t& bd = h->batch_ev[h->batch_ev_head++ % bftsim::BATCH_EVS];
+    if (!bd) HIPCHECK(h, hipEventCreateWithFlags(&bd, hipEventDisableTiming));
+    HIPCHECK(h, hipEventRecord(bd, t));
     for (uint32_t i = 0; i < h->n_pend; ++i) {
         bftsim::RowSet& r = h->sets[h->pend[i].set];
-        HIPCHECK(h, hipEventRecord(r.done, t));
+        r.batch_done = bd;
         r.busy = true;
     }
     h->n_pend = 0;
