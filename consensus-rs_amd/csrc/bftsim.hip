@@ -463,6 +463,9 @@ struct bftsim {
     // (BFTSIM_TESTING + BFTSIM_CHAIN_INLINE=0: the suffix rows)
     uint32_t chain_inline = 1;
     uint32_t chain_prio = 0;          // s_setprio of the chain waves (BFTSIM_TESTING + BFTSIM_CHAIN_PRIO)
+    // predicted chains (small shards, their latency the step's tail): above the FAST kernels' 2, with their suffix
+    // rows (2,048 per GPU: 1.08e9 at 0, 1.13e9-1.22e9 at 3; profiles/r06/ab_prio; BFTSIM_CHAIN_PRIO_SPEC)
+    uint32_t chain_prio_spec = 3;
     uint32_t fast_lds_pad = 0;        // extra LDS per FAST wave: fewer resident FAST waves (BFTSIM_TESTING + BFTSIM_FAST_LDS_PAD)
     bool seed_spec = true;            // little-endian seeds, N = 64: predicted blocks (BFTSIM_TESTING + BFTSIM_SEED_SPEC=0: off)
     int pipeline = 0;                 // number of row-table sets (0: no pipelining)
@@ -854,6 +857,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         };
         knob("BFTSIM_LAUNCH_STREAMS", h->n_cs, 1, bftsim::MAX_CS);
         knob("BFTSIM_CHAIN_GRID", h->chain_grid, 0, 1u << 20);
+        knob("BFTSIM_CHAIN_PRIO_SPEC", h->chain_prio_spec, 0, 3);
         knob("BFTSIM_CHAIN_INLINE", h->chain_inline, 0, 1);
         knob("BFTSIM_LAUNCH_STREAMS_SEEDED", h->n_cs_seeded, 1, bftsim::MAX_CS);
         knob("BFTSIM_HASH_STREAMS", h->n_hs, 1, bftsim::MAX_HS);   // A/B arms
@@ -1259,6 +1263,7 @@ static int flush_batch(bftsim* h) {
     bft::Params p = h->batch_p;
     HIPCHECK(h, hipEventRecord(last.h0, t));
     if (h->batch_spec) {
+        p.chain_prio = h->chain_prio_spec;
         // the predicted blocks' suffix rows and chains, which need nothing of the consensus kernels (one suffix
         // pass for the whole batch: per launch on a stream of their own they fell behind the launches); once
         // every launch's consensus kernel is done, the check of its recorded blocks against the predictions, and

@@ -443,7 +443,7 @@ __device__ inline void lane_chain(const Params& p, const ChainSets& cs, uint32_t
 // Persistent: at most p.chain_grid workgroups (one wave each), each taking 64 instances after another. A chain wave
 // runs its instances' 100 heights back to back, so a grid of every task at once held every SIMD slot for the whole
 // dispatch and the consensus kernels beside it got none (cfg3: a FAST kernel 0.40 -> 4.6 ms under a 12-launch chain
-// dispatch, profiles/r06/trace_k16); capped, the chain waves leave slots to them.
+// dispatch, profiles/r06/traces/r06n_timeline_k16.txt); capped, the chain waves leave slots to them.
 // register budget: a chain wave beside the FAST kernel's waves (4 per SIMD) on the same SIMD
 #ifndef BFT_LANE_WAVES_PER_SIMD
 #define BFT_LANE_WAVES_PER_SIMD 3
@@ -483,6 +483,7 @@ static hipError_t launch_lane(uint32_t tasks, const ChainSets& cs, hipStream_t s
 // predicted hash is kept only where its block and all of its ancestors were predicted right, so every hash is
 // the recorded block's by construction.
 __global__ __launch_bounds__(256) void bft_spec_byz_kernel(Params p, ChainSets cs) {
+    set_prio(p.chain_prio);                           // on the predicted chains' critical path
     __shared__ uint8_t perm[256 * 64];                // byz_mask64's permutation, per thread
     const uint32_t n = p.n_instances, bpl = (n + 255u) / 256u, k = blockIdx.x / bpl;
     const uint32_t il = (blockIdx.x % bpl) * 256u + threadIdx.x;
@@ -495,6 +496,7 @@ __device__ inline uint64_t spec_time(const Params& p, uint32_t tick) {
 }
 // thread per (launch, height, instance), consecutive threads = consecutive instances (the row layout)
 __global__ __launch_bounds__(256) void bft_spec_suffix_kernel(Params p, ChainSets cs) {
+    set_prio(p.chain_prio);                           // on the predicted chains' critical path
     const uint32_t n = p.n_instances, H = p.heights;
     const uint32_t bpl = (uint32_t)(((uint64_t)n * H + 255u) / 256u), k = blockIdx.x / bpl;
     const uint32_t t = (blockIdx.x % bpl) * 256u + threadIdx.x;   // n * H < 2^32 (bftsim.hip)
