@@ -18,6 +18,19 @@
 #pragma once
 #include "bft_common.h"
 
+// Invariant checks of the CPU emulator build (tests/emu, -DBFT_EMU_CHECKS): a violated invariant aborts the run.
+// They compile to nothing in the kernels.
+#if defined(BFT_EMU_CHECKS) && !defined(__HIP_DEVICE_COMPILE__)
+#include <cstdio>
+#include <cstdlib>
+#define BFT_EMU_CHECK(cond, what)                                                         \
+    do {                                                                                  \
+        if (!(cond)) { fprintf(stderr, "emu: invariant violated: %s\n", what); abort(); } \
+    } while (0)
+#else
+#define BFT_EMU_CHECK(cond, what) do { } while (0)
+#endif
+
 namespace bft {
 
 constexpr int REC_WORDS = 22;            // LDS words per published outbox record
@@ -521,6 +534,7 @@ struct Sim {
 
     BFT_FN uint32_t canon_seed(uint32_t x) {
         if (x == 0) return P.genesis_seed;
+        if constexpr (SEG_HASH) BFT_EMU_CHECK(!(canon_stale & (x == canon_h)), "canon_seed of a stale canonical tip");
         if (x == canon_h) return canon_tip_seed;
         check_window(x);
         return wv.gload(rec_row(x) + 3);
@@ -778,6 +792,8 @@ struct Sim {
     }
 
     BFT_FN void start_new_zero_round() {                                     // core.rs:441-470
+        // (SEG_HASH) the tip's seed is read below: its hash must not be pending (phase_hashes resolves it first)
+        if constexpr (SEG_HASH) BFT_EMU_CHECK(!seed_stale, "start_new_zero_round reads a stale tip seed");
         uint32_t last_height = last;
         h = last_height + 1;
         r = 0;
@@ -793,6 +809,7 @@ struct Sim {
     BFT_FN void start_new_round(uint32_t round) {                            // core.rs:474-551
         uint32_t last_height = last;
         if (last_height > h) return;
+        if constexpr (SEG_HASH) BFT_EMU_CHECK(!seed_stale, "start_new_round reads a stale tip seed");
         n_rcs = 0;
         if (!blk_valid(lock)) pp = BLK_NONE;
         prep = comm = M::zero();

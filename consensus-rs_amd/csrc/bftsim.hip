@@ -494,6 +494,10 @@ struct bftsim {
     uint32_t n_pend = 0;
     bft::Params batch_p{};            // the launch parameters of the pending batch (sizes, genesis, prio)
     bool batch_spec = false;          // the pending batch runs predicted chains
+    uint32_t batch_hs = 0;            // the pending batch's hash stream (chosen at its first launch)
+    // predicted suffix rows per launch at the launch, on the batch's hash stream (0: the whole batch's at the flush;
+    // BFTSIM_TESTING + BFTSIM_SPEC_EARLY)
+    uint32_t spec_early = 0;   // measured: 0.99e9-1.07e9 early vs 1.09e9-1.13e9 at the flush (profiles/r06/ab_spec_early)
     // per-launch kernel timing: a ring of event quadruples, read by bftsim_kernel_ms_sum
     static constexpr uint32_t RING = 64;
     struct LaunchEv { hipEvent_t c0, c1, h0, h1, sx; bool has_hash, pending; } ring[RING] = {};
@@ -858,6 +862,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         knob("BFTSIM_LAUNCH_STREAMS", h->n_cs, 1, bftsim::MAX_CS);
         knob("BFTSIM_CHAIN_GRID", h->chain_grid, 0, 1u << 20);
         knob("BFTSIM_CHAIN_PRIO_SPEC", h->chain_prio_spec, 0, 3);
+        knob("BFTSIM_SPEC_EARLY", h->spec_early, 0, 1);
         knob("BFTSIM_CHAIN_INLINE", h->chain_inline, 0, 1);
         knob("BFTSIM_LAUNCH_STREAMS_SEEDED", h->n_cs_seeded, 1, bftsim::MAX_CS);
         knob("BFTSIM_HASH_STREAMS", h->n_hs, 1, bftsim::MAX_HS);   // A/B arms
@@ -1176,6 +1181,24 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
             if (h->n_pend == 0) {
                 h->batch_p = p;
                 h->batch_spec = hspec;
+                h->cur_hs = (h->cur_hs + 1) % (hspec ? h->n_hs_spec : h->n_hs);   // the batch's hash stream
+                if (!h->hstr[h->cur_hs]) HIPCHECK(h, hipStreamCreateWithFlags(&h->hstr[h->cur_hs], hipStreamNonBlocking));
+                h->batch_hs = h->cur_hs;
+            }
+            if (hspec && h->spec_early) {
+                // this launch's predicted suffix rows now, on the batch's hash stream, once its set is free (the
+                // caller's earlier work, the set's last hash pass): at the flush only the chains are left
+                hipStream_t t = h->hstr[h->batch_hs];
+                HIPCHECK(h, hipStreamWaitEvent(t, r.entry, 0));
+                if (r.busy) HIPCHECK(h, hipStreamWaitEvent(t, r.batch_done ? r.batch_done : r.done, 0));
+                bft::ChainSets one{};
+                one.count = 1;
+                one.sfx[0] = r.sfx; one.byz[0] = r.byz; one.bad[0] = r.bad; one.pred[0] = r.pred;
+                one.first[0] = (uint32_t)first;
+                bft::Params ps = p;
+                ps.chain_prio = h->chain_prio_spec;
+                HIPCHECK(h, bft::launch_spec_suffix((uint32_t)n, one, t, ps));
+                HIPCHECK(h, pmc_evict(h, t));
             }
             h->pend[h->n_pend++] = {h->cur_set, (h->ring_head - 1) % bftsim::RING, (uint32_t)first, h->cur_cs};
             if (h->n_pend >= h->hash_batch) if (int rc = flush_batch(h)) return rc;
@@ -1222,9 +1245,7 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
 // the chains of the pending launches as one kernel on the next hash stream, after each launch's suffix rows
 static int flush_batch(bftsim* h) {
     if (h->n_pend == 0) return BFTSIM_OK;
-    h->cur_hs = (h->cur_hs + 1) % (h->batch_spec ? h->n_hs_spec : h->n_hs);
-    if (!h->hstr[h->cur_hs]) HIPCHECK(h, hipStreamCreateWithFlags(&h->hstr[h->cur_hs], hipStreamNonBlocking));
-    hipStream_t t = h->hstr[h->cur_hs];
+    hipStream_t t = h->hstr[h->batch_hs];           // chosen at the batch's first launch
     bft::ChainSets cs{};
     cs.count = h->n_pend;
     // a launch stream runs its launches in order, so the last pending launch of each launch stream stands for the
@@ -1236,7 +1257,7 @@ static int flush_batch(bftsim* h) {
     if (!h->batch_spec) {
         for (uint32_t k = 0; k < bftsim::MAX_CS; ++k)
             if (last_on[k] >= 0) HIPCHECK(h, hipStreamWaitEvent(t, h->ring[h->pend[last_on[k]].ev].sx, 0));
-    } else {
+    } else if (!h->spec_early) {
         // predicted chains need only their sets free, not the launch streams' earlier kernels: the caller's work
         // before the last pending launch (its entry event: the caller's stream is in order) and each distinct
         // previous hash pass of the sets
@@ -1268,8 +1289,10 @@ static int flush_batch(bftsim* h) {
         // pass for the whole batch: per launch on a stream of their own they fell behind the launches); once
         // every launch's consensus kernel is done, the check of its recorded blocks against the predictions, and
         // the chains again from the first height that differs
-        HIPCHECK(h, bft::launch_spec_suffix(p.n_instances, cs, t, p));
-        HIPCHECK(h, pmc_evict(h, t));
+        if (!h->spec_early) {
+            HIPCHECK(h, bft::launch_spec_suffix(p.n_instances, cs, t, p));
+            HIPCHECK(h, pmc_evict(h, t));
+        }
         p.chain_mode = bft::CHAIN_PREDICTED;
         HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, chain_kind(h, p.n_instances, true), t, p));
         HIPCHECK(h, pmc_evict(h, t));

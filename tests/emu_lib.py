@@ -25,7 +25,7 @@ def build():
         return
     # build to a private name and rename: concurrent test workers never load a half-written library
     tmp = f"{LIB}.{os.getpid()}.tmp"
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unknown-pragmas",
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unknown-pragmas", "-DBFT_EMU_CHECKS",
                            "-o", tmp, SRCS[0]])
     os.replace(tmp, LIB)
 

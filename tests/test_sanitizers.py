@@ -34,7 +34,7 @@ def _build():
         subprocess.check_call(["gcc", "-std=gnu11", "-mpopcnt", "-c", "-o", o, os.path.join(ROOT, "oracle", c)] + SAN)
         objs.append(o)
     tmp = f"{exe}.{os.getpid()}.tmp"
-    subprocess.check_call(["g++", "-std=c++17", "-Wno-unknown-pragmas", "-o", tmp, srcs[0]] + objs + SAN +
+    subprocess.check_call(["g++", "-std=c++17", "-Wno-unknown-pragmas", "-DBFT_EMU_CHECKS", "-o", tmp, srcs[0]] + objs + SAN +
                           ["-lpthread"])
     os.replace(tmp, exe)
     return exe
