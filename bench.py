@@ -101,7 +101,8 @@ def step_traffic(workload: str, batch: int):
     ks = json.load(open(files[-1])).get("kernels", {})
     names = ["bft_consensus_fast_kernel", "bft_consensus_resume_kernel"] if "bft_consensus_fast_kernel" in ks \
         else ["bft_consensus_kernel"]
-    names += ["bft_seed_chain_kernel", "bft_hash_suffix_kernel", "bft_hash_chain_kernel"]
+    names += ["bft_clear_kernel", "bft_seed_chain_kernel", "bft_hash_suffix_kernel", "bft_spec_byz_kernel",
+              "bft_spec_suffix_kernel", "bft_spec_verify_kernel", "bft_hash_chain_kernel"]
     parts, attributed = {}, True
     for k in names:
         e = ks.get(k)
@@ -509,7 +510,12 @@ def main():
             dom, ops, ms = "bft_hash_chain_kernel", h_ops, hms
         achieved = ops / (ms / 1e3) / 1e12
         peak = VALU_PEAK / 1e12
+        # the PMC summary of this exact line: cfg4 per validator count, cfg3 per shard size and seed byte order
         pmc_key = f"cfg4_n{cfg.n}" if wl == "cfg4" else wl
+        if wl == "cfg3" and cfg.seed_byte_order:
+            pmc_key = "cfg3le"
+        elif wl == "cfg3" and I != 16_384:
+            pmc_key = f"cfg3_{I}"
         traffic, traffic_src = pmc_traffic(pmc_key)
         algo_bytes = ALGO_BYTES_PER_VIEW * views_rank
         stp = step_traffic(pmc_key, args.hash_batch if pipelined else 1)
