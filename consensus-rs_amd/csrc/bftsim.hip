@@ -497,6 +497,7 @@ struct bftsim {
     uint32_t batch_hs = 0;            // the pending batch's hash stream (chosen at its first launch)
     // predicted suffix rows per launch at the launch, on the batch's hash stream (0: the whole batch's at the flush;
     // BFTSIM_TESTING + BFTSIM_SPEC_EARLY)
+    uint32_t rec_clear = 0;           // zero the record rows of FAST launches too (BFTSIM_TESTING + BFTSIM_REC_CLEAR)
     uint32_t spec_early = 0;   // measured: 0.99e9-1.07e9 early vs 1.09e9-1.13e9 at the flush (profiles/r06/ab_spec_early)
     // per-launch kernel timing: a ring of event quadruples, read by bftsim_kernel_ms_sum
     static constexpr uint32_t RING = 64;
@@ -863,6 +864,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         knob("BFTSIM_CHAIN_GRID", h->chain_grid, 0, 1u << 20);
         knob("BFTSIM_CHAIN_PRIO_SPEC", h->chain_prio_spec, 0, 3);
         knob("BFTSIM_SPEC_EARLY", h->spec_early, 0, 1);
+        knob("BFTSIM_REC_CLEAR", h->rec_clear, 0, 1);
         knob("BFTSIM_CHAIN_INLINE", h->chain_inline, 0, 1);
         knob("BFTSIM_LAUNCH_STREAMS_SEEDED", h->n_cs_seeded, 1, bftsim::MAX_CS);
         knob("BFTSIM_HASH_STREAMS", h->n_hs, 1, bftsim::MAX_HS);   // A/B arms
@@ -1108,9 +1110,15 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         ev.pending = false;
     }
     h->ring_head += 1;
-    // the record rows, the histogram and (FAST launches) the hand-over flags and queue, zeroed by one dispatch
-    hipLaunchKernelGGL(bft_clear_kernel, dim3(clear_blocks(n * h->hcap)), dim3(256), 0, s, (uint4*)h->d_rec,
-                       (uint64_t)n * h->hcap, h->d_hist, fast_launch ? h->d_resume : nullptr, (uint32_t)n,
+    // the histogram and (FAST launches) the hand-over flags and queue zeroed by one dispatch; the record rows too,
+    // except for FAST launches: the FAST and resume bodies read a row only once they have recorded it (canon_blk,
+    // canon_seed, refresh_tip_from_table: rows <= the canonical height), and every reader after the launch stops at
+    // the committed height (fetch, export, tips, chains, the predicted chains' check) -- 43 MB of writes per cfg3
+    // launch saved (BFTSIM_TESTING + BFTSIM_REC_CLEAR=1: cleared anyway)
+    const bool clear_rec = !fast_launch || h->rec_clear;
+    const uint64_t n_rec = clear_rec ? (uint64_t)n * h->hcap : 0;
+    hipLaunchKernelGGL(bft_clear_kernel, dim3(clear_blocks(n_rec > n ? n_rec : n)), dim3(256), 0, s, (uint4*)h->d_rec,
+                       n_rec, h->d_hist, fast_launch ? h->d_resume : nullptr, (uint32_t)n,
                        fast_launch ? h->d_resume_q : nullptr);
     HIPCHECK(h, hipGetLastError());
     if (h->d_backlog) HIPCHECK(h, hipMemsetAsync(h->d_backlog, 0, h->backlog_bytes, s));
