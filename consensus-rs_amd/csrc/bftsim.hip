@@ -498,7 +498,8 @@ struct bftsim {
     // predicted suffix rows per launch at the launch, on the batch's hash stream (0: the whole batch's at the flush;
     // BFTSIM_TESTING + BFTSIM_SPEC_EARLY)
     uint32_t rec_clear = 0;           // zero the record rows of FAST launches too (BFTSIM_TESTING + BFTSIM_REC_CLEAR)
-    uint32_t spec_early = 0;   // measured: 0.99e9-1.07e9 early vs 1.09e9-1.13e9 at the flush (profiles/r06/ab_spec_early)
+    uint32_t spec_early = 0;
+    uint32_t spec_final = 1;          // the flush of bftsim_sync as predicted pair chains (BFTSIM_TESTING + BFTSIM_SPEC_FINAL)   // measured: 0.99e9-1.07e9 early vs 1.09e9-1.13e9 at the flush (profiles/r06/ab_spec_early)
     // per-launch kernel timing: a ring of event quadruples, read by bftsim_kernel_ms_sum
     static constexpr uint32_t RING = 64;
     struct LaunchEv { hipEvent_t c0, c1, h0, h1, sx; bool has_hash, pending; } ring[RING] = {};
@@ -585,10 +586,10 @@ static void free_bufs(bftsim* h) {
     h->last_first = 0;
 }
 
-static int flush_batch(bftsim* h);
+static int flush_batch(bftsim* h, bool final = false);
 static int sync_all(bftsim* h) {
     HIPCHECK(h, hipSetDevice(h->device));
-    if (int rc = flush_batch(h)) return rc;
+    if (int rc = flush_batch(h, true)) return rc;
     HIPCHECK(h, hipStreamSynchronize(h->last_stream));
     for (uint32_t k = 0; k < bftsim::MAX_CS; ++k)
         if (h->cs[k]) HIPCHECK(h, hipStreamSynchronize(h->cs[k]));
@@ -864,6 +865,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         knob("BFTSIM_CHAIN_GRID", h->chain_grid, 0, 1u << 20);
         knob("BFTSIM_CHAIN_PRIO_SPEC", h->chain_prio_spec, 0, 3);
         knob("BFTSIM_SPEC_EARLY", h->spec_early, 0, 1);
+        knob("BFTSIM_SPEC_FINAL", h->spec_final, 0, 1);
         knob("BFTSIM_REC_CLEAR", h->rec_clear, 0, 1);
         knob("BFTSIM_CHAIN_INLINE", h->chain_inline, 0, 1);
         knob("BFTSIM_LAUNCH_STREAMS_SEEDED", h->n_cs_seeded, 1, bftsim::MAX_CS);
@@ -1251,9 +1253,15 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
 }
 
 // the chains of the pending launches as one kernel on the next hash stream, after each launch's suffix rows
-static int flush_batch(bftsim* h) {
+// `final`: the flush of bftsim_sync (the last launches of a burst), whose chains are the burst's tail
+static int flush_batch(bftsim* h, bool final) {
     if (h->n_pend == 0) return BFTSIM_OK;
     hipStream_t t = h->hstr[h->batch_hs];           // chosen at the batch's first launch
+    // A final batch of recorded chains (a large shard's lane chains, which start once the last launch's consensus
+    // kernel is done and take ~2 ms) runs as predicted lane-pair chains instead: they start now, beside the launches'
+    // consensus kernels, and only the check and the repairs are left behind them
+    const bool conv = final && !h->batch_spec && h->spec_final && h->sets[h->pend[0].set].byz != nullptr;
+    const bool spec = h->batch_spec || conv;
     bft::ChainSets cs{};
     cs.count = h->n_pend;
     // a launch stream runs its launches in order, so the last pending launch of each launch stream stands for the
@@ -1262,10 +1270,10 @@ static int flush_batch(bftsim* h) {
     int32_t last_on[bftsim::MAX_CS];
     for (uint32_t k = 0; k < bftsim::MAX_CS; ++k) last_on[k] = -1;
     for (uint32_t i = 0; i < h->n_pend; ++i) last_on[h->pend[i].cs] = (int32_t)i;
-    if (!h->batch_spec) {
+    if (!spec) {
         for (uint32_t k = 0; k < bftsim::MAX_CS; ++k)
             if (last_on[k] >= 0) HIPCHECK(h, hipStreamWaitEvent(t, h->ring[h->pend[last_on[k]].ev].sx, 0));
-    } else if (!h->spec_early) {
+    } else if (!h->spec_early || conv) {
         // predicted chains need only their sets free, not the launch streams' earlier kernels: the caller's work
         // before the last pending launch (its entry event: the caller's stream is in order) and each distinct
         // previous hash pass of the sets
@@ -1291,25 +1299,26 @@ static int flush_batch(bftsim* h) {
     bftsim::LaunchEv& last = h->ring[h->pend[h->n_pend - 1].ev];
     bft::Params p = h->batch_p;
     HIPCHECK(h, hipEventRecord(last.h0, t));
-    if (h->batch_spec) {
+    if (spec) {
         p.chain_prio = h->chain_prio_spec;
+        const uint32_t kind = conv ? bft::CHAIN_KERNEL_PAIR : chain_kind(h, p.n_instances, true);
         // the predicted blocks' suffix rows and chains, which need nothing of the consensus kernels (one suffix
         // pass for the whole batch: per launch on a stream of their own they fell behind the launches); once
         // every launch's consensus kernel is done, the check of its recorded blocks against the predictions, and
         // the chains again from the first height that differs
-        if (!h->spec_early) {
+        if (!h->spec_early || conv) {
             HIPCHECK(h, bft::launch_spec_suffix(p.n_instances, cs, t, p));
             HIPCHECK(h, pmc_evict(h, t));
         }
         p.chain_mode = bft::CHAIN_PREDICTED;
-        HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, chain_kind(h, p.n_instances, true), t, p));
+        HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, kind, t, p));
         HIPCHECK(h, pmc_evict(h, t));
         for (uint32_t k = 0; k < bftsim::MAX_CS; ++k)   // every launch's consensus kernels (per launch stream)
             if (last_on[k] >= 0) HIPCHECK(h, hipStreamWaitEvent(t, h->ring[h->pend[last_on[k]].ev].c1, 0));
         HIPCHECK(h, bft::launch_spec_verify(p.n_instances, cs, t, p));
         HIPCHECK(h, pmc_evict(h, t));
         p.chain_mode = bft::CHAIN_REPAIR;
-        HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, chain_kind(h, p.n_instances, true), t, p));
+        HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, kind, t, p));
     } else {
         p.chain_mode = bft::CHAIN_RECORDED;
         HIPCHECK(h, bft::launch_hash_chain_batch(p.n_instances, cs, chain_kind(h, p.n_instances, false), t, p));
