@@ -111,13 +111,13 @@ def _timed_run(cfg, first, n, launches=25):
 
 def test_timed_mode_full_size():
     """The exact configuration of the headline number: cfg3 at 16,384 instances on one GPU with bench.py's
-    pipeline depth and hash batch (16 x 8, lane-per-instance chains), 25 launches of the same instances; every
+    pipeline depth and hash batch (32 x 8, lane-per-instance chains), 25 launches of the same instances; every
     instance against the oracle."""
     from bftsim.configs import INSTANCES
     cfg = cfg3()
     n = INSTANCES["cfg3"]
     got, st, (depth, batch) = _timed_run(cfg, 0, n)
-    assert (depth, batch) == (16, 8)
+    assert (depth, batch) == (32, 8)
     ref = O.run(cfg, 0, n, threads=16)
     assert_same(ref, got, f"cfg3 {n} depth {depth} batch {batch} x25")
     assert st["views"] == int(ref["views"].sum()) == n * 100
