@@ -136,12 +136,10 @@ INSTANCES = {"cfg1": 1, "cfg2": 65_536, "cfg3": 16_384, "cfg4": 16_384, "cfg5": 
 
 def timed_pipeline(instances_per_gpu: int):
     """(pipeline depth, hash batch) that bench.py times a launch size with (bftsim_set_pipeline /
-    bftsim_set_hash_batch): from 12,288 instances per GPU, where the chains run a lane per instance,
-    a ring of 32 row-table sets (no launch of the 5 warmup + 20 timed waits for a set to come back from its chain
-    batch) with the chains of 8 launches per kernel; below, where the chains run on
-    predicted blocks from launch time on, 32 sets (no launch of the 5 warmup + 20 timed waits for a
-    set) with chain batches of 8. tests/test_gpu_pipeline.py runs exactly these settings at full
-    size."""
+    bftsim_set_hash_batch): a ring of 32 row-table sets, so that no launch of the 5 warmup + 20 timed ones waits for a
+    set to come back from its chain batch, with the chains of 8 launches per kernel -- a lane per instance from 8,192
+    instances per launch, lane pairs on the predicted blocks below (§4h). tests/test_gpu_pipeline.py
+    runs exactly these settings at full size (`instances_per_gpu` kept for the shape of the call)."""
     return (32, 8)
 
 

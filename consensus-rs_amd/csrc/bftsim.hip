@@ -454,7 +454,7 @@ struct bftsim {
     uint64_t chain_wave_max = 0;
     // one lane per instance from this many instances per launch (kern_fast.hip bft_hash_chain_lane_kernel: fewer
     // instructions per header, longer chains; BFTSIM_TESTING + BFTSIM_CHAIN_LANE_MIN overrides)
-    uint64_t chain_lane_min = 12288;
+    uint64_t chain_lane_min = 8192;   // 8,192: lanes 1.62e9 vs predicted pairs 1.55e9; 4,096: 1.12e9 vs 1.47e9 (r06/ab_mid)
     // persistent lane-chain waves per dispatch, 0: a wave per 64 instances (BFTSIM_TESTING + BFTSIM_CHAIN_GRID; an A/B
     // arm: capping the chain waves so that the consensus kernels keep SIMD slots measured the same or slower)
     uint32_t chain_grid = 0;
@@ -483,7 +483,7 @@ struct bftsim {
     // batches of a burst of launches run side by side
     // on for launches of fewer than hash_spec_max instances: a small shard is bound by the latency of its chains,
     // a large one by the chip's issue, which the checks only add to (profiles/r06/ab_spec)
-    uint64_t hash_spec_max = 12288;
+    uint64_t hash_spec_max = 8192;
     uint32_t n_hs_spec = 3;
     struct Pending { uint32_t set, ev, first, cs; } pend[MAX_BATCH];   // cs: the launch stream it ran on
     // one event per chain batch (flush_batch) instead of one per set: a ring, re-recorded after BATCH_EVS batches (a set

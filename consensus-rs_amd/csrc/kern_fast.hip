@@ -333,7 +333,7 @@ __device__ inline void keccak_f1600_lane(uint32_t L[25], uint32_t H[25]) {
 }
 #endif
 
-// Large shards (>= 12,288 instances per launch, bftsim.hip chain_lane_min): a LANE per instance. The whole state in
+// Large shards (>= 8,192 instances per launch, bftsim.hip chain_lane_min): a LANE per instance. The whole state in
 // one lane: ~180 VALU per round instead of 2 x 118 for a lane pair, i.e. ~24 % fewer instructions per header for
 // ~1.5x the chain latency, which a large shard's throughput-bound pipeline hides (cfg3 at 16,384: 1.70e9 with lane
 // pairs, 1.82e9-1.85e9 with lanes in batches of 12; profiles/r06/ab_lane).

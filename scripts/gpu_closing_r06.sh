@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-6 closing measurement passes (through gpurun), one group of workloads per call so each call stays well
-# inside gpurun's limit:  bash scripts/gpu_closing_r06.sh A|B|C|D
+# inside gpurun's limit:  bash scripts/gpu_closing_r06.sh A|B|C|D|E
+#   E: the shard curve (2,048 .. 16,384 instances per GPU) of the strong-scaling workload
 #   A: the whole -m gpu suite, smoke(), cfg3 (the headline, 20 steps after 5 warmup) and its 2,048-instance shard
 #   B: cfg5 (one 10,000-height step), cfg2, drop64
 #   C: cfg4 N = 256 and N = 128, little-endian cfg3
@@ -29,6 +30,14 @@ C)
   STEPS=5 WARMUP=1 PSTEPS=1 PWARMUP=0 NAME=r06/cfg4_n256 bash scripts/gpu_profile.sh cfg4 --n 256 || exit 1
   STEPS=5 WARMUP=1 PSTEPS=1 PWARMUP=0 NAME=r06/cfg4_n128 bash scripts/gpu_profile.sh cfg4 --n 128 || exit 1
   STEPS=20 WARMUP=5 NAME=r06/cfg3le bash scripts/gpu_profile.sh cfg3 --seed-order le || exit 1
+  ;;
+E)
+  # the shard curve of the strong-scaling workload: instances per GPU 2,048 .. 16,384, twice each
+  mkdir -p $O/curve
+  for rep in 1 2; do for n in 2048 4096 8192 16384; do
+    timeout -k 10 300 python bench.py --no-cpu --instances $n > $O/curve/n${n}_$rep.json 2> $O/curve/n${n}_$rep.err || { tail -5 $O/curve/n${n}_$rep.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/curve/n${n}_$rep.json')); print('$n', '%.4g' % d['value'], d['config']['host_enqueue_ms'])"
+  done; done
   ;;
 D)
   mkdir -p $O/lines
