@@ -499,7 +499,9 @@ struct bftsim {
     // BFTSIM_TESTING + BFTSIM_SPEC_EARLY)
     uint32_t rec_clear = 0;           // zero the record rows of FAST launches too (BFTSIM_TESTING + BFTSIM_REC_CLEAR)
     uint32_t spec_early = 0;
-    uint32_t spec_final = 1;          // the flush of bftsim_sync as predicted pair chains (BFTSIM_TESTING + BFTSIM_SPEC_FINAL)   // measured: 0.99e9-1.07e9 early vs 1.09e9-1.13e9 at the flush (profiles/r06/ab_spec_early)
+    uint32_t spec_final = 1;
+    uint32_t spec_first = 0;          // the first batch after a sync as predicted pair chains too (BFTSIM_SPEC_FIRST)
+    bool synced = true, batch_after_sync = false;          // the flush of bftsim_sync as predicted pair chains (BFTSIM_TESTING + BFTSIM_SPEC_FINAL)   // measured: 0.99e9-1.07e9 early vs 1.09e9-1.13e9 at the flush (profiles/r06/ab_spec_early)
     // per-launch kernel timing: a ring of event quadruples, read by bftsim_kernel_ms_sum
     static constexpr uint32_t RING = 64;
     struct LaunchEv { hipEvent_t c0, c1, h0, h1, sx; bool has_hash, pending; } ring[RING] = {};
@@ -590,6 +592,7 @@ static int flush_batch(bftsim* h, bool final = false);
 static int sync_all(bftsim* h) {
     HIPCHECK(h, hipSetDevice(h->device));
     if (int rc = flush_batch(h, true)) return rc;
+    h->synced = true;
     HIPCHECK(h, hipStreamSynchronize(h->last_stream));
     for (uint32_t k = 0; k < bftsim::MAX_CS; ++k)
         if (h->cs[k]) HIPCHECK(h, hipStreamSynchronize(h->cs[k]));
@@ -866,6 +869,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         knob("BFTSIM_CHAIN_PRIO_SPEC", h->chain_prio_spec, 0, 3);
         knob("BFTSIM_SPEC_EARLY", h->spec_early, 0, 1);
         knob("BFTSIM_SPEC_FINAL", h->spec_final, 0, 1);
+        knob("BFTSIM_SPEC_FIRST", h->spec_first, 0, 1);
         knob("BFTSIM_REC_CLEAR", h->rec_clear, 0, 1);
         knob("BFTSIM_CHAIN_INLINE", h->chain_inline, 0, 1);
         knob("BFTSIM_LAUNCH_STREAMS_SEEDED", h->n_cs_seeded, 1, bftsim::MAX_CS);
@@ -1191,6 +1195,8 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
             if (h->n_pend == 0) {
                 h->batch_p = p;
                 h->batch_spec = hspec;
+                h->batch_after_sync = h->synced;
+                h->synced = false;
                 h->cur_hs = (h->cur_hs + 1) % (hspec ? h->n_hs_spec : h->n_hs);   // the batch's hash stream
                 if (!h->hstr[h->cur_hs]) HIPCHECK(h, hipStreamCreateWithFlags(&h->hstr[h->cur_hs], hipStreamNonBlocking));
                 h->batch_hs = h->cur_hs;
@@ -1260,7 +1266,8 @@ static int flush_batch(bftsim* h, bool final) {
     // A final batch of recorded chains (a large shard's lane chains, which start once the last launch's consensus
     // kernel is done and take ~2 ms) runs as predicted lane-pair chains instead: they start now, beside the launches'
     // consensus kernels, and only the check and the repairs are left behind them
-    const bool conv = final && !h->batch_spec && h->spec_final && h->sets[h->pend[0].set].byz != nullptr;
+    const bool first = h->batch_after_sync && h->spec_first;   // the burst's first batch (A/B arm)
+    const bool conv = ((final && h->spec_final) || first) && !h->batch_spec && h->sets[h->pend[0].set].byz != nullptr;
     const bool spec = h->batch_spec || conv;
     bft::ChainSets cs{};
     cs.count = h->n_pend;
