@@ -831,6 +831,39 @@ BFT_FN void lane_block_hash(uint8_t* buf, const uint32_t prev[8], const uint8_t*
     for (int i = 0; i < 4; ++i) { out[2 * i] = (uint32_t)a[i]; out[2 * i + 1] = (uint32_t)(a[i] >> 32); }
 }
 
+// header_prefix_perm's words in registers (the lane chain kernel: no per-lane LDS buffer, so more chain waves fit
+// a CU): word wi is a select over the words it can be at that step. Field i starts at byte 4 + 4i .. 4 + 8i (each
+// hash byte is 1 or 2 bytes), so step i writes one of the words (1 + i) / 2 .. i and the last partial word is one
+// of 4 .. 8; the words past it stay 0. pw: the PFX_WORDS words as 2 * PFX_WORDS dwords (low first).
+BFT_FN uint32_t header_prefix_regs(const uint32_t prev[8], const PfxSel* tbl, uint32_t pw[2 * PFX_WORDS]) {
+    uint64_t wv[PFX_WORDS];
+#pragma unroll
+    for (uint32_t k = 0; k < PFX_WORDS; ++k) wv[k] = 0;
+    uint64_t acc = 0x2000dc9dull;                     // array(13); prev_hash: array16(32)
+    uint32_t fill = 4, wi = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+        const uint32_t w = prev[i];
+        const uint32_t idx = ((((w >> 7) & 0x01010101u) * 0x10204080u) >> 28);   // the four high bits
+        const PfxSel sel = tbl[idx];
+        const uint64_t v = (uint64_t)perm_bytes(0xccccccccu, w, sel.lo) | ((uint64_t)perm_bytes(0xccccccccu, w, sel.hi) << 32);
+        const uint32_t n = 4u + (uint32_t)__builtin_popcount(idx);
+        const uint32_t sh = 8u * fill, nf = fill + n;
+        const uint64_t lo = acc | (v << sh);
+#pragma unroll
+        for (uint32_t k = (1u + i) / 2u; k <= i; ++k) wv[k] = wi == k ? lo : wv[k];
+        const bool full = nf >= 8u;
+        acc = full ? (sh ? v >> (64u - sh) : 0ull) : lo;
+        wi += full ? 1u : 0u;
+        fill = full ? nf - 8u : nf;
+    }
+#pragma unroll
+    for (uint32_t k = 4; k < PFX_WORDS; ++k) wv[k] = wi == k ? acc : wv[k];
+#pragma unroll
+    for (uint32_t k = 0; k < PFX_WORDS; ++k) { pw[2 * k] = (uint32_t)wv[k]; pw[2 * k + 1] = (uint32_t)(wv[k] >> 32); }
+    return 8u * wi + fill;
+}
+
 #if !defined(__HIP_DEVICE_COMPILE__)
 // The same hash through the two-kernel block-hash pass's splice (host: the CPU emulator's post-pass).
 // sfx: the height's suffix row (SFX_DWORDS dwords, header_suffix).
@@ -844,6 +877,9 @@ inline void spliced_block_hash(const uint32_t* sfx, const uint32_t prev[8], uint
     const uint32_t lp = header_prefix_perm(pfx, prev, tbl);
     if (header_prefix(ref, prev) != lp) return;      // leaves `out` unset: the checks fail loudly
     for (uint32_t i = 0; i < PFX_WORDS; ++i) if (ref[i] != pfx[i]) return;
+    uint32_t pr[2 * PFX_WORDS];                       // the register form of the lane chain kernel
+    if (header_prefix_regs(prev, tbl, pr) != lp) return;
+    for (uint32_t i = 0; i < PFX_WORDS; ++i) if (pr[2 * i] != (uint32_t)ref[i] || pr[2 * i + 1] != (uint32_t)(ref[i] >> 32)) return;
     uint32_t pw[2 * PFX_WORDS];
     for (uint32_t i = 0; i < PFX_WORDS; ++i) { pw[2 * i] = (uint32_t)pfx[i]; pw[2 * i + 1] = (uint32_t)(pfx[i] >> 32); }
     const uint32_t c = 72u - lp, nb = splice_blocks(lp, sfx[SFX_LEN_DW]);
@@ -863,16 +899,19 @@ inline void spliced_block_hash(const uint32_t* sfx, const uint32_t prev[8], uint
 // ---- little-endian seeds, N = 64: the canonical schedule's blocks, predicted ----
 // The Byzantine validators of an instance of 64 (SPEC.md §5: partial Fisher-Yates; `perm`: 64 bytes of
 // scratch), as Fast64::init_byzantine draws them.
+// STRIDE: byte i of `perm` at (i / 4) * 4 * STRIDE + i % 4 (STRIDE 64: a lane's column of a [dword][lane] LDS array)
+template <uint32_t STRIDE = 1>
 BFT_FN uint64_t byz_mask64(uint64_t seed, uint32_t inst, uint32_t f, uint8_t* perm) {
-    for (uint32_t i = 0; i < 64u; ++i) perm[i] = (uint8_t)i;
+    auto at = [&](uint32_t i) -> uint8_t& { return perm[(i >> 2) * 4u * STRIDE + (i & 3u)]; };
+    for (uint32_t i = 0; i < 64u; ++i) at(i) = (uint8_t)i;
     uint64_t mask = 0;
     if (f > 64u) f = 64u;
     for (uint32_t i = 0; i < f; ++i) {
         uint32_t w[4];
         philox(seed, inst, i, 0, DOM_BYZ, w);
         const uint32_t j = i + w[0] % (64u - i);
-        const uint8_t t = perm[i]; perm[i] = perm[j]; perm[j] = t;
-        mask |= 1ull << perm[i];
+        const uint8_t t = at(i); at(i) = at(j); at(j) = t;
+        mask |= 1ull << at(i);
     }
     return mask;
 }

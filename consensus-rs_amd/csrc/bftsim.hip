@@ -466,6 +466,9 @@ struct bftsim {
     // predicted chains (small shards, their latency the step's tail): above the FAST kernels' 2, with their suffix
     // rows (2,048 per GPU: 1.08e9 at 0, 1.13e9-1.22e9 at 3; profiles/r06/ab_prio; BFTSIM_CHAIN_PRIO_SPEC)
     uint32_t chain_prio_spec = 3;
+    // predicted LANE chains (large shards: throughput, not latency) below the FAST kernels: 2.06e9-2.10e9 at 0 or 1
+    // against 1.80e9-1.93e9 at 3 (cfg3; profiles/r06/ab_spec_lane; BFTSIM_CHAIN_PRIO_SPEC_LANE)
+    uint32_t chain_prio_spec_lane = 0;
     uint32_t fast_lds_pad = 0;        // extra LDS per FAST wave: fewer resident FAST waves (BFTSIM_TESTING + BFTSIM_FAST_LDS_PAD)
     bool seed_spec = true;            // little-endian seeds, N = 64: predicted blocks (BFTSIM_TESTING + BFTSIM_SEED_SPEC=0: off)
     int pipeline = 0;                 // number of row-table sets (0: no pipelining)
@@ -481,9 +484,11 @@ struct bftsim {
     // big-endian seeds, N = 64, pipelined: the chains of a batch run on predicted blocks from launch time on
     // (BFTSIM_TESTING + BFTSIM_HASH_SPEC=0: off), over up to n_hs_spec hash streams so that the
     // batches of a burst of launches run side by side
-    // on for launches of fewer than hash_spec_max instances: a small shard is bound by the latency of its chains,
-    // a large one by the chip's issue, which the checks only add to (profiles/r06/ab_spec)
-    uint64_t hash_spec_max = 8192;
+    // on at every size: a small shard's chains (lane pairs) are bound by their latency, which they start ahead
+    // of; a large shard's (lanes, each predicting and encoding its blocks itself) fill the issue slots the consensus
+    // kernels leave from the first launch on (cfg3: 2.06e9-2.10e9 against 1.94e9-1.98e9 recorded;
+    // profiles/r06/ab_spec_lane). BFTSIM_TESTING + BFTSIM_HASH_SPEC=0: recorded chains at every size
+    uint64_t hash_spec_max = ~0ull;
     uint32_t n_hs_spec = 3;
     struct Pending { uint32_t set, ev, first, cs; } pend[MAX_BATCH];   // cs: the launch stream it ran on
     // one event per chain batch (flush_batch) instead of one per set: a ring, re-recorded after BATCH_EVS batches (a set
@@ -497,8 +502,12 @@ struct bftsim {
     uint32_t batch_hs = 0;            // the pending batch's hash stream (chosen at its first launch)
     // predicted suffix rows per launch at the launch, on the batch's hash stream (0: the whole batch's at the flush;
     // BFTSIM_TESTING + BFTSIM_SPEC_EARLY)
-    uint32_t rec_clear = 0;           // zero the record rows of FAST launches too (BFTSIM_TESTING + BFTSIM_REC_CLEAR)
     uint32_t spec_early = 0;
+    uint32_t rec_clear = 0;           // zero the record rows of FAST launches too (BFTSIM_TESTING + BFTSIM_REC_CLEAR)
+    uint32_t diag_no_chain = 0;       // diagnostic: flush_batch enqueues no chain kernels (wrong hashes)
+    uint32_t conv_stream = 0;         // a converted final batch on a hash stream of its own (A/B: BFTSIM_CONV_STREAM;
+                                      // 1.70e9-1.74e9 against 1.82e9-1.85e9 on the batch's, profiles/r06/ab_conv_stream)
+    uint32_t chain_on_launch = 0;     // the chain batches on the last launch's stream (BFTSIM_CHAIN_ON_LAUNCH)
     uint32_t spec_final = 1;
     uint32_t spec_first = 0;          // the first batch after a sync as predicted pair chains too (BFTSIM_SPEC_FIRST)
     bool synced = true, batch_after_sync = false;          // the flush of bftsim_sync as predicted pair chains (BFTSIM_TESTING + BFTSIM_SPEC_FINAL)   // measured: 0.99e9-1.07e9 early vs 1.09e9-1.13e9 at the flush (profiles/r06/ab_spec_early)
@@ -867,10 +876,14 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         knob("BFTSIM_LAUNCH_STREAMS", h->n_cs, 1, bftsim::MAX_CS);
         knob("BFTSIM_CHAIN_GRID", h->chain_grid, 0, 1u << 20);
         knob("BFTSIM_CHAIN_PRIO_SPEC", h->chain_prio_spec, 0, 3);
+        knob("BFTSIM_CHAIN_PRIO_SPEC_LANE", h->chain_prio_spec_lane, 0, 3);
         knob("BFTSIM_SPEC_EARLY", h->spec_early, 0, 1);
         knob("BFTSIM_SPEC_FINAL", h->spec_final, 0, 1);
         knob("BFTSIM_SPEC_FIRST", h->spec_first, 0, 1);
         knob("BFTSIM_REC_CLEAR", h->rec_clear, 0, 1);
+        knob("BFTSIM_DIAG_NO_CHAIN", h->diag_no_chain, 0, 1);
+        knob("BFTSIM_CONV_STREAM", h->conv_stream, 0, 1);
+        knob("BFTSIM_CHAIN_ON_LAUNCH", h->chain_on_launch, 0, 1);
         knob("BFTSIM_CHAIN_INLINE", h->chain_inline, 0, 1);
         knob("BFTSIM_LAUNCH_STREAMS_SEEDED", h->n_cs_seeded, 1, bftsim::MAX_CS);
         knob("BFTSIM_HASH_STREAMS", h->n_hs, 1, bftsim::MAX_HS);   // A/B arms
@@ -1269,6 +1282,13 @@ static int flush_batch(bftsim* h, bool final) {
     const bool first = h->batch_after_sync && h->spec_first;   // the burst's first batch (A/B arm)
     const bool conv = ((final && h->spec_final) || first) && !h->batch_spec && h->sets[h->pend[0].set].byz != nullptr;
     const bool spec = h->batch_spec || conv;
+    if (h->chain_on_launch) t = h->cs[h->pend[h->n_pend - 1].cs];   // A/B: behind the launches, no overlap
+    else if (conv && h->conv_stream && h->n_hs < bftsim::MAX_HS) {
+        // on a hash stream of its own: on the batch's (recorded chains' rotation) it would start only behind the
+        // recorded chains of an earlier batch there, ~9 ms at 16,384 (profiles/r06/traces/r06af_timeline_t16k.txt)
+        if (!h->hstr[h->n_hs]) HIPCHECK(h, hipStreamCreateWithFlags(&h->hstr[h->n_hs], hipStreamNonBlocking));
+        t = h->hstr[h->n_hs];
+    }
     bft::ChainSets cs{};
     cs.count = h->n_pend;
     // a launch stream runs its launches in order, so the last pending launch of each launch stream stands for the
@@ -1306,14 +1326,20 @@ static int flush_batch(bftsim* h, bool final) {
     bftsim::LaunchEv& last = h->ring[h->pend[h->n_pend - 1].ev];
     bft::Params p = h->batch_p;
     HIPCHECK(h, hipEventRecord(last.h0, t));
-    if (spec) {
-        p.chain_prio = h->chain_prio_spec;
-        const uint32_t kind = conv ? bft::CHAIN_KERNEL_PAIR : chain_kind(h, p.n_instances, true);
+    if (h->diag_no_chain) {
+        // diagnostic (BFTSIM_TESTING + BFTSIM_DIAG_NO_CHAIN=1): no chain kernels, so no block hashes; the consensus
+        // kernels' pace alone
+    } else if (spec) {
+        // a converted final batch on lane pairs (its chains are the burst's tail: latency); the burst's first batch
+        // (spec_first) has the whole burst to finish in, so it keeps the large shard's lanes (throughput)
+        const uint32_t kind = conv && !(first && !final) ? bft::CHAIN_KERNEL_PAIR : chain_kind(h, p.n_instances, true);
+        p.chain_prio = kind == bft::CHAIN_KERNEL_LANE ? h->chain_prio_spec_lane : h->chain_prio_spec;
         // the predicted blocks' suffix rows and chains, which need nothing of the consensus kernels (one suffix
         // pass for the whole batch: per launch on a stream of their own they fell behind the launches); once
         // every launch's consensus kernel is done, the check of its recorded blocks against the predictions, and
         // the chains again from the first height that differs
-        if (!h->spec_early || conv) {
+        // (inline lane chains predict, mask and encode each block themselves: no suffix pass)
+        if ((!h->spec_early || conv) && !(kind == bft::CHAIN_KERNEL_LANE && h->chain_inline)) {
             HIPCHECK(h, bft::launch_spec_suffix(p.n_instances, cs, t, p));
             HIPCHECK(h, pmc_evict(h, t));
         }

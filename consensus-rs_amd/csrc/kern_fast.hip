@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void bft_hash_suffix_loop_kernel(Params p) {
 #endif
 constexpr uint32_t CHAIN_SB = BFT_CHAIN_COMPACT ? 80u : SFX_BUF;        // splice buffer dwords per pair
 constexpr uint32_t CHAIN_SB_ZERO = SFX_PAD + SFX_BODY_DW;              // a zero dword (compact: reads past it clamp here)
-constexpr uint32_t CHAIN_PB_SLOTS = BFT_CHAIN_COMPACT ? 32u : 64u;      // prefix buffers per block
+[[maybe_unused]] constexpr uint32_t CHAIN_PB_SLOTS = BFT_CHAIN_COMPACT ? 32u : 64u;      // prefix buffers per block
 static_assert(CHAIN_SB > CHAIN_SB_ZERO && CHAIN_SB % 4u == 0u, "splice buffer layout");
 
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -345,8 +345,8 @@ __device__ inline void keccak_f1600_lane(uint32_t L[25], uint32_t H[25]) {
 // column of `sl` (LDS, dword j at sl[64 j]) instead of reading a suffix row of bft_hash_suffix_kernel (RECORDED and
 // REPAIR modes only)
 template <bool INLINE>
-__device__ inline void lane_chain(const Params& p, const ChainSets& cs, uint32_t k, uint32_t il, uint64_t* pbuf,
-                                  const PfxSel* ptbl, uint32_t* sl) {
+__device__ inline void lane_chain(const Params& p, const ChainSets& cs, uint32_t k, uint32_t il, const PfxSel* ptbl,
+                                  uint32_t* sl) {
     const uint32_t n = p.n_instances;
     const uint32_t K = p.sfx_rows, x0 = p.sfx_x0;
     uint32_t x1 = x0 + K - 1u, xs = x0;
@@ -368,17 +368,34 @@ __device__ inline void lane_chain(const Params& p, const ChainSets& cs, uint32_t
     // rows are < 2 GiB, bftsim.hip); dword j of the row of height x at 4 (il + ((x - x0) SFX_DEV_DW + j) n)
     const char* const sbase = (const char*)cs.sfx[k];
     const uint32_t n4 = 4u * n;                      // < 2^24 (launch_hash_chain_batch): 24-bit multiplies
-    const uint64_t* pb = pbuf;
     const uint32_t* const rec = cs.rec[k] + (uint64_t)il * p.rows * 4u;
+    const bool predicted = INLINE && p.chain_mode == CHAIN_PREDICTED;
+    uint64_t byz = 0;
+    if (predicted) {   // the instance's Byzantine set (bft_spec_byz_kernel's), its permutation in the lane's LDS column
+        byz = byz_mask64<64>(p.seed, cs.first[k] + il, p.byz_count, (uint8_t*)sl);
+        cs.bad[k][il] = 0xffffffffu;                  // no recorded block differs yet (bft_spec_verify_kernel)
+    }
+    uint32_t* const pred = predicted ? cs.pred[k] + (uint64_t)il * p.heights : nullptr;
     for (uint32_t x = xs; x <= x1; ++x) {
         const uint32_t rowoff = 4u * il + (x - x0) * SFX_DEV_DW * n4;
         uint32_t len_s;
-        if constexpr (INLINE) {                      // the suffix of the recorded block x (bft_hash_suffix_kernel's)
-            const uint4 row = *(const uint4*)(rec + 4u * x);
-            const uint32_t prop = row.y & 0xffffu, var = (row.y >> 16) & 1u;
+        if constexpr (INLINE) {                      // the suffix of block x (bft_hash_suffix_kernel's)
+            uint32_t prop, var, tick;
+            if (p.chain_mode == CHAIN_PREDICTED) {
+                // the block the canonical tick would commit, and its prediction word (bft_spec_suffix_kernel's)
+                const bool ok = spec_block64(p.seed, cs.first[k] + il, x, byz, 0u, prop, var);
+                pred[x - 1u] = ok ? SPEC_VALID | prop | (var << 16) : 0u;
+                if (!ok) break;                      // no prediction for x: the chain stops (repaired from here)
+                tick = x - 1u;
+            } else {                                 // the recorded block
+                const uint4 row = *(const uint4*)(rec + 4u * x);
+                prop = row.y & 0xffffu;
+                var = (row.y >> 16) & 1u;
+                tick = row.z;
+            }
             HdrWriter w(sl, 64u);
             header_suffix_fields(w, p.addresses + 20u * prop, p.seed, cs.first[k] + il, x, prop, var,
-                                 p.genesis_time + (uint64_t)p.block_period * ((uint64_t)row.z + 1ull));
+                                 p.genesis_time + (uint64_t)p.block_period * ((uint64_t)tick + 1ull));
             len_s = 8u * w.wi + w.fill;
             w.store(w.wi++, w.acc | (0x01ull << (8u * w.fill)));
             while (w.wi < SFX_BODY_DW / 2u) w.store(w.wi++, 0);
@@ -386,10 +403,8 @@ __device__ inline void lane_chain(const Params& p, const ChainSets& cs, uint32_t
             len_s = *(const uint32_t*)(sbase + rowoff + SFX_DEV_LEN_DW * n4);
         }
         if (len_s == 0u) break;                      // no prediction for x (CHAIN_PREDICTED only)
-        const uint32_t len_p = header_prefix_perm(pbuf, prev, ptbl);
         uint32_t pw[2 * PFX_WORDS];
-#pragma unroll
-        for (uint32_t i = 0; i < PFX_WORDS; ++i) { const uint64_t v = pb[i]; pw[2 * i] = (uint32_t)v; pw[2 * i + 1] = (uint32_t)(v >> 32); }
+        const uint32_t len_p = header_prefix_regs(prev, ptbl, pw);
         const uint32_t c = 72u - len_p, r = c & 3u, nb = splice_blocks(len_p, len_s);
         const int j0 = (int)(c >> 2) - (int)SFX_PAD;   // body dword of splice dword q0: -17 .. -9
         // splice-buffer dword j0 + i: the body dword, zero outside [0, SFX_BODY_DW) (the pad and the tail)
@@ -399,11 +414,16 @@ __device__ inline void lane_chain(const Params& p, const ChainSets& cs, uint32_t
         };
         auto S = [&](int j) -> uint32_t {
             const uint32_t v = G((uint32_t)(j < 0 ? 0 : j > (int)SFX_BODY_DW - 1 ? (int)SFX_BODY_DW - 1 : j));
-            return (j >= 0) & (j < (int)SFX_BODY_DW) ? v : 0u;
+            return ((j >= 0) & (j < (int)SFX_BODY_DW)) ? v : 0u;
         };
+        // the state starts as the prefix words (the suffix bytes spliced in below are 0 where the prefix is, so
+        // XOR = OR), so the prefix registers die before the block loop
         uint32_t L[25], H[25];
 #pragma unroll
-        for (int i = 0; i < 25; ++i) L[i] = H[i] = 0u;
+        for (int i = 0; i < 25; ++i) {
+            L[i] = i < (int)PFX_WORDS ? pw[2 * i] : 0u;
+            H[i] = i < (int)PFX_WORDS ? pw[2 * i + 1] : 0u;
+        }
         for (uint32_t blk = 0; blk < nb; ++blk) {     // one permutation site (code size)
             uint32_t d[35];
             if (blk == 0u) {                         // the prefix lies here; dwords from 17 on are in the body
@@ -418,9 +438,7 @@ __device__ inline void lane_chain(const Params& p, const ChainSets& cs, uint32_t
                     for (int i = 17; i < 35; ++i, vo += n4) d[i] = *(const uint32_t*)(sbase + vo);
                 }
 #pragma unroll
-                for (int i = 0; i < 2 * (int)PFX_WORDS; ++i) d[i] = align_bytes(d[i + 1], d[i], r) | pw[i];
-#pragma unroll
-                for (int i = 2 * (int)PFX_WORDS; i < 34; ++i) d[i] = align_bytes(d[i + 1], d[i], r);
+                for (int i = 0; i < 34; ++i) d[i] = align_bytes(d[i + 1], d[i], r);
             } else {
 #pragma unroll
                 for (int i = 0; i < 35; ++i) d[i] = S(j0 + 34 * (int)blk + i);
@@ -444,15 +462,17 @@ __device__ inline void lane_chain(const Params& p, const ChainSets& cs, uint32_t
 // runs its instances' 100 heights back to back, so a grid of every task at once held every SIMD slot for the whole
 // dispatch and the consensus kernels beside it got none (cfg3: a FAST kernel 0.40 -> 4.6 ms under a 12-launch chain
 // dispatch, profiles/r06/traces/r06n_timeline_k16.txt); capped, the chain waves leave slots to them.
-// register budget: a chain wave beside the FAST kernel's waves (4 per SIMD) on the same SIMD
+// register budget: the inline variant at 4 waves per SIMD (126 VGPRs, no scratch; 149 at 3) so that two chain waves
+// fit a SIMD beside two FAST waves (111 VGPRs each): 2 x 128 + 2 x 112 <= 512; the global-row variant (predicted
+// chains) at 3
 #ifndef BFT_LANE_WAVES_PER_SIMD
-#define BFT_LANE_WAVES_PER_SIMD 3
+#define BFT_LANE_WAVES_PER_SIMD 4
 #endif
+
 template <bool INLINE>
-__global__ __launch_bounds__(64, BFT_LANE_WAVES_PER_SIMD) void bft_hash_chain_lane_kernel(Params p, ChainSets cs) {
+__global__ __launch_bounds__(64, INLINE ? BFT_LANE_WAVES_PER_SIMD : 3) void bft_hash_chain_lane_kernel(Params p, ChainSets cs) {
 #if defined(__HIP_DEVICE_COMPILE__)
     set_prio(p.chain_prio);
-    __shared__ __attribute__((aligned(16))) uint64_t pbuf[64 * (PFX_WORDS + 4)];   // prefix words per lane
     __shared__ PfxSel ptbl[16];
     extern __shared__ uint32_t sfx_lds[];             // INLINE: [SFX_BODY_DW][64] suffix dwords (launch's dynamic LDS)
     if (threadIdx.x < 16) ptbl[threadIdx.x] = PFX_TBL[threadIdx.x];
@@ -461,13 +481,13 @@ __global__ __launch_bounds__(64, BFT_LANE_WAVES_PER_SIMD) void bft_hash_chain_la
     for (uint32_t t = blockIdx.x; t < tasks; t += gridDim.x) {   // every wave reaches the end of the task list
         const uint32_t k = t / bps, il = (t % bps) * 64u + threadIdx.x;
         if (il < p.n_instances)
-            lane_chain<INLINE>(p, cs, k, il, pbuf + threadIdx.x * (PFX_WORDS + 4), ptbl, INLINE ? sfx_lds + threadIdx.x : nullptr);
+            lane_chain<INLINE>(p, cs, k, il, ptbl, INLINE ? sfx_lds + threadIdx.x : nullptr);
     }
 #endif
 }
 static hipError_t launch_lane(uint32_t tasks, const ChainSets& cs, hipStream_t s, const Params& p) {
     const uint32_t g = p.chain_grid && p.chain_grid < tasks ? p.chain_grid : tasks;   // persistent waves
-    if (p.chain_inline && p.chain_mode != CHAIN_PREDICTED)   // the inline suffix columns in dynamic LDS
+    if (p.chain_inline)                               // the inline suffix columns in dynamic LDS
         hipLaunchKernelGGL(bft_hash_chain_lane_kernel<true>, dim3(g), dim3(64), (size_t)SFX_BODY_DW * 64u * 4u, s, p, cs);
     else hipLaunchKernelGGL(bft_hash_chain_lane_kernel<false>, dim3(g), dim3(64), 0, s, p, cs);
     return hipGetLastError();

@@ -260,7 +260,8 @@ def test_predicted_chains_match_oracle(name, mk, depth, batch, monkeypatch):
 def test_lane_chain_kernel(name, mk, spec, inline, grid, monkeypatch):
     """The lane-per-instance chain kernel (BFTSIM_CHAIN_LANE_MIN) in all three chain modes: recorded blocks, and
     predicted blocks with the repair from the first one that differs; the suffix spliced from the suffix rows or
-    encoded by each lane from the recorded row (BFTSIM_CHAIN_INLINE); one wave per task or 3 persistent waves for
+    encoded by each lane from the recorded row or its own prediction (BFTSIM_CHAIN_INLINE); one wave per task or 3
+    persistent waves for
     the whole batch (BFTSIM_CHAIN_GRID)."""
     monkeypatch.setenv("BFTSIM_TESTING", "1")
     monkeypatch.setenv("BFTSIM_CHAIN_LANE_MIN", "1")
