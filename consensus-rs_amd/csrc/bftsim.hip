@@ -469,6 +469,7 @@ struct bftsim {
     // predicted LANE chains (large shards: throughput, not latency) below the FAST kernels: 2.06e9-2.10e9 at 0 or 1
     // against 1.80e9-1.93e9 at 3 (cfg3; profiles/r06/ab_spec_lane; BFTSIM_CHAIN_PRIO_SPEC_LANE)
     uint32_t chain_prio_spec_lane = 0;
+    uint32_t chain_prio_spec_early = 3;   // A/B: BFTSIM_CHAIN_PRIO_SPEC_EARLY
     uint32_t fast_lds_pad = 0;        // extra LDS per FAST wave: fewer resident FAST waves (BFTSIM_TESTING + BFTSIM_FAST_LDS_PAD)
     bool seed_spec = true;            // little-endian seeds, N = 64: predicted blocks (BFTSIM_TESTING + BFTSIM_SEED_SPEC=0: off)
     int pipeline = 0;                 // number of row-table sets (0: no pipelining)
@@ -487,8 +488,10 @@ struct bftsim {
     // on at every size: a small shard's chains (lane pairs) are bound by their latency, which they start ahead
     // of; a large shard's (lanes, each predicting and encoding its blocks itself) fill the issue slots the consensus
     // kernels leave from the first launch on (cfg3: 2.06e9-2.10e9 against 1.94e9-1.98e9 recorded;
-    // profiles/r06/ab_spec_lane). BFTSIM_TESTING + BFTSIM_HASH_SPEC=0: recorded chains at every size
+    // profiles/r06/ab_spec_lane). BFTSIM_TESTING + BFTSIM_HASH_SPEC=0: recorded chains at every size; =2: predicted
+    // for lossy schedules too
     uint64_t hash_spec_max = ~0ull;
+    bool spec_lossy = false;          // predicted chains with drops or crashes too (BFTSIM_HASH_SPEC=2)
     uint32_t n_hs_spec = 3;
     struct Pending { uint32_t set, ev, first, cs; } pend[MAX_BATCH];   // cs: the launch stream it ran on
     // one event per chain batch (flush_batch) instead of one per set: a ring, re-recorded after BATCH_EVS batches (a set
@@ -877,6 +880,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         knob("BFTSIM_CHAIN_GRID", h->chain_grid, 0, 1u << 20);
         knob("BFTSIM_CHAIN_PRIO_SPEC", h->chain_prio_spec, 0, 3);
         knob("BFTSIM_CHAIN_PRIO_SPEC_LANE", h->chain_prio_spec_lane, 0, 3);
+        knob("BFTSIM_CHAIN_PRIO_SPEC_EARLY", h->chain_prio_spec_early, 0, 3);
         knob("BFTSIM_SPEC_EARLY", h->spec_early, 0, 1);
         knob("BFTSIM_SPEC_FINAL", h->spec_final, 0, 1);
         knob("BFTSIM_SPEC_FIRST", h->spec_first, 0, 1);
@@ -893,6 +897,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         if (testing && ss) h->seed_spec = atoi(ss) != 0;
         const char* hs = getenv("BFTSIM_HASH_SPEC");   // 0: off, 1: at every size
         if (testing && hs) h->hash_spec_max = atoi(hs) != 0 ? ~0ull : 0ull;
+        h->spec_lossy = testing && hs && atoi(hs) == 2;   // 2: lossy schedules too (the tests of the repairs)
         const char* pe = getenv("BFTSIM_PMC_EVICT");
         h->pmc_evict = testing && pe && atoi(pe) != 0;   // scripts/gpu_profile.sh's attribution pass
         if (h->pmc_evict && !h->d_evict) {          // before any launch, so every eviction is the same dispatch
@@ -1191,7 +1196,10 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
         const bool on_launch = fast;
         if (pipe && K >= H && on_launch) {
             bftsim::RowSet& r = h->sets[h->cur_set];
-            const bool hspec = r.byz && n < h->hash_spec_max;   // big-endian seeds: predicted chains
+            // big-endian seeds: predicted chains, for lossless schedules (no drops, no proposer crashes),
+            // where the canonical tick commits every height; with drops most instances leave it early and the
+            // predicted chains would mostly be repaired (drop64: 22.6 ms of chain kernels per launch against 0.7)
+            const bool hspec = r.byz && n < h->hash_spec_max && ((p.thr16 == 0 && p.crash_on == 0) || h->spec_lossy);
             if (!hspec) {
                 // suffix rows now (unless the lane chains encode them); the chains in the next batch (flush_batch)
                 if (!(h->chain_inline && chain_kind(h, n, false) == bft::CHAIN_KERNEL_LANE)) {
@@ -1333,7 +1341,10 @@ static int flush_batch(bftsim* h, bool final) {
         // a converted final batch on lane pairs (its chains are the burst's tail: latency); the burst's first batch
         // (spec_first) has the whole burst to finish in, so it keeps the large shard's lanes (throughput)
         const uint32_t kind = conv && !(first && !final) ? bft::CHAIN_KERNEL_PAIR : chain_kind(h, p.n_instances, true);
-        p.chain_prio = kind == bft::CHAIN_KERNEL_LANE ? h->chain_prio_spec_lane : h->chain_prio_spec;
+        // lane pairs: the sync's batch (the burst's tail) at chain_prio_spec, earlier full batches (slack: they end
+        // long before the burst does) at chain_prio_spec_early
+        p.chain_prio = kind == bft::CHAIN_KERNEL_LANE ? h->chain_prio_spec_lane
+                     : final ? h->chain_prio_spec : h->chain_prio_spec_early;
         // the predicted blocks' suffix rows and chains, which need nothing of the consensus kernels (one suffix
         // pass for the whole batch: per launch on a stream of their own they fell behind the launches); once
         // every launch's consensus kernel is done, the check of its recorded blocks against the predictions, and

@@ -233,7 +233,7 @@ def test_predicted_chains_match_oracle(name, mk, depth, batch, monkeypatch):
     cfg = mk()
     n = 96
     outs = []
-    for spec in ("1", "0"):
+    for spec in ("2", "0"):                          # 2: predicted for lossy schedules too
         monkeypatch.setenv("BFTSIM_HASH_SPEC", spec)
         sim = _sim(cfg)
         try:
@@ -253,7 +253,7 @@ def test_predicted_chains_match_oracle(name, mk, depth, batch, monkeypatch):
 
 @pytest.mark.parametrize("grid", ["0", "3"])
 @pytest.mark.parametrize("inline", ["0", "1"])
-@pytest.mark.parametrize("spec", ["1", "0"])
+@pytest.mark.parametrize("spec", ["2", "0"])
 @pytest.mark.parametrize("name,mk", [("cfg3-30", lambda: cfg3(heights=30)),
                                      ("n64-drop", lambda: BftConfig(n=64, heights=30, seed=17, byz_count=21,
                                                                     drop_ppm=50_000, name="n64-drop"))])
