@@ -1288,7 +1288,8 @@ static int flush_batch(bftsim* h, bool final) {
     // kernel is done and take ~2 ms) runs as predicted lane-pair chains instead: they start now, beside the launches'
     // consensus kernels, and only the check and the repairs are left behind them
     const bool first = h->batch_after_sync && h->spec_first;   // the burst's first batch (A/B arm)
-    const bool conv = ((final && h->spec_final) || first) && !h->batch_spec && h->sets[h->pend[0].set].byz != nullptr;
+    const bool conv = ((final && h->spec_final) || first) && !h->batch_spec && h->sets[h->pend[0].set].byz != nullptr &&
+                      ((h->batch_p.thr16 == 0 && h->batch_p.crash_on == 0) || h->spec_lossy);   // lossless (launch)
     const bool spec = h->batch_spec || conv;
     if (h->chain_on_launch) t = h->cs[h->pend[h->n_pend - 1].cs];   // A/B: behind the launches, no overlap
     else if (conv && h->conv_stream && h->n_hs < bftsim::MAX_HS) {
