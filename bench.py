@@ -144,6 +144,20 @@ def pmc_issue(workload: str = "cfg3", kernel: str = "bft_consensus_kernel"):
             "salu": e.get("SQ_INSTS_SALU_per_launch", e.get("SQ_INSTS_SALU"))}
 
 
+def pmc_issue_step(workload: str = "cfg3"):
+    """VALU / SALU wave-instructions per launch of every kernel of the step (the summary's kernels, each counted
+    once: the composite consensus entry is left out), or None."""
+    files = _pmc_files(workload)
+    if not files:
+        return None
+    k = json.load(open(files[-1])).get("kernels", {})
+    es = [e for e in k.values() if "SQ_INSTS_VALU" in e and "composed_of" not in e]
+    if not es:
+        return None
+    return {"valu": sum(e.get("SQ_INSTS_VALU_per_launch", e["SQ_INSTS_VALU"]) for e in es),
+            "salu": sum(e.get("SQ_INSTS_SALU_per_launch", e.get("SQ_INSTS_SALU") or 0) for e in es)}
+
+
 def cfg_desc(cfg) -> str:
     d = [f"N={cfg.n}"]
     if cfg.byz_count:
@@ -578,6 +592,12 @@ def main():
                     "salu_frac": q["salu"] / (ms / 1e3) / SALU_ISSUE_PEAK,
                     "per_instance_round": {"valu": q["valu"] / max(views_rank, 1),
                                            "salu": q["salu"] / max(views_rank, 1)}})(pmc_issue(pmc_key, dom)),
+                # the whole step: every kernel's VALU per launch over the step time (the chain kernels run under the
+                # consensus kernels at a lower priority, so their own event time is stretched)
+                "issue_step": (lambda q: None if q is None else {
+                    "valu_wave_instr_per_launch": q["valu"], "salu_wave_instr_per_launch": q["salu"],
+                    "valu_per_s": q["valu"] / (ms_step / 1e3), "valu_frac": q["valu"] / (ms_step / 1e3) / VALU_ISSUE_PEAK,
+                    "salu_frac": q["salu"] / (ms_step / 1e3) / SALU_ISSUE_PEAK})(pmc_issue_step(pmc_key)),
                 "per": "launch (one step; a chain dispatch's time and counters shared among the launches it carries)",
                 "dispatch": {"launches_per_dispatch": batch, "ops_per_dispatch": ops * batch, "ms_per_dispatch": ms * batch},
                 "traffic_source": traffic_src,
