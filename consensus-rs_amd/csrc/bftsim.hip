@@ -508,6 +508,7 @@ struct bftsim {
     uint32_t spec_early = 0;
     uint32_t rec_clear = 0;           // zero the record rows of FAST launches too (BFTSIM_TESTING + BFTSIM_REC_CLEAR)
     uint32_t diag_no_chain = 0;       // diagnostic: flush_batch enqueues no chain kernels (wrong hashes)
+    uint32_t first_batch = 0;         // launches in the first chain batch after a sync (0: hash_batch; BFTSIM_FIRST_BATCH)
     uint32_t conv_stream = 0;         // a converted final batch on a hash stream of its own (A/B: BFTSIM_CONV_STREAM;
                                       // 1.70e9-1.74e9 against 1.82e9-1.85e9 on the batch's, profiles/r06/ab_conv_stream)
     uint32_t chain_on_launch = 0;     // the chain batches on the last launch's stream (BFTSIM_CHAIN_ON_LAUNCH)
@@ -887,6 +888,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         knob("BFTSIM_REC_CLEAR", h->rec_clear, 0, 1);
         knob("BFTSIM_DIAG_NO_CHAIN", h->diag_no_chain, 0, 1);
         knob("BFTSIM_CONV_STREAM", h->conv_stream, 0, 1);
+        knob("BFTSIM_FIRST_BATCH", h->first_batch, 0, bftsim::MAX_BATCH);
         knob("BFTSIM_CHAIN_ON_LAUNCH", h->chain_on_launch, 0, 1);
         knob("BFTSIM_CHAIN_INLINE", h->chain_inline, 0, 1);
         knob("BFTSIM_LAUNCH_STREAMS_SEEDED", h->n_cs_seeded, 1, bftsim::MAX_CS);
@@ -1238,7 +1240,9 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
                 HIPCHECK(h, pmc_evict(h, t));
             }
             h->pend[h->n_pend++] = {h->cur_set, (h->ring_head - 1) % bftsim::RING, (uint32_t)first, h->cur_cs};
-            if (h->n_pend >= h->hash_batch) if (int rc = flush_batch(h)) return rc;
+            // the burst's first batch may be shorter (its chains start sooner; A/B: BFTSIM_FIRST_BATCH)
+            const uint32_t cap = h->batch_after_sync && h->first_batch ? h->first_batch : h->hash_batch;
+            if (h->n_pend >= cap) if (int rc = flush_batch(h)) return rc;
         } else {
             // one launch's hash pass: on a hash stream (pipelined) or the launch stream; chunks of K heights
             // share the suffix rows (suffix and chain kernels in order on one stream)

@@ -192,7 +192,11 @@ SECP_FN U256 fe_reduce_wide(const uint32_t t[16]) {
         r.v[0] = (uint32_t)d; d >>= 32;
         d += (uint64_t)r.v[1] + 1u;
         r.v[1] = (uint32_t)d; d >>= 32;
-        for (int k = 2; k < 8 && d; ++k) { d += r.v[k]; r.v[k] = (uint32_t)d; d >>= 32; }
+        // the whole ripple of the carry bit, unrolled (adding a zero carry changes nothing): an early exit on
+        // d == 0 made the limbs a dynamically indexed private array, 36 B of scratch per lane in every secp kernel
+        uint32_t cy = (uint32_t)d;                   // 0 or 1
+#pragma unroll
+        for (int k = 2; k < 8; ++k) { r.v[k] += cy; cy = r.v[k] < cy ? 1u : 0u; }
     }
     U256 s;
     uint32_t br = u_sub(s, r, c_p());
