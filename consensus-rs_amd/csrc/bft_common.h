@@ -91,7 +91,7 @@ struct Params {
     uint32_t chain_mode;
     uint32_t chain_grid;              // lane-chain kernel: at most this many (persistent) waves; 0: one per task
     uint32_t chain_inline;            // lane-chain kernel: each lane encodes its suffixes (no suffix rows)
-    uint32_t pad7;
+    uint32_t fast_prio;               // s_setprio of the FAST kernel + 1 (0: its default, 2; BFTSIM_FAST_PRIO)
 };
 constexpr uint32_t RCS_DEFAULT_K = 16, RCS_MAX_K = 4096;
 // one logged broadcast: {tick, phase | code << 8 | sender << 16, height, round, block id lo, hi,

@@ -508,6 +508,7 @@ struct bftsim {
     uint32_t spec_early = 0;
     uint32_t rec_clear = 0;           // zero the record rows of FAST launches too (BFTSIM_TESTING + BFTSIM_REC_CLEAR)
     uint32_t diag_no_chain = 0;       // diagnostic: flush_batch enqueues no chain kernels (wrong hashes)
+    uint32_t fast_prio = 0;           // FAST kernel priority + 1 (0: the kernel's default; BFTSIM_FAST_PRIO)
     uint32_t first_batch = 0;         // launches in the first chain batch after a sync (0: hash_batch; BFTSIM_FIRST_BATCH)
     uint32_t conv_stream = 0;         // a converted final batch on a hash stream of its own (A/B: BFTSIM_CONV_STREAM;
                                       // 1.70e9-1.74e9 against 1.82e9-1.85e9 on the batch's, profiles/r06/ab_conv_stream)
@@ -889,6 +890,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         knob("BFTSIM_DIAG_NO_CHAIN", h->diag_no_chain, 0, 1);
         knob("BFTSIM_CONV_STREAM", h->conv_stream, 0, 1);
         knob("BFTSIM_FIRST_BATCH", h->first_batch, 0, bftsim::MAX_BATCH);
+        knob("BFTSIM_FAST_PRIO", h->fast_prio, 0, 4);
         knob("BFTSIM_CHAIN_ON_LAUNCH", h->chain_on_launch, 0, 1);
         knob("BFTSIM_CHAIN_INLINE", h->chain_inline, 0, 1);
         knob("BFTSIM_LAUNCH_STREAMS_SEEDED", h->n_cs_seeded, 1, bftsim::MAX_CS);
@@ -1021,6 +1023,7 @@ static bft::Params make_params(bftsim* h, uint64_t first, uint64_t n) {
     p.rcs = h->d_rcs;
     p.rcs_k = h->rcs_k;
     p.chain_prio = h->chain_prio;
+    p.fast_prio = h->fast_prio;
     p.chain_grid = h->chain_grid;
     p.chain_inline = h->chain_inline;
     p.fast_lds_pad = h->fast_lds_pad;

@@ -21,8 +21,12 @@ void bft_consensus_fast_kernel(Params p) {
 #define BFT_CONSENSUS_PRIO 2
 #endif
     // win issue arbitration against the hash waves of the previous launch (the hash pass stretches into
-    // the issue gaps and still finishes within the step)
-    __builtin_amdgcn_s_setprio(BFT_CONSENSUS_PRIO);
+    // the issue gaps and still finishes within the step); s_setprio takes an immediate
+    if (p.fast_prio == 0u) __builtin_amdgcn_s_setprio(BFT_CONSENSUS_PRIO);
+    else if (p.fast_prio == 1u) __builtin_amdgcn_s_setprio(0);
+    else if (p.fast_prio == 2u) __builtin_amdgcn_s_setprio(1);
+    else if (p.fast_prio == 3u) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(3);
     Fast64<WaveHip, LOSSY, SEEDED> sim(p, lds, blockIdx.x);
     sim.run();
 }
