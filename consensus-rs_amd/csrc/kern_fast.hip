@@ -337,6 +337,12 @@ __device__ inline void keccak_f1600_lane(uint32_t L[25], uint32_t H[25]) {
 }
 #endif
 
+// INLINE: the suffix body dwords a lane keeps in its LDS column. The suffix is at most 212 bytes (address 44, root 35,
+// tx_hash <= 67, receipt 35, the scalars and extra 31) plus the domain byte: dwords 0 .. 53; the splice reads every
+// dword past the column as 0 (as it reads the row's zero tail). 56 instead of SFX_BODY_DW's 60: 14 KB per chain wave,
+// so that more consensus waves fit a CU beside two chain waves per SIMD.
+constexpr uint32_t SFX_LDS_DW = 56;
+static_assert(SFX_LDS_DW * 4u >= 213u && SFX_LDS_DW <= SFX_BODY_DW && SFX_LDS_DW % 2u == 0u, "inline suffix column");
 // Large shards (>= 8,192 instances per launch, bftsim.hip chain_lane_min): a LANE per instance. The whole state in
 // one lane: ~180 VALU per round instead of 2 x 118 for a lane pair, i.e. ~24 % fewer instructions per header for
 // ~1.5x the chain latency, which a large shard's throughput-bound pipeline hides (cfg3 at 16,384: 1.70e9 with lane
@@ -402,7 +408,7 @@ __device__ inline void lane_chain(const Params& p, const ChainSets& cs, uint32_t
                                  p.genesis_time + (uint64_t)p.block_period * ((uint64_t)tick + 1ull));
             len_s = 8u * w.wi + w.fill;
             w.store(w.wi++, w.acc | (0x01ull << (8u * w.fill)));
-            while (w.wi < SFX_BODY_DW / 2u) w.store(w.wi++, 0);
+            while (w.wi < SFX_LDS_DW / 2u) w.store(w.wi++, 0);
         } else {
             len_s = *(const uint32_t*)(sbase + rowoff + SFX_DEV_LEN_DW * n4);
         }
@@ -411,14 +417,15 @@ __device__ inline void lane_chain(const Params& p, const ChainSets& cs, uint32_t
         const uint32_t len_p = header_prefix_regs(prev, ptbl, pw);
         const uint32_t c = 72u - len_p, r = c & 3u, nb = splice_blocks(len_p, len_s);
         const int j0 = (int)(c >> 2) - (int)SFX_PAD;   // body dword of splice dword q0: -17 .. -9
-        // splice-buffer dword j0 + i: the body dword, zero outside [0, SFX_BODY_DW) (the pad and the tail)
+        // splice-buffer dword j0 + i: the body dword, zero outside [0, BODY) (the pad and the tail)
         auto G = [&](uint32_t jj) -> uint32_t {      // body dword jj < SFX_BODY_DW
             if constexpr (INLINE) return sl[64u * jj];
             else return *(const uint32_t*)(sbase + rowoff + __umul24(jj, n4));
         };
+        constexpr int BODY = INLINE ? (int)SFX_LDS_DW : (int)SFX_BODY_DW;   // dwords past it read as 0
         auto S = [&](int j) -> uint32_t {
-            const uint32_t v = G((uint32_t)(j < 0 ? 0 : j > (int)SFX_BODY_DW - 1 ? (int)SFX_BODY_DW - 1 : j));
-            return ((j >= 0) & (j < (int)SFX_BODY_DW)) ? v : 0u;
+            const uint32_t v = G((uint32_t)(j < 0 ? 0 : j > BODY - 1 ? BODY - 1 : j));
+            return ((j >= 0) & (j < BODY)) ? v : 0u;
         };
         // the state starts as the prefix words (the suffix bytes spliced in below are 0 where the prefix is, so
         // XOR = OR), so the prefix registers die before the block loop
@@ -478,7 +485,7 @@ __global__ __launch_bounds__(64, INLINE ? BFT_LANE_WAVES_PER_SIMD : 3) void bft_
 #if defined(__HIP_DEVICE_COMPILE__)
     set_prio(p.chain_prio);
     __shared__ PfxSel ptbl[16];
-    extern __shared__ uint32_t sfx_lds[];             // INLINE: [SFX_BODY_DW][64] suffix dwords (launch's dynamic LDS)
+    extern __shared__ uint32_t sfx_lds[];             // INLINE: [SFX_LDS_DW][64] suffix dwords (launch's dynamic LDS)
     if (threadIdx.x < 16) ptbl[threadIdx.x] = PFX_TBL[threadIdx.x];
     __syncthreads();
     const uint32_t bps = (p.n_instances + 63u) / 64u, tasks = cs.count * bps;
@@ -492,7 +499,7 @@ __global__ __launch_bounds__(64, INLINE ? BFT_LANE_WAVES_PER_SIMD : 3) void bft_
 static hipError_t launch_lane(uint32_t tasks, const ChainSets& cs, hipStream_t s, const Params& p) {
     const uint32_t g = p.chain_grid && p.chain_grid < tasks ? p.chain_grid : tasks;   // persistent waves
     if (p.chain_inline)                               // the inline suffix columns in dynamic LDS
-        hipLaunchKernelGGL(bft_hash_chain_lane_kernel<true>, dim3(g), dim3(64), (size_t)SFX_BODY_DW * 64u * 4u, s, p, cs);
+        hipLaunchKernelGGL(bft_hash_chain_lane_kernel<true>, dim3(g), dim3(64), (size_t)SFX_LDS_DW * 64u * 4u, s, p, cs);
     else hipLaunchKernelGGL(bft_hash_chain_lane_kernel<false>, dim3(g), dim3(64), 0, s, p, cs);
     return hipGetLastError();
 }
