@@ -508,6 +508,7 @@ struct bftsim {
     uint32_t spec_early = 0;
     uint32_t rec_clear = 0;           // zero the record rows of FAST launches too (BFTSIM_TESTING + BFTSIM_REC_CLEAR)
     uint32_t diag_no_chain = 0;       // diagnostic: flush_batch enqueues no chain kernels (wrong hashes)
+    uint32_t diag_no_clear = 0;       // diagnostic: no bft_clear_kernel (wrong statistics, hand-overs)
     uint32_t fast_prio = 0;           // FAST kernel priority + 1 (0: the kernel's default; BFTSIM_FAST_PRIO)
     uint32_t first_batch = 0;         // launches in the first chain batch after a sync (0: hash_batch; BFTSIM_FIRST_BATCH)
     uint32_t conv_stream = 0;         // a converted final batch on a hash stream of its own (A/B: BFTSIM_CONV_STREAM;
@@ -888,6 +889,7 @@ int bftsim_prepare(bftsim_t* h, uint64_t n) {
         knob("BFTSIM_SPEC_FIRST", h->spec_first, 0, 1);
         knob("BFTSIM_REC_CLEAR", h->rec_clear, 0, 1);
         knob("BFTSIM_DIAG_NO_CHAIN", h->diag_no_chain, 0, 1);
+        knob("BFTSIM_DIAG_NO_CLEAR", h->diag_no_clear, 0, 1);
         knob("BFTSIM_CONV_STREAM", h->conv_stream, 0, 1);
         knob("BFTSIM_FIRST_BATCH", h->first_batch, 0, bftsim::MAX_BATCH);
         knob("BFTSIM_FAST_PRIO", h->fast_prio, 0, 4);
@@ -1146,10 +1148,12 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
     // launch saved (BFTSIM_TESTING + BFTSIM_REC_CLEAR=1: cleared anyway)
     const bool clear_rec = !fast_launch || h->rec_clear;
     const uint64_t n_rec = clear_rec ? (uint64_t)n * h->hcap : 0;
-    hipLaunchKernelGGL(bft_clear_kernel, dim3(clear_blocks(n_rec > n ? n_rec : n)), dim3(256), 0, s, (uint4*)h->d_rec,
-                       n_rec, h->d_hist, fast_launch ? h->d_resume : nullptr, (uint32_t)n,
-                       fast_launch ? h->d_resume_q : nullptr);
-    HIPCHECK(h, hipGetLastError());
+    if (!h->diag_no_clear) {   // (diagnostic BFTSIM_DIAG_NO_CLEAR=1: the host cost of this dispatch; wrong statistics)
+        hipLaunchKernelGGL(bft_clear_kernel, dim3(clear_blocks(n_rec > n ? n_rec : n)), dim3(256), 0, s, (uint4*)h->d_rec,
+                           n_rec, h->d_hist, fast_launch ? h->d_resume : nullptr, (uint32_t)n,
+                           fast_launch ? h->d_resume_q : nullptr);
+        HIPCHECK(h, hipGetLastError());
+    }
     if (h->d_backlog) HIPCHECK(h, hipMemsetAsync(h->d_backlog, 0, h->backlog_bytes, s));
     uint32_t per_block = h->seg > 64 ? 1u : 64u / h->seg;      // instances per workgroup
     uint32_t grid = (uint32_t)((n + per_block - 1) / per_block);
