@@ -164,9 +164,10 @@ int bftsim_kernel_ms_sum(bftsim_t *h, double *consensus_ms, double *hash_ms, uin
 int bftsim_set_pipeline(bftsim_t *h, int on);
 /* pipelined launches: the number of consecutive launches whose block-hash chains run as one kernel (1..32,
  * default 4). A launch waiting for its batch is hashed when the batch fills, at bftsim_sync, or when the ring
- * needs its row-table set again. With big-endian seeds at N = 64 the chains of a batch run on the predicted
- * canonical blocks from the batch's first launch on, and are checked against the recorded blocks (and re-run
- * from the first one that differs) once the batch's consensus kernels are done. */
+ * needs its row-table set again. With big-endian seeds at N = 64 and a lossless schedule (no drops, no proposer
+ * crashes) the chains of a batch run on the predicted canonical blocks as soon as the batch is flushed, and are
+ * checked against the recorded blocks (and re-run from the first one that differs) once the batch's consensus
+ * kernels are done. */
 int bftsim_set_hash_batch(bftsim_t *h, uint32_t launches);
 /* verification switch: 0 runs N = 64 through the full kernel alone instead of the FAST kernel +
  * resume (results are identical; the default 1 is the fast path) */
