@@ -284,6 +284,34 @@ def test_lane_chain_kernel(name, mk, spec, inline, grid, monkeypatch):
     assert_same(O.run(cfg, 3 * n, n), got, f"{name} lane chains, predicted={spec}")
 
 
+@pytest.mark.parametrize("seed,byz,drop,crash,heights", [
+    (31, 21, 0, 0, 60), (32, 0, 0, 0, 40), (33, 42, 0, 0, 50), (34, 21, 20_000, 0, 40), (35, 10, 0, 200_000, 40),
+    (36, 30, 5_000, 0, 70)])
+def test_predicted_lane_chains_sweep(seed, byz, drop, crash, heights, monkeypatch):
+    """Predicted LANE chains (DESIGN §4j: each lane predicts, masks and encodes its blocks; 56-dword LDS columns;
+    the register-resident prefix) over seeds, Byzantine counts (0 .. 42), drops and proposer crashes, forced at a
+    small size (BFTSIM_CHAIN_LANE_MIN=1; BFTSIM_HASH_SPEC=2: lossy schedules too), 9 launches in batches of 4,
+    every instance against the oracle."""
+    monkeypatch.setenv("BFTSIM_TESTING", "1")
+    monkeypatch.setenv("BFTSIM_CHAIN_LANE_MIN", "1")
+    monkeypatch.setenv("BFTSIM_HASH_SPEC", "2")
+    cfg = BftConfig(n=64, heights=heights, seed=seed, byz_count=byz, drop_ppm=drop, proposer_crash_ppm=crash,
+                    name=f"sweep{seed}")
+    n = 192
+    sim = _sim(cfg)
+    try:
+        sim.set_pipeline(True, 8)
+        sim.set_hash_batch(4)
+        sim.prepare(n)
+        for _ in range(9):
+            sim.launch(5 * n)
+        sim.sync()
+        got = sim.fetch()
+    finally:
+        sim.close()
+    assert_same(O.run(cfg, 5 * n, n), got, f"predicted lane chains {cfg.name}")
+
+
 @pytest.mark.parametrize("name,mk,depth", [
     ("cfg3-le",lambda: __import__("dataclasses").replace(cfg3(heights=40), seed_byte_order=1, name="cfg3-le"), 6),
     ("n64-le-drop", lambda: BftConfig(n=64, heights=20, seed=15, byz_count=21, drop_ppm=50_000, seed_byte_order=1,
