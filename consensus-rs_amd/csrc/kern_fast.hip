@@ -473,7 +473,7 @@ __device__ inline void lane_chain(const Params& p, const ChainSets& cs, uint32_t
 // runs its instances' 100 heights back to back, so a grid of every task at once held every SIMD slot for the whole
 // dispatch and the consensus kernels beside it got none (cfg3: a FAST kernel 0.40 -> 4.6 ms under a 12-launch chain
 // dispatch, profiles/r06/traces/r06n_timeline_k16.txt); capped, the chain waves leave slots to them.
-// register budget: the inline variant at 4 waves per SIMD (126 VGPRs, no scratch; 149 at 3) so that two chain waves
+// register budget: the inline variant at 4 waves per SIMD (128 VGPRs, no scratch; 149 at 3) so that two chain waves
 // fit a SIMD beside two FAST waves (111 VGPRs each): 2 x 128 + 2 x 112 <= 512; the global-row variant (predicted
 // chains) at 3
 #ifndef BFT_LANE_WAVES_PER_SIMD
