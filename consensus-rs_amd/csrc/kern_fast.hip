@@ -10,11 +10,18 @@ namespace bft {
 #ifndef BFT_FAST_WAVES_PER_SIMD
 #define BFT_FAST_WAVES_PER_SIMD 4   // 110 VGPRs, no scratch; since the canonical tick 4, 5 and 6 (80 VGPRs, 76-88 B/lane of spills) measure the same (profiles/r04/ab_occupancy)
 #endif
+// the lossless build (cfg3): 4 waves (110 VGPRs, no scratch). At 5 (96 VGPRs, 28 B/lane spilled: one reload per
+// canonical tick) a third FAST wave fits a SIMD beside one predicted-lane chain wave: +2.3 % on cfg3 in interleaved
+// pairs (2.13e9-2.20e9 against 2.08e9-2.13e9, profiles/r06/ab_fast_waves), within the box-to-box spread; kept at 4
+#ifndef BFT_FAST_LOSSLESS_WAVES_PER_SIMD
+#define BFT_FAST_LOSSLESS_WAVES_PER_SIMD 4
+#endif
 #ifndef BFT_FAST_SEEDED_WAVES_PER_SIMD
 #define BFT_FAST_SEEDED_WAVES_PER_SIMD 4   // the in-kernel wave hash needs registers: 5 spills to scratch (gpurun r03c: 4 waves +6 %)
 #endif
 template <bool LOSSY, bool SEEDED>
-__global__ __launch_bounds__(64, SEEDED ? BFT_FAST_SEEDED_WAVES_PER_SIMD : BFT_FAST_WAVES_PER_SIMD)
+__global__ __launch_bounds__(64, SEEDED ? BFT_FAST_SEEDED_WAVES_PER_SIMD
+                                        : LOSSY ? BFT_FAST_WAVES_PER_SIMD : BFT_FAST_LOSSLESS_WAVES_PER_SIMD)
 void bft_consensus_fast_kernel(Params p) {
     extern __shared__ uint8_t lds[];
 #ifndef BFT_CONSENSUS_PRIO
