@@ -1295,9 +1295,10 @@ int bftsim_launch(bftsim_t* h, uint64_t first, void* stream) {
 static int flush_batch(bftsim* h, bool final) {
     if (h->n_pend == 0) return BFTSIM_OK;
     hipStream_t t = h->hstr[h->batch_hs];           // chosen at the batch's first launch
-    // A final batch of recorded chains (a large shard's lane chains, which start once the last launch's consensus
-    // kernel is done and take ~2 ms) runs as predicted lane-pair chains instead: they start now, beside the launches'
-    // consensus kernels, and only the check and the repairs are left behind them
+    // A final batch of recorded chains (lossless schedules with predictions off, BFTSIM_HASH_SPEC=0: lane chains that
+    // start once the last launch's consensus kernel is done and take ~2 ms) runs as predicted lane-pair chains
+    // instead: they start now, beside the launches' consensus kernels, and only the check and the repairs are left
+    // behind them. With predictions on (the default) every batch is predicted already (§4j).
     const bool first = h->batch_after_sync && h->spec_first;   // the burst's first batch (A/B arm)
     const bool conv = ((final && h->spec_final) || first) && !h->batch_spec && h->sets[h->pend[0].set].byz != nullptr &&
                       ((h->batch_p.thr16 == 0 && h->batch_p.crash_on == 0) || h->spec_lossy);   // lossless (launch)
