@@ -454,7 +454,9 @@ struct bftsim {
     uint64_t chain_wave_max = 0;
     // one lane per instance from this many instances per launch (kern_fast.hip bft_hash_chain_lane_kernel: fewer
     // instructions per header, longer chains; BFTSIM_TESTING + BFTSIM_CHAIN_LANE_MIN overrides)
-    uint64_t chain_lane_min = 8192;   // 8,192: lanes 1.62e9 vs predicted pairs 1.55e9; 4,096: 1.12e9 vs 1.47e9 (r06/ab_mid)
+    // predicted lanes against predicted lane pairs (r06/ab_mid, ab_lane_min): 8,192 1.69e9-1.70e9 vs 1.47e9-1.49e9;
+    // 6,144 1.52e9-1.59e9 vs 1.45e9-1.46e9; 5,120 1.36e9 vs 1.41e9; 4,096 1.31e9 vs 1.41e9
+    uint64_t chain_lane_min = 6144;
     // persistent lane-chain waves per dispatch, 0: a wave per 64 instances (BFTSIM_TESTING + BFTSIM_CHAIN_GRID; an A/B
     // arm: capping the chain waves so that the consensus kernels keep SIMD slots measured the same or slower)
     uint32_t chain_grid = 0;
